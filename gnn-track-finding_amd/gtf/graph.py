@@ -1,0 +1,466 @@
+"""Packed CSR layout of a list of reference subgraphs (host side).
+
+The reference keeps every subgraph as a networkx ``DiGraph`` whose nodes carry
+attribute dicts (SURVEY.md §8b "Node attributes"). The hot path needs them as
+flat structure-of-arrays so one HIP launch can cover every subgraph of every
+event. ``pack`` turns ``list[nx.DiGraph]`` into a :class:`TrackGraph`;
+``unpack`` writes the results back into the same graph objects with the
+reference's attribute schema (key order, aliasing and mutation semantics of
+src/extrapolate/extrapolate_merged_states.py:375-385,443-447,
+src/clustering/clustering.py:291-293, src/utilities/helper.py:30-225).
+
+Layout (see DESIGN.md "Data layout in HBM"):
+
+* nodes are numbered 0..N-1 in subgraph-list order, then in each subgraph's
+  node-iteration order (the order every reference stage loops in);
+* a node's *slots* are the union of its in-edge senders and the keys of its
+  ``track_state_estimates`` (TSE) / ``updated_track_states`` (UTS) dicts,
+  sorted by sender node index (orphan keys whose node left the subgraph go
+  last). Slot ``k`` of node ``v`` describes the directed edge
+  ``slot_src[k] -> v`` and the state ``v`` holds for that sender;
+* the dict order of a state dict is carried explicitly as a per-slot rank
+  (``tse_rank`` / ``uts_rank``; -1 = key absent) -- never re-sorted;
+* per-edge flags (``activated``, edge ``mixture_weight``) are stored per slot,
+  i.e. receiver-major. The out-view ``out_ptr``/``out_slot`` lists each
+  node's successors in ``G.neighbors`` order (the order message passing walks
+  them, extrapolate_merged_states.py:430).
+
+Every state covariance on the path is block diagonal after the reference's
+aliasing (helper.py:422-425, extrapolate_merged_states.py:362-365), so a
+covariance is stored as 5 numbers ``c00 c01 c10 c11 c22``.
+"""
+from __future__ import annotations
+
+import dataclasses
+from typing import List, Optional
+
+import numpy as np
+
+F64 = np.float64
+NAN = float("nan")
+
+# covariance packing order
+COV5 = ((0, 0), (0, 1), (1, 0), (1, 1), (2, 2))
+
+
+def cov5_from_mat(m) -> np.ndarray:
+    m = np.asarray(m, dtype=F64)
+    return np.array([m[0, 0], m[0, 1], m[1, 0], m[1, 1], m[2, 2]], dtype=F64)
+
+
+def mat_from_cov5(c) -> np.ndarray:
+    m = np.zeros((3, 3), dtype=F64)
+    m[0, 0], m[0, 1], m[1, 0], m[1, 1], m[2, 2] = c[0], c[1], c[2], c[3], c[4]
+    return m
+
+
+# --------------------------------------------------------------------------
+# container
+# --------------------------------------------------------------------------
+NODE_FIELDS = {
+    # name: (dtype, trailing shape, fill)
+    "gnn": (F64, (4,), NAN),          # GNN_Measurement x, y, z, r
+    "xyzr": (F64, (4,), NAN),         # node attr 'xyzr' (clustering reads this one)
+    "layer": (F64, (), NAN),          # 'in_volume_layer_id'
+    "has_merged": (np.uint8, (), 0),
+    "merged_state": (F64, (3,), NAN),
+    "merged_cov": (F64, (5,), NAN),
+    "merged_prior": (F64, (), NAN),
+    "has_tse": (np.uint8, (), 0),     # node has a 'track_state_estimates' key
+    "has_uts": (np.uint8, (), 0),     # node has an 'updated_track_states' key
+    "degree": (np.int32, (), -1),
+    "tag": (np.int64, (), -1),        # tags[-1]
+    "node_id": (np.int64, (), -1),    # original networkx node id
+    "sub_id": (np.int32, (), -1),     # index of the subgraph the node came from
+}
+
+SLOT_FIELDS = {
+    "slot_src": (np.int32, (), -1),   # sender node index, -1 = orphan key
+    "slot_key": (np.int64, (), -1),   # sender's original id (dict key)
+    "is_edge": (np.uint8, (), 0),     # edge sender -> receiver exists
+    "rev_edge": (np.uint8, (), 0),    # edge receiver -> sender exists
+    "act": (np.uint8, (), 0),         # edge attr 'activated'
+    "edge_mw": (F64, (), NAN),        # edge attr 'mixture_weight' (NaN = absent)
+    "send_mw": (F64, (), NAN),        # sender's TSE[receiver]['mixture_weight']
+    # track_state_estimates entry (at the receiver, keyed by sender)
+    "tse_rank": (np.int32, (), -1),
+    "tse_sv": (F64, (3,), NAN),       # edge_state_vector a, b, c
+    "tse_tau": (F64, (), NAN),        # joint_vector[2]
+    "tse_cov": (F64, (5,), NAN),
+    "tse_xyzr": (F64, (4,), NAN),
+    "tse_prior": (F64, (), NAN),
+    "tse_mw": (F64, (), NAN),
+    "tse_theta": (F64, (3,), NAN),    # theta, theta2, variance_theta
+    "tse_var_ms": (F64, (), NAN),     # var_ms_node
+    # updated_track_states entry
+    "uts_rank": (np.int32, (), -1),
+    "uts_sv": (F64, (3,), NAN),
+    "uts_tau": (F64, (), NAN),
+    "uts_cov": (F64, (5,), NAN),
+    "uts_xyzr": (F64, (4,), NAN),
+    "uts_lik": (F64, (), NAN),
+    "uts_mw": (F64, (), NAN),
+    "uts_prior": (F64, (), NAN),
+    "uts_lr": (F64, (), NAN),         # lr_layer_norm (int in the reference)
+    "uts_side": (np.int8, (), -1),    # 0 left, 1 right, -1 absent
+    "uts_fresh": (np.uint8, (), 0),   # entry (re)created by the last message passing
+}
+
+
+@dataclasses.dataclass
+class TrackGraph:
+    """Structure-of-arrays CSR view of a list of subgraphs (or events)."""
+
+    n_nodes: int
+    n_slots: int
+    slot_ptr: np.ndarray          # int32 [N+1]
+    out_ptr: np.ndarray           # int32 [N+1]
+    out_slot: np.ndarray          # int32 [E] slot index of each out-edge, successor order
+    node: dict                    # name -> array [N, ...]
+    slot: dict                    # name -> array [S, ...]
+    n_subgraphs: int = 1
+
+    @property
+    def n_edges(self) -> int:
+        return int(self.out_slot.shape[0])
+
+    def copy(self) -> "TrackGraph":
+        return TrackGraph(self.n_nodes, self.n_slots, self.slot_ptr.copy(), self.out_ptr.copy(),
+                          self.out_slot.copy(), {k: v.copy() for k, v in self.node.items()},
+                          {k: v.copy() for k, v in self.slot.items()}, self.n_subgraphs)
+
+    # convenience accessors -------------------------------------------------
+    def __getattr__(self, name):
+        d = self.__dict__
+        if "node" in d and name in d["node"]:
+            return d["node"][name]
+        if "slot" in d and name in d["slot"]:
+            return d["slot"][name]
+        raise AttributeError(name)
+
+    def slot_dst(self) -> np.ndarray:
+        """receiver node index of every slot"""
+        return np.repeat(np.arange(self.n_nodes, dtype=np.int32), np.diff(self.slot_ptr))
+
+
+def empty_arrays(fields: dict, n: int) -> dict:
+    out = {}
+    for name, (dt, shape, fill) in fields.items():
+        out[name] = np.full((n,) + shape, fill, dtype=dt)
+    return out
+
+
+def check_layout(g: TrackGraph) -> None:
+    """Validate every index the HIP kernels will dereference (host-side guard)."""
+    N, S = g.n_nodes, g.n_slots
+    sp, op = g.slot_ptr, g.out_ptr
+    assert sp.shape == (N + 1,) and op.shape == (N + 1,)
+    assert sp[0] == 0 and sp[-1] == S and np.all(np.diff(sp) >= 0)
+    assert op[0] == 0 and op[-1] == g.n_edges and np.all(np.diff(op) >= 0)
+    src = g.slot["slot_src"]
+    assert src.shape == (S,)
+    assert np.all((src >= -1) & (src < N))
+    assert np.all(g.slot["is_edge"][src < 0] == 0), "orphan slot flagged as an edge"
+    if g.n_edges:
+        os_ = g.out_slot
+        assert np.all((os_ >= 0) & (os_ < S))
+        assert np.all(g.slot["is_edge"][os_] == 1)
+        # every out-edge must point at a slot whose sender is the source node
+        owner = np.repeat(np.arange(N, dtype=np.int32), np.diff(op))
+        assert np.array_equal(src[os_], owner), "out_slot does not match slot_src"
+    for name, (dt, shape, _) in NODE_FIELDS.items():
+        assert g.node[name].shape == (N,) + shape and g.node[name].dtype == dt, name
+    for name, (dt, shape, _) in SLOT_FIELDS.items():
+        assert g.slot[name].shape == (S,) + shape and g.slot[name].dtype == dt, name
+
+
+# --------------------------------------------------------------------------
+# pack: list[nx.DiGraph] -> TrackGraph
+# --------------------------------------------------------------------------
+def _f(x) -> float:
+    return float(x)
+
+
+def pack(subgraphs, like: Optional[TrackGraph] = None) -> TrackGraph:
+    """Pack reference subgraphs (list of ``nx.DiGraph``) into a TrackGraph.
+
+    ``like``: reuse the slot layout of an earlier pack of the same nodes (a
+    stage that removes state keys, e.g. remove_state_metadata, then still
+    packs onto the slots of its input so arrays compare index for index).
+    """
+    # global node numbering ------------------------------------------------
+    node_ids: List = []
+    sub_of: List[int] = []
+    local_maps: List[dict] = []
+    for si, G in enumerate(subgraphs):
+        m = {}
+        for n in G.nodes:
+            m[n] = len(node_ids)
+            node_ids.append(n)
+            sub_of.append(si)
+        local_maps.append(m)
+    N = len(node_ids)
+    nodeA = empty_arrays(NODE_FIELDS, N)
+
+    slot_rows = []           # per node: list of (sender_idx or -1, key)
+    slot_ptr = np.zeros(N + 1, dtype=np.int64)
+    gi = 0
+    for si, G in enumerate(subgraphs):
+        lm = local_maps[si]
+        for v in G.nodes:
+            attr = G.nodes[v]
+            keys = []
+            seen = set()
+            for u in G.predecessors(v):
+                if u not in seen:
+                    seen.add(u)
+                    keys.append(u)
+            for dk in ("track_state_estimates", "updated_track_states"):
+                d = attr.get(dk)
+                if d is not None:
+                    for u in d.keys():
+                        if u not in seen:
+                            seen.add(u)
+                            keys.append(u)
+            if like is not None:
+                lo_, hi_ = int(like.slot_ptr[gi]), int(like.slot_ptr[gi + 1])
+                row = [(int(like.slot["slot_src"][k]), int(like.slot["slot_key"][k])) for k in range(lo_, hi_)]
+                rk = set(r[1] for r in row)
+                assert all(int(u) in rk for u in keys), "pack(like=...): new state key not in layout"
+            else:
+                inside = sorted((lm[u], u) for u in keys if u in lm)
+                orphans = [(-1, u) for u in keys if u not in lm]
+                row = inside + orphans
+            slot_rows.append(row)
+            slot_ptr[gi + 1] = slot_ptr[gi] + len(row)
+            gi += 1
+    S = int(slot_ptr[-1])
+    slotA = empty_arrays(SLOT_FIELDS, S)
+
+    # lookup (receiver idx, sender key) -> slot
+    slot_of = {}
+    for vi, row in enumerate(slot_rows):
+        base = int(slot_ptr[vi])
+        for j, (ui, key) in enumerate(row):
+            slot_of[(vi, key)] = base + j
+            slot_of[(vi, int(key))] = base + j
+            slotA["slot_src"][base + j] = ui
+            slotA["slot_key"][base + j] = int(key)
+
+    out_ptr = np.zeros(N + 1, dtype=np.int64)
+    out_slot = []
+
+    gi = 0
+    for si, G in enumerate(subgraphs):
+        lm = local_maps[si]
+        for v in G.nodes:
+            attr = G.nodes[v]
+            vi = gi
+            gm = attr.get("GNN_Measurement")
+            if gm is not None:
+                nodeA["gnn"][vi] = (_f(gm.x), _f(gm.y), _f(gm.z), _f(gm.r))
+            if "xyzr" in attr:
+                nodeA["xyzr"][vi] = [_f(c) for c in attr["xyzr"]]
+            if "in_volume_layer_id" in attr:
+                nodeA["layer"][vi] = _f(attr["in_volume_layer_id"])
+            if "merged_state" in attr:
+                nodeA["has_merged"][vi] = 1
+                nodeA["merged_state"][vi] = np.asarray(attr["merged_state"], dtype=F64)
+                nodeA["merged_cov"][vi] = cov5_from_mat(attr["merged_cov"])
+                nodeA["merged_prior"][vi] = _f(attr.get("merged_prior", NAN))
+            if "degree" in attr:
+                nodeA["degree"][vi] = int(attr["degree"])
+            tags = attr.get("tags")
+            nodeA["tag"][vi] = int(tags[-1]) if tags else int(v)
+            nodeA["node_id"][vi] = int(v)
+            nodeA["sub_id"][vi] = si
+
+            # in-edges
+            for u in G.predecessors(v):
+                k = slot_of[(vi, u)]
+                slotA["is_edge"][k] = 1
+                ed = G[u][v]
+                slotA["act"][k] = int(ed.get("activated", 1))
+                if "mixture_weight" in ed:
+                    slotA["edge_mw"][k] = _f(ed["mixture_weight"])
+                # sender's TSE entry keyed by this receiver (read by message passing)
+                tse_u = G.nodes[u].get("track_state_estimates")
+                if tse_u is not None and v in tse_u and "mixture_weight" in tse_u[v]:
+                    slotA["send_mw"][k] = _f(tse_u[v]["mixture_weight"])
+            for ui_key in [r[1] for r in slot_rows[vi]]:
+                if ui_key in lm:
+                    k = slot_of[(vi, ui_key)]
+                    slotA["rev_edge"][k] = 1 if G.has_edge(v, ui_key) else 0
+
+            d = attr.get("track_state_estimates")
+            if d is not None:
+                nodeA["has_tse"][vi] = 1
+                for rank, (u, st) in enumerate(d.items()):
+                    k = slot_of[(vi, u)]
+                    slotA["tse_rank"][k] = rank
+                    _fill_state(slotA, "tse", k, st)
+                    if "theta" in st:
+                        slotA["tse_theta"][k] = (_f(st["theta"]), _f(st["theta2"]), _f(st["variance_theta"]))
+                    if "var_ms_node" in st:
+                        slotA["tse_var_ms"][k] = _f(st["var_ms_node"])
+            d = attr.get("updated_track_states")
+            if d is not None:
+                nodeA["has_uts"][vi] = 1
+                for rank, (u, st) in enumerate(d.items()):
+                    k = slot_of[(vi, u)]
+                    slotA["uts_rank"][k] = rank
+                    _fill_state(slotA, "uts", k, st)
+                    if "likelihood" in st:
+                        slotA["uts_lik"][k] = _f(st["likelihood"])
+                    if "lr_layer_norm" in st:
+                        slotA["uts_lr"][k] = _f(st["lr_layer_norm"])
+                    if "side" in st:
+                        slotA["uts_side"][k] = 0 if st["side"] == "left" else 1
+
+            # out-edges in successor order
+            for w in G.successors(v):
+                out_slot.append(slot_of[(lm[w], v)])
+            out_ptr[vi + 1] = out_ptr[vi] + G.out_degree(v)
+            gi += 1
+
+    g = TrackGraph(N, S, slot_ptr.astype(np.int32), out_ptr.astype(np.int32),
+                   np.asarray(out_slot, dtype=np.int32), nodeA, slotA, len(subgraphs))
+    check_layout(g)
+    return g
+
+
+def _fill_state(slotA, pfx, k, st):
+    if "edge_state_vector" in st:
+        slotA[pfx + "_sv"][k] = np.asarray(st["edge_state_vector"], dtype=F64)[:3]
+    if "joint_vector" in st:
+        slotA[pfx + "_tau"][k] = _f(st["joint_vector"][2])
+    cov = st.get("joint_vector_covariance", st.get("edge_covariance"))
+    if cov is not None:
+        slotA[pfx + "_cov"][k] = cov5_from_mat(cov)
+    if "xyzr" in st:
+        slotA[pfx + "_xyzr"][k] = [_f(c) for c in st["xyzr"]]
+    if "prior" in st:
+        slotA[pfx + "_prior"][k] = _f(st["prior"])
+    if "mixture_weight" in st:
+        slotA[pfx + "_mw"][k] = _f(st["mixture_weight"])
+
+
+# --------------------------------------------------------------------------
+# unpack: write TrackGraph results back into the reference graphs
+# --------------------------------------------------------------------------
+def unpack(g: TrackGraph, subgraphs, *, states=("tse", "uts"), merged=True,
+           degree=True, edges=True) -> None:
+    """Write packed results back into ``subgraphs`` (the objects given to pack).
+
+    Mirrors the reference's in-place mutations: activation and edge mixture
+    weight per directed edge, node ``degree``, ``merged_state/cov/prior``,
+    and the state dicts rebuilt in rank (dict) order. A freshly created UTS
+    entry gets the key order of extrapolate_merged_states.py:375-385 and
+    ``edge_covariance is joint_vector_covariance`` (aliasing, :362-365).
+    """
+    sp = g.slot_ptr
+    gi = 0
+    for si, G in enumerate(subgraphs):
+        for v in G.nodes:
+            vi = gi
+            gi += 1
+            attr = G.nodes[v]
+            lo, hi = int(sp[vi]), int(sp[vi + 1])
+            if edges:
+                for k in range(lo, hi):
+                    if g.slot["is_edge"][k]:
+                        u = _key(G, g.slot["slot_key"][k])
+                        ed = G[u][v]
+                        ed["activated"] = int(g.slot["act"][k])
+                        mw = g.slot["edge_mw"][k]
+                        if not np.isnan(mw):
+                            ed["mixture_weight"] = mw
+            if degree and g.node["degree"][vi] >= 0:
+                attr["degree"] = int(g.node["degree"][vi])
+            if merged and g.node["has_merged"][vi]:
+                attr["merged_state"] = g.node["merged_state"][vi].copy()
+                attr["merged_cov"] = mat_from_cov5(g.node["merged_cov"][vi])
+                attr["merged_prior"] = g.node["merged_prior"][vi]
+            if "tse" in states and g.node["has_tse"][vi]:
+                _write_dict(g, "tse", attr, "track_state_estimates", lo, hi, G)
+            if "uts" in states and g.node["has_uts"][vi]:
+                _write_dict(g, "uts", attr, "updated_track_states", lo, hi, G)
+
+
+def _key(G, key):
+    # node ids may be python ints or numpy ints; compare by value
+    return key if key in G else int(key)
+
+
+def _write_dict(g, pfx, attr, dname, lo, hi, G):
+    S = g.slot
+    old = attr.get(dname) or {}
+    ranked = sorted((int(S[pfx + "_rank"][k]), k) for k in range(lo, hi) if S[pfx + "_rank"][k] >= 0)
+    new = {}
+    for _, k in ranked:
+        key = int(S["slot_key"][k])
+        okey = next((ok for ok in old.keys() if ok == key), key)
+        st = old.get(okey)
+        fresh = pfx == "uts" and (st is None or bool(S["uts_fresh"][k]))
+        if st is None or fresh:
+            st = _fresh_uts(g, k) if pfx == "uts" else {}
+        else:
+            _update_state(g, pfx, k, st)
+        new[okey] = st
+    attr[dname] = new
+
+
+def _fresh_uts(g, k) -> dict:
+    S = g.slot
+    xyzr = tuple(S["uts_xyzr"][k])
+    sv = S["uts_sv"][k].copy()
+    cov = mat_from_cov5(S["uts_cov"][k])
+    st = {
+        "xy": (xyzr[0], xyzr[1]),
+        "zr": (xyzr[2], xyzr[3]),
+        "xyzr": xyzr,
+        "edge_state_vector": sv,
+        "edge_covariance": cov,
+        "joint_vector": [sv[0], sv[1], S["uts_tau"][k]],
+        "joint_vector_covariance": cov,
+        "likelihood": S["uts_lik"][k],
+        "mixture_weight": S["uts_mw"][k],
+    }
+    _update_state(g, "uts", k, st)
+    return st
+
+
+def _update_state(g, pfx, k, st):
+    S = g.slot
+    if not np.isnan(S[pfx + "_prior"][k]):
+        st["prior"] = S[pfx + "_prior"][k]
+    if not np.isnan(S[pfx + "_mw"][k]):
+        st["mixture_weight"] = S[pfx + "_mw"][k]
+    if pfx == "uts":
+        if S["uts_side"][k] >= 0:
+            st["side"] = "left" if S["uts_side"][k] == 0 else "right"
+        if not np.isnan(S["uts_lr"][k]):
+            st["lr_layer_norm"] = int(S["uts_lr"][k])
+
+
+def concat(graphs: List[TrackGraph]) -> TrackGraph:
+    """Fuse several TrackGraphs (events) into one CSR with node-index offsets."""
+    node = {k: np.concatenate([g.node[k] for g in graphs]) for k in NODE_FIELDS}
+    slot = {k: np.concatenate([g.slot[k] for g in graphs]) for k in SLOT_FIELDS}
+    noff = np.cumsum([0] + [g.n_nodes for g in graphs])
+    soff = np.cumsum([0] + [g.n_slots for g in graphs])
+    eoff = np.cumsum([0] + [g.n_edges for g in graphs])
+    sub_off = np.cumsum([0] + [g.n_subgraphs for g in graphs])
+    slot_ptr = np.concatenate([[0]] + [g.slot_ptr[1:] + soff[i] for i, g in enumerate(graphs)])
+    out_ptr = np.concatenate([[0]] + [g.out_ptr[1:] + eoff[i] for i, g in enumerate(graphs)])
+    out_slot = np.concatenate([g.out_slot + soff[i] for i, g in enumerate(graphs)])
+    src = []
+    for i, g in enumerate(graphs):
+        s = g.slot["slot_src"].astype(np.int64)
+        src.append(np.where(s >= 0, s + noff[i], -1))
+    slot["slot_src"] = np.concatenate(src).astype(np.int32)
+    node["sub_id"] = np.concatenate([g.node["sub_id"] + sub_off[i] for i, g in enumerate(graphs)]).astype(np.int32)
+    out = TrackGraph(int(noff[-1]), int(soff[-1]), slot_ptr.astype(np.int32), out_ptr.astype(np.int32),
+                     out_slot.astype(np.int32), node, slot, int(sub_off[-1]))
+    check_layout(out)
+    return out

@@ -1,0 +1,608 @@
+"""CPU oracle: NumPy restatement of the reference's hot-path algorithm.
+
+TEST INFRASTRUCTURE ONLY. Nothing under ``oracle/`` is part of the product:
+only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s
+``cpu_baseline`` leg may import it, and only as the checker (or, in bench.py,
+as the timed CPU baseline). The product path (``gtf``) never falls back to it.
+
+Every function restates one reference function, op for op with the same NumPy
+calls (``np.linalg.inv``, ``dot``, filterpy's predict/update sequence), on the
+packed :class:`gtf.graph.TrackGraph` layout instead of networkx dicts, so its
+results match the reference bit for bit on the same inputs. Citations are
+``file:line`` in ``/root/reference``.
+
+Pinning (see DESIGN.md "Oracle"): the restatement is checked against
+``tests/golden/*.npz`` -- fixtures produced by running the reference's own
+functions on its committed event data (tests/golden/make_golden.py) -- and the
+parabolic-model KL (a17) against the reference's committed training CSV
+(known-answer test). filterpy (third-party, unpinned, not vendored; SURVEY
+§8c) is restated from its 1.4.5 release; parity for that piece is pinned only
+to that restatement.
+"""
+from __future__ import annotations
+
+import math
+from math import atan2
+
+import numpy as np
+
+from gtf.graph import TrackGraph, mat_from_cov5, cov5_from_mat  # container only
+
+
+class ReferenceError_(ValueError):
+    """Raised where the reference itself raises (KeyError / ValueError paths)."""
+
+
+# ---------------------------------------------------------------------------
+# helpers over the packed layout
+# ---------------------------------------------------------------------------
+def _dict_order(g: TrackGraph, pfx: str, v: int):
+    """slots of node v holding a key of the given state dict, in dict order"""
+    lo, hi = int(g.slot_ptr[v]), int(g.slot_ptr[v + 1])
+    r = g.slot[pfx + "_rank"][lo:hi]
+    ks = [lo + j for j in range(hi - lo) if r[j] >= 0]
+    ks.sort(key=lambda k: int(g.slot[pfx + "_rank"][k]))
+    return ks
+
+
+def _has(g, pfx, v):
+    return bool(g.node["has_" + pfx][v])
+
+
+def _edge_active(g, k):
+    return bool(g.slot["is_edge"][k]) and g.slot["act"][k] == 1
+
+
+# ---------------------------------------------------------------------------
+# filterpy 1.4.5 KalmanFilter restated (third-party; not in /root/reference)
+# call sites: src/extrapolate/extrapolate_merged_states.py:307-323
+# ---------------------------------------------------------------------------
+def _kf_predict_update(x, P, F, H, R, Q, z):
+    dot = np.dot
+    # predict(): x = Fx ; P = alpha_sq * FPF' + Q  (alpha_sq = 1.0)
+    x = dot(F, x)
+    P = 1.0 * dot(dot(F, P), F.T) + Q
+    # update(z): reshape_z(z, dim_z=1, ndim=x.ndim=1) -> shape (1,)
+    z = np.atleast_2d(z)
+    if z.shape[1] == 1:
+        z = z.T
+    z = z[:, 0]
+    y = z - dot(H, x)
+    PHT = dot(P, H.T)
+    S = dot(H, PHT) + R
+    SI = np.linalg.inv(S)
+    K = dot(PHT, SI)
+    x = x + dot(K, y)
+    I_KH = np.eye(3) - dot(K, H)
+    P = dot(dot(I_KH, P), I_KH.T) + dot(dot(K, R), K.T)
+    return x.copy(), P.copy()
+
+
+# ---------------------------------------------------------------------------
+# a7: extrapolate_validate  (extrapolate_merged_states.py:26-402)
+# ---------------------------------------------------------------------------
+def extrapolate_validate(node_gnn, nb_gnn, merged_state, merged_cov, chi2_cut, sigma0xy,
+                         sigma0rz, sigma0rz2, endcap_boundary):
+    """Returns (accepted, payload, chi2). ``merged_cov`` is mutated in place
+    (merged_cov[1,1] += var_ms, :127-128) exactly like the reference."""
+    node_x, node_y, node_z, node_r = node_gnn
+    neighbour_x, neighbour_y, neighbour_z, neighbour_r = nb_gnn
+    angle_of_rotation_C = atan2(node_y, node_x)                                   # :41
+    x_A = (neighbour_x - node_x) * np.cos(angle_of_rotation_C) + (neighbour_y - node_y) * np.sin(angle_of_rotation_C)   # :52
+    y_A = -(neighbour_x - node_x) * np.sin(angle_of_rotation_C) + (neighbour_y - node_y) * np.cos(angle_of_rotation_C)  # :53
+    a, b, c = merged_state[0], merged_state[1], merged_state[2]                   # :58
+    phi = atan2((node_x * neighbour_y) - (node_y * neighbour_x), (node_x * neighbour_x) + (node_y * neighbour_y))  # :59
+    x_prime = x_A + (c * np.sin(phi))                                             # :63
+    Vx_prime = np.cos(phi) + (b * np.sin(phi))
+    Ax_prime = a * np.sin(phi)
+    s_star = (- x_prime * ((2 * Vx_prime**2) + (Ax_prime * x_prime))) / (2 * Vx_prime**3)   # :68
+    # :71-79 (y_c, b_c, a_c are computed by the reference but never used)
+    numer = x_A + c * np.sin(phi)                                                 # :82
+    denom = np.cos(phi) + b * np.sin(phi)
+    ds_da = - (np.sin(phi) * numer**2) / denom**3
+    ds_db = ((np.sin(phi) * numer) * (1 + ((3 * a * np.sin(phi) * numer) / denom**2))) / denom**2
+    ds_dc = - np.sin(phi) * (1 + ((2 * a * np.sin(phi) * numer) / denom**2)) / denom
+    denom = np.cos(phi) + ((2 * a + b) * np.sin(phi))                             # :89
+    da_da = (1 / denom**3) * (1 - ((6 * a * np.sin(phi)) * (s_star + a * ds_da) / denom))
+    da_db = (-3 * a * np.sin(phi) * ((2 * a * ds_db) + 1)) / denom**4
+    da_dc = (-6 * np.sin(phi) * ds_dc * a**2) / denom**4
+    denom = np.cos(phi) + ((2 * a * s_star + b) * np.sin(phi))                    # :95
+    bracket = np.cos(phi) - ((np.sin(phi) * (-np.sin(phi) + ((2 * a * s_star + b) * np.cos(phi)))) / denom)
+    db_da = (2 * (s_star + a * ds_da) * bracket) / denom
+    db_db = ((1 + (2 * a * ds_da)) * bracket) / denom
+    db_dc = (2 * a * ds_dc * bracket) / denom
+    bracket = (np.cos(phi) * (2 * a + b)) - np.sin(phi)                           # :102
+    dc_da = (ds_da * bracket) + (s_star**2 * np.cos(phi))
+    dc_db = (ds_db * bracket) + (s_star * np.cos(phi))
+    dc_dc = (ds_dc * bracket) + np.cos(phi)
+    F = np.array([[da_da, da_db, da_dc],
+                  [db_da, db_db, db_dc],
+                  [dc_da, dc_db, dc_dc]])                                          # :108
+    dr = neighbour_r - node_r                                                     # :114
+    dz = neighbour_z - node_z
+    hyp = np.sqrt(dr**2 + dz**2)
+    sin_t = np.abs(dr) / hyp
+    kappa = (2 * a) / (1 + ((2 * a * neighbour_x) + b)**2)**1.5
+    var_ms = sin_t * ((13.6 * 1e-3 * np.sqrt(0.02) * kappa) / 0.3)**2              # :120
+    if np.abs(node_z) >= endcap_boundary:
+        tan_t = np.abs(dr) / np.abs(dz)
+        var_ms = var_ms * tan_t
+    merged_cov[1, 1] += var_ms                                                    # :128 (in place)
+    extrp_state = F.dot(merged_state)
+    extrp_cov = F.dot(merged_cov).dot(F.T)
+    H = np.array([[0., 0., 1.]])
+    residual = .0 - H.dot(extrp_state)                                           # :137
+    S = H.dot(extrp_cov).dot(H.T) + sigma0xy**2
+    inv_S = np.linalg.inv(S)
+    chi2 = residual.T.dot(inv_S).dot(residual)                                   # :140
+    # :143-295 rz-plane chi2 / CSV appends: diagnostics only, no effect on outputs
+    if chi2 <= chi2_cut:                                                          # :298
+        factor = 2 * math.pi * np.abs(S)
+        norm_factor = math.pow(float(factor[0, 0]), -0.5)
+        likelihood = norm_factor * np.exp(-0.5 * chi2)                            # :304
+        Q = np.array([[0., 0., 0.], [0., var_ms, 0.], [0., 0., 0.]])
+        updated_state, updated_cov = _kf_predict_update(extrp_state, extrp_cov, F, H,
+                                                        sigma0xy**2, Q, .0)       # :307-323
+        tau = dz / dr                                                             # :326
+        sigma_r, sigma_z = sigma0rz, sigma0rz2
+        if np.abs(node_z) >= endcap_boundary:
+            sigma_z, sigma_r = sigma0rz, sigma0rz2
+        sigma_r_neighbour, sigma_z_neighbour = sigma0rz, sigma0rz2
+        if np.abs(neighbour_z) >= endcap_boundary:
+            sigma_z_neighbour, sigma_r_neighbour = sigma0rz, sigma0rz2
+        J = np.array([1 / dr, -1 / dr, - dz / dr**2, dz / dr**2])                  # :344-348
+        S2 = np.array([[sigma_z**2, 0, 0, 0],
+                       [0, sigma_z_neighbour**2, 0, 0],
+                       [0, 0, sigma_r**2, 0],
+                       [0, 0, 0, sigma_r_neighbour**2]])
+        variance_tau = J.dot(S2).dot(J.T)                                         # :357-358
+        jcov = updated_cov                                                        # alias :362
+        jcov[:, 2] = 0.0
+        jcov[2, :] = 0.0
+        jcov[2, 2] = variance_tau + var_ms
+        return True, dict(sv=updated_state, tau=tau, cov=jcov, lik=likelihood), chi2
+    return False, None, chi2
+
+
+# ---------------------------------------------------------------------------
+# a6: message_passing  (extrapolate_merged_states.py:406-451)
+# ---------------------------------------------------------------------------
+def message_passing(g: TrackGraph, p) -> dict:
+    N, S = g.node, g.slot
+    dst = g.slot_dst()
+    S["uts_fresh"][:] = 0
+    next_rank = np.full(g.n_nodes, 0, dtype=np.int64)
+    for v in range(g.n_nodes):
+        lo, hi = g.slot_ptr[v], g.slot_ptr[v + 1]
+        r = S["uts_rank"][lo:hi]
+        next_rank[v] = (int(r.max()) + 1) if (hi > lo and r.max() >= 0) else 0
+    chi2_all = np.full(g.n_slots, np.nan)
+    for u in range(g.n_nodes):                                                    # :419
+        if not N["has_merged"][u]:
+            continue
+        state = N["merged_state"][u].copy()
+        cov = mat_from_cov5(N["merged_cov"][u])                                   # stored array, mutated
+        for e in range(g.out_ptr[u], g.out_ptr[u + 1]):                           # :430 successors
+            k = int(g.out_slot[e])
+            if S["act"][k] != 1:                                                  # :431
+                continue
+            v = int(dst[k])
+            ok, res, chi2 = extrapolate_validate(N["gnn"][u], N["gnn"][v], state, cov, p.chi2_cut,
+                                                 p.sigma0xy, p.sigma0rz, p.sigma0rz2, p.endcap_boundary)
+            chi2_all[k] = chi2
+            if ok:                                                                # :441-447
+                if not N["has_uts"][v]:
+                    N["has_uts"][v] = 1
+                if S["uts_rank"][k] < 0:
+                    S["uts_rank"][k] = next_rank[v]
+                    next_rank[v] += 1
+                S["uts_fresh"][k] = 1
+                S["uts_sv"][k] = res["sv"]
+                S["uts_tau"][k] = res["tau"]
+                S["uts_cov"][k] = cov5_from_mat(res["cov"])
+                S["uts_xyzr"][k] = N["gnn"][u]                                    # sender coords :377
+                S["uts_lik"][k] = res["lik"]
+                if np.isnan(S["send_mw"][k]):
+                    raise ReferenceError_("KeyError: sender TSE has no entry for receiver (:384)")
+                S["uts_mw"][k] = S["send_mw"][k]                                  # :384
+                S["uts_prior"][k] = np.nan                                        # fresh dict: no prior yet
+                S["uts_lr"][k] = np.nan
+                S["uts_side"][k] = -1
+            else:
+                S["act"][k] = 0                                                   # :393
+        N["merged_cov"][u] = cov5_from_mat(cov)                                   # in-place mutation persisted
+    return {"chi2": chi2_all}
+
+
+# ---------------------------------------------------------------------------
+# a3 / a4 / a5  (helper.py:30-96)
+# ---------------------------------------------------------------------------
+def compute_prior_probabilities(g: TrackGraph, pfx: str) -> None:                # helper.py:30-63
+    S = g.slot
+    for v in range(g.n_nodes):
+        if not _has(g, pfx, v):
+            continue
+        groups = {}
+        for k in _dict_order(g, pfx, v):
+            if _edge_active(g, k):
+                layer = g.node["layer"][S["slot_src"][k]]
+                groups.setdefault(layer, []).append(k)
+        for ks in groups.values():
+            prior = 1 / len(ks)
+            for k in ks:
+                S[pfx + "_prior"][k] = prior
+
+
+def compute_mixture_weights(g: TrackGraph, pfx: str) -> None:                    # helper.py:76-96
+    for v in range(g.n_nodes):
+        if not _has(g, pfx, v):
+            continue
+        ks = _dict_order(g, pfx, v)
+        if not ks:
+            # single-node subgraphs are skipped (helper.py:79); elsewhere 1/0 raises (:90)
+            if np.count_nonzero(g.node["sub_id"] == g.node["sub_id"][v]) == 1:
+                continue
+            raise ReferenceError_("ZeroDivisionError: empty state dict (helper.py:90)")
+        mw = 1 / len(ks)
+        for k in ks:
+            g.slot[pfx + "_mw"][k] = mw
+
+
+def query_node_degree_in_edges(g: TrackGraph) -> None:                           # helper.py:67-73
+    S = g.slot
+    for v in range(g.n_nodes):
+        lo, hi = g.slot_ptr[v], g.slot_ptr[v + 1]
+        g.node["degree"][v] = int(np.sum((S["is_edge"][lo:hi] == 1) & (S["act"][lo:hi] == 1)))
+
+
+# ---------------------------------------------------------------------------
+# a9 + a10: calculate_side_norm_factor + reweight  (helper.py:99-225)
+# ---------------------------------------------------------------------------
+def reweight(g: TrackGraph, pfx: str = "uts", threshold: float = 0.1) -> None:
+    S, N = g.slot, g.node
+    for v in range(g.n_nodes):
+        if not _has(g, pfx, v):
+            continue
+        order = _dict_order(g, pfx, v)
+        # --- calculate_side_norm_factor (helper.py:99-139)
+        node_x = N["gnn"][v][0]
+        left, right, lc, rc = [], [], [], []
+        for k in order:
+            nx_ = S[pfx + "_xyzr"][k][0]
+            if _edge_active(g, k):
+                if nx_ < node_x:
+                    left.append(k); lc.append(nx_)
+                else:
+                    right.append(k); rc.append(nx_)
+        last = order[-1] if order else None           # stale loop variable (helper.py:131,138)
+        if (left or right) and not S["is_edge"][last]:
+            raise ReferenceError_("KeyError: stale neighbour_num has no edge (helper.py:131)")
+        left_norm = len(list(set(lc)))
+        for k in left:
+            S["uts_side"][k] = 0
+            S["uts_lr"][k] = 1
+            if S["act"][last] == 1:
+                S["uts_lr"][k] = left_norm
+        right_norm = len(list(set(rc)))
+        for k in right:
+            S["uts_side"][k] = 1
+            S["uts_lr"][k] = 1
+            if S["act"][last] == 1:
+                S["uts_lr"][k] = right_norm
+        # --- reweight (helper.py:164-200)
+        denom = 0
+        for k in order:
+            if _edge_active(g, k):
+                denom += (S[pfx + "_mw"][k] * S[pfx + "_lik"][k]) if pfx == "uts" else np.nan
+        for k in order:
+            if _edge_active(g, k):
+                w = (S["uts_mw"][k] * S["uts_lik"][k] * S["uts_prior"][k]) / denom
+                w /= S["uts_lr"][k]
+                S["uts_mw"][k] = w
+                S["edge_mw"][k] = w
+                S["act"][k] = 0 if w < threshold else 1
+
+
+# ---------------------------------------------------------------------------
+# a11: remove_state_metadata  (src/update/remove_state_metadata.py:29-53)
+# ---------------------------------------------------------------------------
+def prune_states(g: TrackGraph) -> None:
+    S = g.slot
+    for v in range(g.n_nodes):
+        pfx = "uts" if g.node["has_uts"][v] else "tse"
+        if not _has(g, pfx, v):
+            raise ReferenceError_("KeyError: node has no state dict (remove_state_metadata.py:39)")
+        for k in _dict_order(g, pfx, v):
+            if not S["rev_edge"][k]:          # sender not in graph.neighbors(node)
+                S[pfx + "_rank"][k] = -1
+
+
+def update_stage(g: TrackGraph, p) -> None:
+    prune_states(g)
+    compute_prior_probabilities(g, "tse")                                        # :51
+    compute_prior_probabilities(g, "uts")                                        # :52
+    reweight(g, "uts", p.reweight_threshold)                                     # :53
+
+
+def extrapolate_stage(g: TrackGraph, p) -> dict:
+    info = message_passing(g, p)                                                 # :552
+    compute_prior_probabilities(g, "uts")                                        # :554
+    reweight(g, "uts", p.reweight_threshold)
+    compute_prior_probabilities(g, "uts")                                        # :558
+    reweight(g, "uts", p.reweight_threshold)
+    query_node_degree_in_edges(g)                                                # :562-566
+    return info
+
+
+# ---------------------------------------------------------------------------
+# a12-a14: clustering  (src/clustering/clustering.py:11-124,181-327,372-373)
+# ---------------------------------------------------------------------------
+def mahalanobis_distance(mean1, cov1, mean2, cov2, node_coords, n1, n2, sigma0rz, sigma0rz2,
+                         endcap_boundary):                                        # clustering.py:11-78
+    residual = mean1[:2] - mean2[:2]
+    covariance_delta_ab = cov1[0:2, 0:2] + cov2[0:2, 0:2]
+    inv_covariance_delta_ab = np.linalg.inv(covariance_delta_ab)
+    distance1 = residual.T.dot(inv_covariance_delta_ab).dot(residual)
+    x_a, x_b, x_c = node_coords[0], n1[0], n2[0]
+    z_a, r_a = node_coords[2], node_coords[3]
+    z_b, r_b = n1[2], n1[3]
+    z_c, r_c = n2[2], n2[3]
+    j2 = 1 / (r_b - r_a)
+    j3 = -1 / (r_c - r_a)
+    j1 = - j3 - j2
+    j5 = -(z_b - z_a) / (r_b - r_a)**2
+    j6 = (z_c - z_a) / (r_c - r_a)**2
+    j4 = - j5 - j6
+    J = np.array([j1, j2, j3, j4, j5, j6])
+    sza = szb = szc = sigma0rz2
+    sra = srb = src = sigma0rz
+    if np.abs(x_a) >= endcap_boundary:
+        sza, sra = sigma0rz, sigma0rz2
+    if np.abs(x_b) >= endcap_boundary:
+        szb, srb = sigma0rz, sigma0rz2
+    if np.abs(x_c) >= endcap_boundary:
+        szc, src = sigma0rz, sigma0rz2
+    Sm = np.diag([sza**2, szb**2, szc**2, sra**2, srb**2, src**2]).astype(float)
+    cov_delta_tau = J.dot(Sm).dot(J.T)
+    inv_cov_delta_tau = 1 / cov_delta_tau
+    tau1 = (z_b - z_a) / (r_b - r_a)
+    tau2 = (z_c - z_a) / (r_c - r_a)
+    residual = tau1 - tau2
+    distance2 = residual**2 * inv_cov_delta_tau
+    return distance1 + distance2
+
+
+def mahalanobis_distance_updated(mean1, cov1, mean2, cov2, node_coords, n1, n2):
+    """a15: calculate_distance_between_updated_track_states.py:27-104 (hard-coded
+    sigmas, |x| >= 600 endcap test). Returns (chi2, <tau>, <theta>, dtheta)."""
+    residual = mean1[:2] - mean2[:2]
+    inv = np.linalg.inv(cov1[0:2, 0:2] + cov2[0:2, 0:2])
+    distance1 = residual.T.dot(inv).dot(residual)
+    x_a, x_b, x_c = node_coords[0], n1[0], n2[0]
+    z_a, r_a = node_coords[2], node_coords[3]
+    z_b, r_b = n1[2], n1[3]
+    z_c, r_c = n2[2], n2[3]
+    j2 = 1 / (r_b - r_a)
+    j3 = -1 / (r_c - r_a)
+    j1 = - j3 - j2
+    j5 = -(z_b - z_a) / (r_b - r_a)**2
+    j6 = (z_c - z_a) / (r_c - r_a)**2
+    j4 = - j5 - j6
+    J = np.array([j1, j2, j3, j4, j5, j6])
+    sza = szb = szc = 0.5
+    sra = srb = src = 0.1
+    if np.abs(x_a) >= 600.0:
+        sza, sra = 0.1, 0.5
+    if np.abs(x_b) >= 600.0:
+        szb, srb = 0.1, 0.5
+    if np.abs(x_c) >= 600.0:
+        szc, src = 0.1, 0.5
+    Sm = np.diag([sza**2, szb**2, szc**2, sra**2, srb**2, src**2]).astype(float)
+    inv_cov_delta_tau = 1 / J.dot(Sm).dot(J.T)
+    dz1, dr1 = z_b - z_a, r_b - r_a
+    dz2, dr2 = z_c - z_a, r_c - r_a
+    tau1, tau2 = dz1 / dr1, dz2 / dr2
+    theta1, theta2 = atan2(dz1, dr1), atan2(dz2, dr2)
+    distance2 = (tau1 - tau2)**2 * inv_cov_delta_tau
+    return distance1 + distance2, (tau1 + tau2) / 2, (theta1 + theta2) / 2, theta1 - theta2
+
+
+def KLDistance(mean1, cov1, mean2, cov2):                                        # clustering.py:90-94
+    inv1 = np.linalg.inv(cov1)
+    inv2 = np.linalg.inv(cov2)
+    trace = np.trace((cov1 - cov2) * (inv2 - inv1))
+    return trace + (mean1 - mean2).T.dot(inv1 + inv2).dot(mean1 - mean2)
+
+
+def merge_states(mean1, cov1, mean2, cov2):                                      # clustering.py:97-105
+    inv1 = np.linalg.inv(cov1)
+    inv2 = np.linalg.inv(cov2)
+    merged_cov = np.linalg.inv(inv1 + inv2)
+    merged_mean = inv1.dot(mean1) + inv2.dot(mean2)
+    merged_mean = merged_cov.dot(merged_mean)
+    return merged_mean, merged_cov
+
+
+def get_smallest_dist_idx(distances):                                            # clustering.py:114-124
+    if isinstance(distances, list):
+        smallest = np.min(distances)
+        return smallest, distances.index(smallest)
+    nonzero = distances[np.nonzero(distances)]
+    smallest = np.min(nonzero)
+    row, column = np.where(distances == smallest)
+    return smallest, np.concatenate((row, column), axis=None)
+
+
+def cluster_node(g, pfx, v, chi2_threshold, KL_threshold, p, tie_policy="raise"):
+    """One node of clustering.cluster (clustering.py:197-307). Returns the list
+    of slots whose in-edge gets deactivated, or None when no merge happened."""
+    S = g.slot
+    order = _dict_order(g, pfx, v)
+    num = len(order)
+    if num <= 2 or num >= 16:                                                     # :207
+        return None
+    nbrs = np.array(order)
+    psv = np.array([S[pfx + "_sv"][k] for k in order])
+    pcov = np.array([mat_from_cov5(S[pfx + "_cov"][k]) for k in order])       # edge_covariance is the joint cov
+    priors = np.array([S[pfx + "_prior"][k] for k in order])
+    node_coords = g.node["xyzr"][v]
+    nb_coords = np.array([S[pfx + "_xyzr"][k] for k in order])
+    jsv = np.array([[S[pfx + "_sv"][k][0], S[pfx + "_sv"][k][1], S[pfx + "_tau"][k]] for k in order])
+    jcov = pcov.copy()
+    D = np.zeros((num, num))
+    for i in range(num):                                                          # :80-86
+        for j in range(i):
+            D[i][j] = mahalanobis_distance(jsv[i], jcov[i], jsv[j], jcov[j], node_coords, nb_coords[i],
+                                           nb_coords[j], p.sigma0rz, p.sigma0rz2, p.endcap_boundary)
+    if not np.any(D):
+        raise ReferenceError_("ValueError: all pairwise distances are zero (clustering.py:120)")
+    smallest, idx = get_smallest_dist_idx(D)
+    if not (smallest < chi2_threshold):                                          # :228
+        return None
+    pm, pc = merge_states(psv[idx[0]], pcov[idx[0]], psv[idx[1]], pcov[idx[1]])
+    jm, jc = merge_states(jsv[idx[0]], jcov[idx[0]], jsv[idx[1]], jcov[idx[1]])
+    mprior = priors[idx[0]] + priors[idx[1]]
+    psv = np.delete(psv, idx, axis=0); pcov = np.delete(pcov, idx, axis=0)
+    jsv = np.delete(jsv, idx, axis=0); jcov = np.delete(jcov, idx, axis=0)
+    priors = np.delete(priors, idx)
+    nbrs = np.delete(nbrs, idx, axis=0)
+    num = psv.shape[0]
+    tie_stop = False
+    if num == 0:
+        if tie_policy == "raise":
+            raise ReferenceError_("ValueError: tie emptied the state list (clustering.py:116)")
+        tie_stop = True
+    if not tie_stop:
+        dists = [KLDistance(jsv[i], jcov[i], jm, jc) for i in range(num)]
+        smallest, idx = get_smallest_dist_idx(dists)
+        while smallest < KL_threshold:                                            # :261
+            pm, pc = merge_states(psv[idx], pcov[idx], pm, pc)
+            jm, jc = merge_states(jsv[idx], jcov[idx], jm, jc)
+            mprior = priors[idx] + mprior
+            psv = np.delete(psv, idx, axis=0); pcov = np.delete(pcov, idx, axis=0)
+            jsv = np.delete(jsv, idx, axis=0); jcov = np.delete(jcov, idx, axis=0)
+            priors = np.delete(priors, idx)
+            nbrs = np.delete(nbrs, idx, axis=0)
+            num = psv.shape[0]
+            if len(nbrs) == 0:
+                break
+            dists = [KLDistance(jsv[i], jcov[i], jm, jc) for i in range(num)]
+            smallest, idx = get_smallest_dist_idx(dists)
+    g.node["has_merged"][v] = 1                                                   # :291-293
+    g.node["merged_state"][v] = pm
+    g.node["merged_cov"][v] = cov5_from_mat(pc)
+    g.node["merged_prior"][v] = mprior
+    return [int(k) for k in nbrs]
+
+
+def cluster_stage(g: TrackGraph, pfx: str, chi2_threshold: float, KL_threshold: float, p,
+                  tie_policy="raise") -> dict:
+    """clustering.cluster body after loading (clustering.py:181-373)."""
+    deact = []
+    merged = 0
+    for v in range(g.n_nodes):
+        if not _has(g, pfx, v):
+            continue
+        r = cluster_node(g, pfx, v, chi2_threshold, KL_threshold, p, tie_policy)
+        if r is not None:
+            merged += 1
+            deact.extend(r)
+    for k in deact:                                                               # :311-321
+        if g.slot["is_edge"][k]:
+            g.slot["act"][k] = 0
+    query_node_degree_in_edges(g)                                                 # :324-327
+    compute_mixture_weights(g, pfx)                                               # :372
+    compute_prior_probabilities(g, pfx)                                           # :373
+    return {"merged_nodes": merged}
+
+
+def full_pass(g: TrackGraph, p, tie_policy="stop") -> dict:
+    """The benchmarked pass: extrapolate stage -> update stage -> clustering on
+    updated_track_states (run_gnn_trackml_mod.sh:101,138,112 order)."""
+    info = extrapolate_stage(g, p)
+    update_stage(g, p)
+    info.update(cluster_stage(g, "uts", p.cluster_chi2, p.cluster_kl, p, tie_policy))
+    return info
+
+
+# ---------------------------------------------------------------------------
+# a16: tag propagation  (tag_propagation/tag_propagation.py:64-164)
+# ---------------------------------------------------------------------------
+def tag_propagation(g: TrackGraph, threshold: float = 0.1):
+    """Returns (final tags [N], number of tags flipped per sweep)."""
+    N = g.n_nodes
+    r = g.node["gnn"][:, 3] if np.all(np.isnan(g.node["xyzr"][:, 3])) else g.node["xyzr"][:, 3]
+    # A = to_dict_of_dicts: successors (:67); keep neighbours with r_nbr <= r_node (:99-110)
+    dst = g.slot_dst()
+    proc = {}
+    for u in range(N):
+        nb = []
+        for e in range(g.out_ptr[u], g.out_ptr[u + 1]):
+            w = int(dst[g.out_slot[e]])
+            if not (r[w] > r[u]):
+                nb.append(w)
+        if nb:
+            proc[u] = nb
+    tags = g.node["tag"].copy()
+    flips_hist = []
+    total = len(proc)
+    frac = 1.0
+    while frac > threshold:                                                       # :137
+        new = tags.copy()
+        flips = 0
+        for u, nb in proc.items():
+            t = max([tags[u]] + [tags[w] for w in nb])                            # :148 max
+            new[u] = t
+            if tags[u] != t:
+                flips += 1
+        flips_hist.append(flips)
+        frac = flips / total if total else 0.0
+        tags = new
+    return tags, flips_hist
+
+
+# ---------------------------------------------------------------------------
+# a17: parabolic 3-parameter state + pairwise KL
+# learn_KL_parabolic_model/src/generate_training_data/utils.py:221-299,
+# extract_metadata_trackml_parabolic_model.py:15-99
+# ---------------------------------------------------------------------------
+def parabolic_states(gnn_node, gnn_nbrs):
+    """track_state_estimates of one node for its neighbours (utils.py:221-289)."""
+    S = np.array([[4.0**2, 0, 0], [0, 0.1**2, 0], [0, 0, 0.1**2]])
+    coords = [(0.0, 0.0), (gnn_node[0], gnn_node[1])] + [(c[0], c[1]) for c in gnn_nbrs]
+    coords.reverse()
+    # rotate_track (utils.py:197-218): p1 = origin, p2 = node
+    p1, p2 = coords[-1], coords[-2]
+    a = atan2(p2[1] - p1[1], p2[0] - p1[0])
+    while a < 0.0:
+        a += math.pi * 2
+    angle = 2 * math.pi - a
+    rotated = []
+    for c in coords:
+        x, y = c[0], c[1]
+        rotated.append((x * np.cos(angle) - y * np.sin(angle), x * np.sin(angle) + y * np.cos(angle)))
+    xt, yt = rotated[-2][0], rotated[-2][1]
+    tc = [(rc[0] - xt, rc[1] - yt) for rc in rotated]
+    x_0 = tc[-1][0]
+    out = []
+    for tnc in tc[:-2]:
+        x_B, m_B = tnc[0], tnc[1]
+        H = np.array([[x_0**2, x_0, 1], [0, 0, 1], [x_B**2, x_B, 1]])
+        H_inv = np.linalg.inv(H)
+        sv = H_inv.dot([0.0, 0.0, m_B])
+        cov = H_inv.dot(S).dot(H_inv.T)
+        out.append((sv, cov))
+    out.reverse()          # back to neighbour order (keys were reversed too)
+    return out
+
+
+def parabolic_kl_pairs(svs, covs):
+    """calc_pairwise_distances (extract_metadata_trackml_parabolic_model.py:15-25):
+    lower triangle i > j, row-major."""
+    inv = np.linalg.inv(np.asarray(covs))
+    out = []
+    for i in range(len(svs)):
+        for j in range(i):
+            trace = np.trace((covs[i] - covs[j]) * (inv[j] - inv[i]))
+            out.append(trace + (svs[i] - svs[j]).T.dot(inv[i] + inv[j]).dot(svs[i] - svs[j]))
+    return out

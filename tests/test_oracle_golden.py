@@ -1,0 +1,75 @@
+"""The CPU oracle reproduces the reference's outputs on the golden fixtures.
+
+Fixtures come from tests/golden/make_golden.py, which ran the reference's own
+functions on the committed volume-7 event. This pins the oracle before it is
+used to check the HIP path.
+"""
+import numpy as np
+import pytest
+
+import gtf_oracle as O
+from compare import compare
+from fixtures import load, expected_graph
+from gtf.params import Params
+
+
+def _params(meta):
+    return Params(sigma0xy=meta["sigma0xy"], sigma0rz=meta["sigma0rz"], sigma0rz2=meta["sigma0rz2"],
+                  endcap_boundary=meta["endcap_boundary"], chi2_cut=meta.get("chi2_cut", 2.0),
+                  cluster_chi2=meta.get("chi2", 1000.0), cluster_kl=meta.get("kl", 100.0))
+
+
+RTOL = 1e-12   # oracle vs reference: same NumPy calls, so (near) bit-exact
+
+
+def test_extrapolate_it2():
+    g, out, _, meta = load("extrapolate_it2")
+    exp = expected_graph(g, out)
+    O.extrapolate_stage(g, _params(meta))
+    assert compare(g, exp, rtol=RTOL) == []
+
+
+def test_extrapolate_full_load():
+    g, out, _, meta = load("extrapolate_full")
+    exp = expected_graph(g, out)
+    O.extrapolate_stage(g, _params(meta))
+    assert compare(g, exp, rtol=RTOL) == []
+
+
+def test_update_with_orphans():
+    g, out, _, meta = load("update_it2")
+    assert (g.slot["slot_src"] < 0).any(), "fixture should carry orphan state keys"
+    exp = expected_graph(g, out)
+    O.update_stage(g, _params(meta))
+    assert compare(g, exp, rtol=RTOL) == []
+
+
+def test_cluster_tse():
+    g, out, _, meta = load("cluster_tse")
+    exp = expected_graph(g, out)
+    O.cluster_stage(g, "tse", meta["chi2"], meta["kl"], _params(meta))
+    assert compare(g, exp, rtol=RTOL) == []
+
+
+def test_cluster_uts():
+    g, out, _, meta = load("cluster_uts")
+    exp = expected_graph(g, out)
+    O.cluster_stage(g, "uts", meta["chi2"], meta["kl"], _params(meta))
+    assert compare(g, exp, rtol=RTOL) == []
+
+
+def test_full_pass():
+    g, out, _, meta = load("pass_full")
+    exp = expected_graph(g, out)
+    O.full_pass(g, _params(meta))
+    assert compare(g, exp, rtol=RTOL) == []
+
+
+def test_tag_propagation():
+    g, _, extra, _ = load("tags_vol7")
+    tags, flips = O.tag_propagation(g)
+    assert list(flips) == list(extra["flips"])
+    kept = extra["tags"] >= 0          # isolated nodes are dropped by the script (:75-92)
+    assert kept.sum() > 0.7 * len(kept)
+    assert np.array_equal(tags[kept], extra["tags"][kept])
+    assert np.array_equal(tags[~kept], g.node["tag"][~kept])

@@ -1,0 +1,613 @@
+// gtf_pass.hip -- the extrapolate -> update -> cluster pass as HIP kernels for
+// gfx950 (MI355X), behind the C-ABI of include/gtf.h.
+//
+// Work decomposition (DESIGN.md "Kernels"):
+//   k_sender_scan     1 thread / sender node: walks the node's active out-edges in
+//                     successor order and forms the running merged_cov[1,1] += var_ms
+//                     that each extrapolation sees (the in-place mutation of
+//                     extrapolate_merged_states.py:127-128, an inclusive sequential scan).
+//   k_extrapolate     1 thread / slot (receiver-major, coalesced writes of the new
+//                     updated_track_states entry): parabolic extrapolation, chi2 gate,
+//                     Kalman predict + update (extrapolate_merged_states.py:26-402).
+//   k_node_*          1 thread / receiver node over its slot segment: everything after
+//                     message passing only reads/writes the node's own in-edge segment
+//                     (priors, side norm, reweight, degree, pruning, KL clustering), so
+//                     these stages fuse into one launch with no inter-node traffic.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "../../include/gtf.h"
+#include "gtf_math.h"
+
+using namespace gtf;
+
+namespace {
+
+constexpr int BLOCK = 256;
+constexpr int MAX_CLUSTER = 15;  // clustering.py:207 (2 < d < 16)
+
+struct Ws {
+    uint32_t* err;     // error word
+    double* c11_seen;  // [S] merged_cov[1,1] value seen by the extrapolation of out-edge (slot)
+    double* var_ms;    // [S] var_ms of that extrapolation
+};
+
+__host__ inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+__host__ inline Ws carve(void* base, int32_t n_nodes, int32_t n_slots) {
+    (void)n_nodes;
+    char* p = (char*)base;
+    Ws w;
+    w.err = (uint32_t*)p;
+    p += 256;
+    w.c11_seen = (double*)p;
+    p += align256(sizeof(double) * (size_t)(n_slots > 0 ? n_slots : 1));
+    w.var_ms = (double*)p;
+    return w;
+}
+
+__device__ __forceinline__ void raise_flag(uint32_t* err, uint32_t f) { atomicOr(err, f); }
+
+__device__ __forceinline__ Cov5 load_cov5(const double* c, int64_t i) {
+    const double* p = c + 5 * i;
+    return Cov5{p[0], p[1], p[2], p[3], p[4]};
+}
+__device__ __forceinline__ void store_cov5(double* c, int64_t i, const Cov5& v) {
+    double* p = c + 5 * i;
+    p[0] = v.c00; p[1] = v.c01; p[2] = v.c10; p[3] = v.c11; p[4] = v.c22;
+}
+
+// ---------------------------------------------------------------------------
+// var_ms: Highland multiple scattering term (extrapolate_merged_states.py:114-124)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double highland_var_ms(double a, double b, const double* ng, const double* nb,
+                                                  double boundary) {
+    double dr = nb[3] - ng[3];
+    double dz = nb[2] - ng[2];
+    double hyp = sqrt(dr * dr + dz * dz);
+    double sin_t = fabs(dr) / hyp;
+    double q = (2.0 * a * nb[0]) + b;
+    double kappa = (2.0 * a) / pow(1.0 + q * q, 1.5);
+    double t = ((13.6 * 1e-3 * sqrt(0.02)) * kappa) / 0.3;
+    double var_ms = sin_t * (t * t);
+    if (fabs(ng[2]) >= boundary) {
+        double tan_t = fabs(dr) / fabs(dz);
+        var_ms = var_ms * tan_t;
+    }
+    return var_ms;
+}
+
+// ---------------------------------------------------------------------------
+// k_sender_scan
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(BLOCK) k_sender_scan(gtf_graph g, gtf_nodes n, gtf_edges e, gtf_params p, Ws w) {
+    int u = blockIdx.x * BLOCK + threadIdx.x;
+    if (u >= g.n_nodes || !n.has_merged[u]) return;
+    const double a = n.merged_state[3 * u + 0];
+    const double b = n.merged_state[3 * u + 1];
+    const double* ng = g.gnn + 4 * (int64_t)u;
+    double c11 = n.merged_cov[5 * (int64_t)u + 3];
+    const int lo = g.out_ptr[u], hi = g.out_ptr[u + 1];
+    for (int i = lo; i < hi; i++) {
+        const int k = g.out_slot[i];
+        if (e.act[k] != 1) continue;  // :431
+        const int v = g.slot_dst[k];
+        const double vm = highland_var_ms(a, b, ng, g.gnn + 4 * (int64_t)v, p.endcap_boundary);
+        c11 = c11 + vm;  // :128 cumulative, in successor order
+        w.c11_seen[k] = c11;
+        w.var_ms[k] = vm;
+    }
+    n.merged_cov[5 * (int64_t)u + 3] = c11;  // the mutated array is what the stage saves
+}
+
+// ---------------------------------------------------------------------------
+// k_extrapolate: one slot (edge u -> v) per thread
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(BLOCK) k_extrapolate(gtf_graph g, gtf_nodes n, gtf_states uts, gtf_edges e,
+                                                       gtf_params p, Ws w) {
+    const int k = blockIdx.x * BLOCK + threadIdx.x;
+    if (k >= g.n_slots) return;
+    uts.fresh[k] = 0;
+    if (!g.is_edge[k]) return;
+    const int u = g.slot_src[k];
+    if (!n.has_merged[u] || e.act[k] != 1) return;
+    const int v = g.slot_dst[k];
+    const double* ng = g.gnn + 4 * (int64_t)u;  // sender ("node" in the reference)
+    const double* nb = g.gnn + 4 * (int64_t)v;  // receiver ("neighbour")
+    const double node_x = ng[0], node_y = ng[1], node_z = ng[2];
+    const double nbx = nb[0], nby = nb[1], nbz = nb[2];
+    const double a = n.merged_state[3 * u + 0], b = n.merged_state[3 * u + 1], c = n.merged_state[3 * u + 2];
+
+    const double ang = atan2(node_y, node_x);                                    // :41
+    const double x_A = (nbx - node_x) * cos(ang) + (nby - node_y) * sin(ang);     // :52
+    const double phi = atan2((node_x * nby) - (node_y * nbx), (node_x * nbx) + (node_y * nby));  // :59
+    const double sp = sin(phi), cp = cos(phi);
+    const double x_prime = x_A + (c * sp);                                        // :63
+    const double Vx = cp + (b * sp);
+    const double Ax = a * sp;
+    const double s_star = (-x_prime * ((2.0 * (Vx * Vx)) + (Ax * x_prime))) / (2.0 * pow(Vx, 3.0));  // :68
+
+    double numer = x_A + c * sp;                                                  // :82
+    double denom = cp + b * sp;
+    const double d2 = denom * denom;
+    const double ds_da = -(sp * (numer * numer)) / pow(denom, 3.0);
+    const double ds_db = ((sp * numer) * (1.0 + ((3.0 * a * sp * numer) / d2))) / d2;
+    const double ds_dc = (-sp * (1.0 + ((2.0 * a * sp * numer) / d2))) / denom;
+    denom = cp + ((2.0 * a + b) * sp);                                             // :89
+    const double da_da = (1.0 / pow(denom, 3.0)) * (1.0 - ((6.0 * a * sp) * (s_star + a * ds_da) / denom));
+    const double da_db = (-3.0 * a * sp * ((2.0 * a * ds_db) + 1.0)) / pow(denom, 4.0);
+    const double da_dc = (-6.0 * sp * ds_dc * (a * a)) / pow(denom, 4.0);
+    denom = cp + ((2.0 * a * s_star + b) * sp);                                    // :95
+    double bracket = cp - ((sp * (-sp + ((2.0 * a * s_star + b) * cp))) / denom);
+    const double db_da = (2.0 * (s_star + a * ds_da) * bracket) / denom;
+    const double db_db = ((1.0 + (2.0 * a * ds_da)) * bracket) / denom;
+    const double db_dc = (2.0 * a * ds_dc * bracket) / denom;
+    bracket = (cp * (2.0 * a + b)) - sp;                                           // :102
+    const double dc_da = (ds_da * bracket) + ((s_star * s_star) * cp);
+    const double dc_db = (ds_db * bracket) + (s_star * cp);
+    const double dc_dc = (ds_dc * bracket) + cp;
+    const Mat3 F = {{{da_da, da_db, da_dc}, {db_da, db_db, db_dc}, {dc_da, dc_db, dc_dc}}};
+
+    const double var_ms = w.var_ms[k];
+    const Cov5 mc = load_cov5(n.merged_cov, u);
+    const Mat3 C = {{{mc.c00, mc.c01, 0.0}, {mc.c10, w.c11_seen[k], 0.0}, {0.0, 0.0, mc.c22}}};  // :128
+    const double m[3] = {a, b, c};
+    double xe[3];
+    mv3(F, m, xe);                                                                 // :129
+    const Mat3 Pe = mm3t(mm3(F, C), F);                                            // :130
+    const double sig2 = p.sigma0xy * p.sigma0xy;
+    const double S = Pe.m[2][2] + sig2;                                            // :138
+    const double invS = 1.0 / S;
+    const double resid = 0.0 - xe[2];
+    const double chi2 = (resid * invS) * resid;                                    // :140
+    if (!(chi2 <= p.chi2_cut)) {                                                   // :298
+        e.act[k] = 0;                                                              // :393
+        return;
+    }
+    const double lik = pow((2.0 * M_PI) * fabs(S), -0.5) * exp(-0.5 * chi2);      // :302-304
+
+    // filterpy 1.4.5 predict() + update(0)  (:307-323): F applied a second time
+    double xp[3];
+    mv3(F, xe, xp);
+    Mat3 Pp = mm3t(mm3(F, Pe), F);
+    Pp.m[1][1] = Pp.m[1][1] + var_ms;                                              // + Q
+    const double y = 0.0 - xp[2];
+    const double S2 = Pp.m[2][2] + sig2;
+    const double SI = 1.0 / S2;
+    const double K0 = Pp.m[0][2] * SI, K1 = Pp.m[1][2] * SI, K2 = Pp.m[2][2] * SI;
+    const double xu0 = xp[0] + K0 * y, xu1 = xp[1] + K1 * y, xu2 = xp[2] + K2 * y;
+    const Mat3 IKH = {{{1.0, 0.0, 0.0 - K0}, {0.0, 1.0, 0.0 - K1}, {0.0, 0.0, 1.0 - K2}}};
+    const Mat3 A = mm3(IKH, Pp);
+    // P = A IKH^T + (K R) K^T, only the [a,b] block survives the aliasing (:362-365)
+    double P00 = A.m[0][0] * IKH.m[0][0]; P00 = P00 + A.m[0][1] * IKH.m[0][1]; P00 = P00 + A.m[0][2] * IKH.m[0][2];
+    double P01 = A.m[0][0] * IKH.m[1][0]; P01 = P01 + A.m[0][1] * IKH.m[1][1]; P01 = P01 + A.m[0][2] * IKH.m[1][2];
+    double P10 = A.m[1][0] * IKH.m[0][0]; P10 = P10 + A.m[1][1] * IKH.m[0][1]; P10 = P10 + A.m[1][2] * IKH.m[0][2];
+    double P11 = A.m[1][0] * IKH.m[1][0]; P11 = P11 + A.m[1][1] * IKH.m[1][1]; P11 = P11 + A.m[1][2] * IKH.m[1][2];
+    P00 = P00 + (K0 * sig2) * K0;
+    P01 = P01 + (K0 * sig2) * K1;
+    P10 = P10 + (K1 * sig2) * K0;
+    P11 = P11 + (K1 * sig2) * K1;
+
+    // tau and its variance (:326-358) -- NOT squared here, unlike helper.py:421
+    const double dr = nb[3] - ng[3];
+    const double dz = nbz - node_z;
+    const double tau = dz / dr;
+    double sigma_r = p.sigma0rz, sigma_z = p.sigma0rz2;
+    if (fabs(node_z) >= p.endcap_boundary) { sigma_z = p.sigma0rz; sigma_r = p.sigma0rz2; }
+    double sigma_rn = p.sigma0rz, sigma_zn = p.sigma0rz2;
+    if (fabs(nbz) >= p.endcap_boundary) { sigma_zn = p.sigma0rz; sigma_rn = p.sigma0rz2; }
+    const double J0 = 1.0 / dr, J1 = -1.0 / dr, J2 = (-dz) / (dr * dr), J3 = dz / (dr * dr);
+    double vt = (J0 * (sigma_z * sigma_z)) * J0;
+    vt = vt + (J1 * (sigma_zn * sigma_zn)) * J1;
+    vt = vt + (J2 * (sigma_r * sigma_r)) * J2;
+    vt = vt + (J3 * (sigma_rn * sigma_rn)) * J3;
+
+    const double smw = e.send_mw[k];
+    if (isnan(smw)) raise_flag(w.err, GTF_ERR_SEND_MW_MISSING);
+    uts.sv[3 * (int64_t)k + 0] = xu0;
+    uts.sv[3 * (int64_t)k + 1] = xu1;
+    uts.sv[3 * (int64_t)k + 2] = xu2;
+    uts.tau[k] = tau;
+    store_cov5(uts.cov, k, Cov5{P00, P01, P10, P11, vt + var_ms});
+    double* sx = uts.xyzr + 4 * (int64_t)k;
+    sx[0] = ng[0]; sx[1] = ng[1]; sx[2] = ng[2]; sx[3] = ng[3];
+    uts.lik[k] = lik;
+    uts.mw[k] = smw;                                                               // :384
+    uts.prior[k] = NAN;
+    uts.lr[k] = NAN;
+    uts.side[k] = -1;
+    uts.fresh[k] = 1;
+    n.has_uts[v] = 1;  // benign same-value race between the receiver's accepted slots
+}
+
+// ---------------------------------------------------------------------------
+// node-local stages (1 thread per receiver node)
+// ---------------------------------------------------------------------------
+struct Seg {
+    int lo, hi;
+};
+
+// iterate the slots of a dict in rank order: calls f(slot) for each present key
+template <typename Fn>
+__device__ __forceinline__ void for_dict(const int32_t* rank, Seg s, bool monotone, Fn f) {
+    if (monotone) {
+        for (int k = s.lo; k < s.hi; k++)
+            if (rank[k] >= 0) f(k);
+        return;
+    }
+    int prev = -1;
+    while (true) {
+        int best = -1, br = 0x7fffffff;
+        for (int k = s.lo; k < s.hi; k++) {
+            const int r = rank[k];
+            if (r > prev && r < br) { br = r; best = k; }
+        }
+        if (best < 0) break;
+        f(best);
+        prev = br;
+    }
+}
+
+__device__ __forceinline__ bool ranks_monotone(const int32_t* rank, Seg s) {
+    int prev = -1;
+    for (int k = s.lo; k < s.hi; k++) {
+        const int r = rank[k];
+        if (r >= 0) {
+            if (r <= prev) return false;
+            prev = r;
+        }
+    }
+    return true;
+}
+
+__device__ __forceinline__ bool edge_active(const gtf_graph& g, const gtf_edges& e, int k) {
+    return g.is_edge[k] && e.act[k] == 1;
+}
+
+// compute_prior_probabilities for one node (helper.py:30-63)
+__device__ void node_priors(const gtf_graph& g, const gtf_edges& e, const gtf_states& st, Seg s) {
+    for (int k = s.lo; k < s.hi; k++) {
+        if (st.rank[k] < 0 || !edge_active(g, e, k)) continue;
+        const double lk = g.layer[g.slot_src[k]];
+        int cnt = 0;
+        for (int j = s.lo; j < s.hi; j++)
+            if (st.rank[j] >= 0 && edge_active(g, e, j) && g.layer[g.slot_src[j]] == lk) cnt++;
+        st.prior[k] = 1.0 / (double)cnt;
+    }
+}
+
+// calculate_side_norm_factor + reweight for one node (helper.py:99-200)
+__device__ void node_reweight(const gtf_graph& g, gtf_edges& e, gtf_states& st, Seg s, int v, double thr,
+                              uint32_t* err) {
+    const bool mono = ranks_monotone(st.rank, s);
+    // the stale loop variable after the side-norm loop is the LAST dict key (helper.py:131,138)
+    int last = -1, lastr = -1;
+    for (int k = s.lo; k < s.hi; k++)
+        if (st.rank[k] > lastr) { lastr = st.rank[k]; last = k; }
+    const double node_x = g.gnn[4 * (int64_t)v];
+    int nl = 0, nr = 0, dl = 0, dr = 0;
+    for (int k = s.lo; k < s.hi; k++) {
+        if (st.rank[k] < 0 || !edge_active(g, e, k)) continue;
+        const double xk = st.xyzr[4 * (int64_t)k];
+        const bool left = xk < node_x;
+        bool dup = false;  // distinct x values per side: len(set(coords))
+        for (int j = s.lo; j < k; j++) {
+            if (st.rank[j] < 0 || !edge_active(g, e, j)) continue;
+            const double xj = st.xyzr[4 * (int64_t)j];
+            if ((xj < node_x) == left && xj == xk) { dup = true; break; }
+        }
+        if (left) { nl++; if (!dup) dl++; } else { nr++; if (!dup) dr++; }
+    }
+    if (nl + nr > 0) {
+        if (!g.is_edge[last]) raise_flag(err, GTF_ERR_STALE_KEY_NO_EDGE);
+        const bool last_act = g.is_edge[last] && e.act[last] == 1;
+        for (int k = s.lo; k < s.hi; k++) {
+            if (st.rank[k] < 0 || !edge_active(g, e, k)) continue;
+            const bool left = st.xyzr[4 * (int64_t)k] < node_x;
+            st.side[k] = left ? 0 : 1;
+            st.lr[k] = last_act ? (double)(left ? dl : dr) : 1.0;
+        }
+    }
+    double denom = 0.0;  // sequential sum in dict order (:165-169)
+    for_dict(st.rank, s, mono, [&](int k) {
+        if (edge_active(g, e, k)) denom = denom + (st.mw[k] * st.lik[k]);
+    });
+    for (int k = s.lo; k < s.hi; k++) {  // :172-200 (order-independent)
+        if (st.rank[k] < 0 || !edge_active(g, e, k)) continue;
+        double wgt = (st.mw[k] * st.lik[k] * st.prior[k]) / denom;
+        wgt = wgt / st.lr[k];
+        st.mw[k] = wgt;
+        e.edge_mw[k] = wgt;
+        e.act[k] = (wgt < thr) ? 0 : 1;
+    }
+}
+
+__device__ __forceinline__ int node_degree(const gtf_graph& g, const gtf_edges& e, Seg s) {
+    int d = 0;
+    for (int k = s.lo; k < s.hi; k++) d += edge_active(g, e, k) ? 1 : 0;
+    return d;
+}
+
+// compute_mixture_weights for one node (helper.py:76-96)
+__device__ void node_mixture_weights(const gtf_graph& g, gtf_states& st, Seg s, int v, uint32_t* err) {
+    int cnt = 0;
+    for (int k = s.lo; k < s.hi; k++) cnt += st.rank[k] >= 0 ? 1 : 0;
+    if (cnt == 0) {
+        if (!g.solo[v]) raise_flag(err, GTF_ERR_EMPTY_DICT_MW);
+        return;
+    }
+    const double mw = 1.0 / (double)cnt;
+    for (int k = s.lo; k < s.hi; k++)
+        if (st.rank[k] >= 0) st.mw[k] = mw;
+}
+
+// new UTS keys created by this message passing are appended after the existing
+// ones in sender order (dict insertion, extrapolate_merged_states.py:443-447)
+__device__ void node_assign_ranks(gtf_states& uts, Seg s) {
+    int next = -1;
+    for (int k = s.lo; k < s.hi; k++) next = max(next, uts.rank[k]);
+    next += 1;
+    for (int k = s.lo; k < s.hi; k++)
+        if (uts.fresh[k] && uts.rank[k] < 0) uts.rank[k] = next++;
+}
+
+// remove_state_metadata pruning (remove_state_metadata.py:31-48)
+__device__ void node_prune(const gtf_graph& g, const gtf_nodes& n, gtf_states& tse, gtf_states& uts, Seg s, int v,
+                           uint32_t* err) {
+    gtf_states& st = n.has_uts[v] ? uts : tse;
+    if (!n.has_uts[v] && !n.has_tse[v]) {
+        raise_flag(err, GTF_ERR_NO_STATE_DICT);
+        return;
+    }
+    for (int k = s.lo; k < s.hi; k++)
+        if (st.rank[k] >= 0 && !g.rev_edge[k]) st.rank[k] = -1;
+}
+
+// clustering of one node (clustering.py:197-307)
+__device__ void node_cluster(const gtf_graph& g, gtf_nodes& n, const gtf_states& st, gtf_edges& e, Seg s, int v,
+                             double chi2_thr, double kl_thr, const gtf_params& p, uint32_t* err) {
+    int d = 0;
+    for (int k = s.lo; k < s.hi; k++) d += st.rank[k] >= 0 ? 1 : 0;
+    if (d <= 2 || d >= 16) return;                                                 // :207
+    int ord[MAX_CLUSTER];
+    {
+        int i = 0;
+        for_dict(st.rank, s, ranks_monotone(st.rank, s), [&](int k) { ord[i++] = k; });
+    }
+    const double* na = g.xyzr + 4 * (int64_t)v;
+    // pairwise chi2 over the lower triangle, np.where semantics on ties (:114-124)
+    double best = INFINITY;
+    bool any_nonzero = false, has_nan = false;
+    int ti0 = -1, tj0 = -1, ti1 = -1;
+    uint32_t tiemask = 0;
+    for (int i = 1; i < d; i++) {
+        const int ki = ord[i];
+        const Cov5 ci = load_cov5(st.cov, ki);
+        const double ai = st.sv[3 * (int64_t)ki], bi = st.sv[3 * (int64_t)ki + 1];
+        for (int j = 0; j < i; j++) {
+            const int kj = ord[j];
+            const Cov5 cj = load_cov5(st.cov, kj);
+            const double D = mahalanobis(ai, bi, ci, st.sv[3 * (int64_t)kj], st.sv[3 * (int64_t)kj + 1], cj, na,
+                                         st.xyzr + 4 * (int64_t)ki, st.xyzr + 4 * (int64_t)kj, p.sigma0rz2,
+                                         p.sigma0rz, p.sigma0rz, p.sigma0rz2, p.endcap_boundary);
+            if (D == 0.0) continue;  // zeros are excluded (np.nonzero)
+            any_nonzero = true;
+            if (isnan(D)) { has_nan = true; continue; }
+            if (D < best) {
+                best = D; ti0 = i; tj0 = j; ti1 = -1;
+                tiemask = (1u << i) | (1u << j);
+            } else if (D == best) {
+                if (ti1 < 0) ti1 = i;
+                tiemask |= (1u << i) | (1u << j);
+            }
+        }
+    }
+    if (!any_nonzero) { raise_flag(err, GTF_ERR_ALL_ZERO_DIST); return; }
+    if (has_nan || !(best < chi2_thr)) return;                                     // :228
+    // merge pair = (idx[0], idx[1]) of concatenate((rows, cols))
+    const int p0 = ti0, p1 = (ti1 >= 0) ? ti1 : tj0;
+    double pm[3], jm[3];
+    Cov5 pc, jc;
+    {
+        const int k0 = ord[p0], k1 = ord[p1];
+        const double ps0[3] = {st.sv[3 * (int64_t)k0], st.sv[3 * (int64_t)k0 + 1], st.sv[3 * (int64_t)k0 + 2]};
+        const double ps1[3] = {st.sv[3 * (int64_t)k1], st.sv[3 * (int64_t)k1 + 1], st.sv[3 * (int64_t)k1 + 2]};
+        const double js0[3] = {ps0[0], ps0[1], st.tau[k0]};
+        const double js1[3] = {ps1[0], ps1[1], st.tau[k1]};
+        const Cov5 c0 = load_cov5(st.cov, k0), c1 = load_cov5(st.cov, k1);
+        merge_states(ps0, c0, ps1, c1, pm, pc);
+        merge_states(js0, c0, js1, c1, jm, jc);
+    }
+    double mprior = st.prior[ord[p0]] + st.prior[ord[p1]];
+    uint32_t alive = ((1u << d) - 1u) & ~tiemask;
+    if (alive == 0) {
+        raise_flag(err, GTF_ERR_TIE_EMPTIED);
+    } else {
+        while (true) {                                                             // :251-287
+            double mind = 0.0;
+            int mi = -1;
+            bool nan_seen = false;
+            for (int i = 0; i < d; i++) {
+                if (!(alive & (1u << i))) continue;
+                const int ki = ord[i];
+                const double js[3] = {st.sv[3 * (int64_t)ki], st.sv[3 * (int64_t)ki + 1], st.tau[ki]};
+                const double D = kl_distance(js, load_cov5(st.cov, ki), jm, jc);
+                if (isnan(D)) nan_seen = true;
+                if (mi < 0 || D < mind) { mind = D; mi = i; }  // first minimum (list.index)
+            }
+            if (nan_seen) { raise_flag(err, GTF_ERR_NAN_KL); break; }
+            if (!(mind < kl_thr)) break;
+            const int ki = ord[mi];
+            const double ps[3] = {st.sv[3 * (int64_t)ki], st.sv[3 * (int64_t)ki + 1], st.sv[3 * (int64_t)ki + 2]};
+            const double js[3] = {ps[0], ps[1], st.tau[ki]};
+            const Cov5 ci = load_cov5(st.cov, ki);
+            double npm[3], njm[3];
+            Cov5 npc, njc;
+            merge_states(ps, ci, pm, pc, npm, npc);
+            merge_states(js, ci, jm, jc, njm, njc);
+            pm[0] = npm[0]; pm[1] = npm[1]; pm[2] = npm[2]; pc = npc;
+            jm[0] = njm[0]; jm[1] = njm[1]; jm[2] = njm[2]; jc = njc;
+            mprior = st.prior[ki] + mprior;
+            alive &= ~(1u << mi);
+            if (alive == 0) break;
+        }
+    }
+    n.has_merged[v] = 1;                                                           // :291-293
+    n.merged_state[3 * (int64_t)v + 0] = pm[0];
+    n.merged_state[3 * (int64_t)v + 1] = pm[1];
+    n.merged_state[3 * (int64_t)v + 2] = pm[2];
+    store_cov5(n.merged_cov, v, pc);
+    n.merged_prior[v] = mprior;
+    for (int i = 0; i < d; i++)                                                    // :311-321 deactivation
+        if (alive & (1u << i)) {
+            const int ki = ord[i];
+            if (g.is_edge[ki]) e.act[ki] = 0;
+        }
+}
+
+enum : int { ST_EXTRAP = 1, ST_UPDATE = 2, ST_CLUSTER = 4 };
+
+__global__ void __launch_bounds__(BLOCK) k_node(gtf_graph g, gtf_nodes n, gtf_states tse, gtf_states uts,
+                                                gtf_edges e, gtf_params p, Ws w, int stages, int cluster_key,
+                                                double chi2_thr, double kl_thr) {
+    const int v = blockIdx.x * BLOCK + threadIdx.x;
+    if (v >= g.n_nodes) return;
+    const Seg s{g.slot_ptr[v], g.slot_ptr[v + 1]};
+    if (stages & ST_EXTRAP) {  // extrapolate_merged_states.py:554-566
+        node_assign_ranks(uts, s);
+        if (n.has_uts[v]) {
+            node_priors(g, e, uts, s);
+            node_reweight(g, e, uts, s, v, p.reweight_threshold, w.err);
+            node_priors(g, e, uts, s);
+            node_reweight(g, e, uts, s, v, p.reweight_threshold, w.err);
+        }
+        n.degree[v] = node_degree(g, e, s);
+    }
+    if (stages & ST_UPDATE) {  // remove_state_metadata.py:31-53
+        node_prune(g, n, tse, uts, s, v, w.err);
+        if (n.has_tse[v]) node_priors(g, e, tse, s);
+        if (n.has_uts[v]) {
+            node_priors(g, e, uts, s);
+            node_reweight(g, e, uts, s, v, p.reweight_threshold, w.err);
+        }
+    }
+    if (stages & ST_CLUSTER) {  // clustering.py:197-373
+        gtf_states& st = cluster_key ? uts : tse;
+        const bool has = cluster_key ? n.has_uts[v] : n.has_tse[v];
+        if (has) {
+            node_cluster(g, n, st, e, s, v, chi2_thr, kl_thr, p, w.err);
+            // clustering only deactivates the node's OWN in-edges, so degree, mixture
+            // weights and priors can follow in the same thread (:324-327, :372-373)
+        }
+        n.degree[v] = node_degree(g, e, s);
+        if (has) {
+            node_mixture_weights(g, st, s, v, w.err);
+            node_priors(g, e, st, s);
+        }
+    }
+}
+
+thread_local char g_err[512] = "";
+
+int fail(const char* what, hipError_t e) {
+    snprintf(g_err, sizeof(g_err), "%s: %s", what, hipGetErrorString(e));
+    return -1;
+}
+
+int check_graph(const gtf_graph* g) {
+    if (!g) { snprintf(g_err, sizeof(g_err), "null graph"); return -2; }
+    if (g->n_nodes < 0 || g->n_slots < 0 || g->n_edges < 0) {
+        snprintf(g_err, sizeof(g_err), "negative sizes"); return -2;
+    }
+    if (g->n_nodes > 0 && (!g->slot_ptr || !g->out_ptr || !g->gnn)) {
+        snprintf(g_err, sizeof(g_err), "missing graph arrays"); return -2;
+    }
+    return 0;
+}
+
+inline int grid(int n) { return (n + BLOCK - 1) / BLOCK; }
+
+int launch_extrap_edges(const gtf_graph* g, gtf_nodes* n, gtf_states* uts, gtf_edges* e, const gtf_params* p,
+                        Ws w, hipStream_t st) {
+    if (g->n_nodes > 0)
+        hipLaunchKernelGGL(k_sender_scan, dim3(grid(g->n_nodes)), dim3(BLOCK), 0, st, *g, *n, *e, *p, w);
+    if (g->n_slots > 0)
+        hipLaunchKernelGGL(k_extrapolate, dim3(grid(g->n_slots)), dim3(BLOCK), 0, st, *g, *n, *uts, *e, *p, w);
+    hipError_t err = hipGetLastError();
+    return err == hipSuccess ? 0 : fail("extrapolate launch", err);
+}
+
+int launch_node(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts, gtf_edges* e,
+                const gtf_params* p, Ws w, int stages, int key, double chi2, double kl, hipStream_t st) {
+    gtf_states dummy;
+    memset(&dummy, 0, sizeof(dummy));
+    if (g->n_nodes > 0)
+        hipLaunchKernelGGL(k_node, dim3(grid(g->n_nodes)), dim3(BLOCK), 0, st, *g, *n, tse ? *tse : dummy,
+                           uts ? *uts : dummy, *e, *p, w, stages, key, chi2, kl);
+    hipError_t err = hipGetLastError();
+    return err == hipSuccess ? 0 : fail("node kernel launch", err);
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t gtf_workspace_bytes(int32_t n_nodes, int32_t n_slots) {
+    (void)n_nodes;
+    return 256 + 2 * align256(sizeof(double) * (size_t)(n_slots > 0 ? n_slots : 1));
+}
+
+int gtf_clear_errors(void* ws, gtf_stream_t stream) {
+    hipError_t e = hipMemsetAsync(ws, 0, 256, (hipStream_t)stream);
+    return e == hipSuccess ? 0 : fail("clear errors", e);
+}
+
+int gtf_read_errors(void* ws, uint32_t* flags, gtf_stream_t stream) {
+    hipError_t e = hipMemcpyAsync(flags, ws, sizeof(uint32_t), hipMemcpyDeviceToHost, (hipStream_t)stream);
+    if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)stream);
+    return e == hipSuccess ? 0 : fail("read errors", e);
+}
+
+int gtf_extrapolate(const gtf_graph* g, gtf_nodes* n, gtf_states* uts, gtf_edges* e, const gtf_params* p,
+                    void* ws, gtf_stream_t stream) {
+    int rc = check_graph(g);
+    if (rc) return rc;
+    Ws w = carve(ws, g->n_nodes, g->n_slots);
+    rc = launch_extrap_edges(g, n, uts, e, p, w, (hipStream_t)stream);
+    if (rc) return rc;
+    return launch_node(g, n, nullptr, uts, e, p, w, ST_EXTRAP, 1, 0.0, 0.0, (hipStream_t)stream);
+}
+
+int gtf_update(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts, gtf_edges* e,
+               const gtf_params* p, void* ws, gtf_stream_t stream) {
+    int rc = check_graph(g);
+    if (rc) return rc;
+    Ws w = carve(ws, g->n_nodes, g->n_slots);
+    return launch_node(g, n, tse, uts, e, p, w, ST_UPDATE, 1, 0.0, 0.0, (hipStream_t)stream);
+}
+
+int gtf_cluster(const gtf_graph* g, gtf_nodes* n, gtf_states* states, gtf_edges* e, int32_t key,
+                double chi2_threshold, double kl_threshold, const gtf_params* p, void* ws, gtf_stream_t stream) {
+    int rc = check_graph(g);
+    if (rc) return rc;
+    Ws w = carve(ws, g->n_nodes, g->n_slots);
+    return launch_node(g, n, key ? nullptr : states, key ? states : nullptr, e, p, w, ST_CLUSTER, key,
+                       chi2_threshold, kl_threshold, (hipStream_t)stream);
+}
+
+int gtf_pass(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts, gtf_edges* e,
+             const gtf_params* p, void* ws, gtf_stream_t stream) {
+    int rc = check_graph(g);
+    if (rc) return rc;
+    Ws w = carve(ws, g->n_nodes, g->n_slots);
+    rc = launch_extrap_edges(g, n, uts, e, p, w, (hipStream_t)stream);
+    if (rc) return rc;
+    return launch_node(g, n, tse, uts, e, p, w, ST_EXTRAP | ST_UPDATE | ST_CLUSTER, 1, p->cluster_chi2,
+                       p->cluster_kl, (hipStream_t)stream);
+}
+
+const char* gtf_last_error(void) { return g_err; }
+const char* gtf_version(void) { return "gtf 0.1.0 (gfx950)"; }
+
+}  // extern "C"

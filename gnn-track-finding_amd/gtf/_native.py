@@ -1,0 +1,92 @@
+"""ctypes binding of libgtf.so (the C-ABI declared in include/gtf.h).
+
+The library is built in-tree (``__graft_entry__.build()`` / ``make -C
+gnn-track-finding_amd/csrc``) and loaded from this directory. There is no CPU
+fallback: if the library is missing or fails to load, every call raises.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libgtf.so")
+
+P = ctypes.c_void_p
+I32 = ctypes.c_int32
+F64 = ctypes.c_double
+
+
+class GtfGraph(ctypes.Structure):
+    _fields_ = [("n_nodes", I32), ("n_slots", I32), ("n_edges", I32), ("pad_", I32),
+                ("slot_ptr", P), ("slot_src", P), ("slot_dst", P), ("out_ptr", P), ("out_slot", P),
+                ("is_edge", P), ("rev_edge", P), ("solo", P), ("gnn", P), ("xyzr", P), ("layer", P)]
+
+
+class GtfNodes(ctypes.Structure):
+    _fields_ = [("has_merged", P), ("merged_state", P), ("merged_cov", P), ("merged_prior", P),
+                ("has_tse", P), ("has_uts", P), ("degree", P)]
+
+
+class GtfStates(ctypes.Structure):
+    _fields_ = [("rank", P), ("sv", P), ("tau", P), ("cov", P), ("xyzr", P), ("lik", P), ("mw", P),
+                ("prior", P), ("lr", P), ("side", P), ("fresh", P)]
+
+
+class GtfEdges(ctypes.Structure):
+    _fields_ = [("act", P), ("edge_mw", P), ("send_mw", P)]
+
+
+class GtfParams(ctypes.Structure):
+    _fields_ = [("sigma0xy", F64), ("sigma0rz", F64), ("sigma0rz2", F64), ("endcap_boundary", F64),
+                ("chi2_cut", F64), ("reweight_threshold", F64), ("cluster_chi2", F64), ("cluster_kl", F64)]
+
+
+ERR_FLAGS = {
+    1: "KeyError: sender has no track_state_estimates entry for the receiver (extrapolate_merged_states.py:384)",
+    2: "KeyError: last state key has no edge (helper.py:131/138)",
+    4: "ValueError: all pairwise distances are zero (clustering.py:120)",
+    8: "ValueError: a distance tie removed every state (clustering.py:116)",
+    16: "ZeroDivisionError: empty state dict (helper.py:90)",
+    32: "ValueError: NaN KL distance (clustering.py:117)",
+    64: "KeyError: node has no state dict (remove_state_metadata.py:39)",
+}
+
+# exported symbols (must match include/gtf.h; tests check the .so exports all of them)
+SYMBOLS = ["gtf_workspace_bytes", "gtf_clear_errors", "gtf_read_errors", "gtf_extrapolate", "gtf_update",
+           "gtf_cluster", "gtf_pass", "gtf_tag_prepare", "gtf_tag_sweep", "gtf_last_error", "gtf_version"]
+
+_lib = None
+
+
+def lib():
+    """Load libgtf.so once; raise loudly if it is missing (no fallback path)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError("libgtf.so not built at %s -- run __graft_entry__.build() "
+                           "(hipcc --offload-arch=gfx950); there is no CPU fallback" % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    L.gtf_workspace_bytes.restype = ctypes.c_size_t
+    L.gtf_workspace_bytes.argtypes = [I32, I32]
+    L.gtf_clear_errors.argtypes = [P, P]
+    L.gtf_read_errors.argtypes = [P, ctypes.POINTER(ctypes.c_uint32), P]
+    G, N, S, E, PR = (ctypes.POINTER(GtfGraph), ctypes.POINTER(GtfNodes), ctypes.POINTER(GtfStates),
+                      ctypes.POINTER(GtfEdges), ctypes.POINTER(GtfParams))
+    L.gtf_extrapolate.argtypes = [G, N, S, E, PR, P, P]
+    L.gtf_update.argtypes = [G, N, S, S, E, PR, P, P]
+    L.gtf_cluster.argtypes = [G, N, S, E, I32, F64, F64, PR, P, P]
+    L.gtf_pass.argtypes = [G, N, S, S, E, PR, P, P]
+    L.gtf_tag_prepare.argtypes = [G, P, P, P, P, P]
+    L.gtf_tag_sweep.argtypes = [G, P, P, P, P, P, P]
+    L.gtf_last_error.restype = ctypes.c_char_p
+    L.gtf_version.restype = ctypes.c_char_p
+    for fn in ("gtf_clear_errors", "gtf_read_errors", "gtf_extrapolate", "gtf_update", "gtf_cluster", "gtf_pass",
+               "gtf_tag_prepare", "gtf_tag_sweep"):
+        getattr(L, fn).restype = ctypes.c_int
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc != 0:
+        raise RuntimeError("libgtf: %s (rc=%d)" % (lib().gtf_last_error().decode(), rc))

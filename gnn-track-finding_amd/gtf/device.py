@@ -1,0 +1,186 @@
+"""Device-resident TrackGraph and the stage entry points (host side of the C-ABI).
+
+``DeviceGraph`` uploads a :class:`gtf.graph.TrackGraph` into HBM once (torch
+tensors are used only as device allocations; every computation runs in
+libgtf.so's HIP kernels), then the stage methods call the C-ABI on the current
+HIP stream. ``download`` copies the mutable arrays back for unpacking.
+
+Stage methods mirror the reference's stage bodies:
+  extrapolate() -> src/extrapolate/extrapolate_merged_states.py:552-566
+  update()      -> src/update/remove_state_metadata.py:29-53
+  cluster()     -> src/clustering/clustering.py:181-373
+  full_pass()   -> the three in run_gnn_trackml_mod.sh order (extrapolate,
+                   update, cluster on updated_track_states), fused
+  tag_propagation() -> tag_propagation/tag_propagation.py:97-164
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _native as nat
+from .graph import TrackGraph, NODE_FIELDS, SLOT_FIELDS
+from .params import Params
+
+STATIC_SLOT = ("slot_src", "is_edge", "rev_edge", "send_mw")
+MUTABLE_NODE = ("has_merged", "merged_state", "merged_cov", "merged_prior", "has_tse", "has_uts", "degree")
+STATE_FIELDS = ("rank", "sv", "tau", "cov", "xyzr", "lik", "mw", "prior", "lr", "side", "fresh")
+
+
+def _torch():
+    import torch
+    if not torch.cuda.is_available():
+        raise RuntimeError("gtf needs a HIP device (MI355X); torch.cuda.is_available() is False")
+    return torch
+
+
+class DeviceGraph:
+    def __init__(self, g: TrackGraph, device: str = "cuda"):
+        torch = _torch()
+        self.torch = torch
+        self.device = torch.device(device)
+        self.lib = nat.lib()
+        self.n_nodes, self.n_slots, self.n_edges = g.n_nodes, g.n_slots, g.n_edges
+        self.t = {}
+        up = self._up
+        up("slot_ptr", g.slot_ptr.astype(np.int32))
+        up("out_ptr", g.out_ptr.astype(np.int32))
+        up("out_slot", g.out_slot.astype(np.int32))
+        up("slot_dst", g.slot_dst().astype(np.int32))
+        sub = g.node["sub_id"].astype(np.int64)
+        if g.n_nodes:
+            sizes = np.bincount(sub - sub.min())
+            solo = (sizes[sub - sub.min()] == 1).astype(np.uint8)
+        else:
+            solo = np.zeros(0, np.uint8)
+        up("solo", solo)
+        for f in ("gnn", "xyzr", "layer") + MUTABLE_NODE:
+            up(f, g.node[f])
+        for f in SLOT_FIELDS:
+            if f in ("slot_key",):
+                continue
+            up(f, g.slot[f])
+        ws_bytes = int(self.lib.gtf_workspace_bytes(g.n_nodes, g.n_slots))
+        self.t["ws"] = torch.zeros(ws_bytes, dtype=torch.uint8, device=self.device)
+        self._build_structs()
+
+    # ---------------------------------------------------------------- memory
+    def _up(self, name, arr):
+        arr = np.ascontiguousarray(arr)
+        t = self.torch.from_numpy(arr.reshape(-1) if arr.size else arr.reshape(0)).to(self.device)
+        self.t[name] = t
+
+    def ptr(self, name):
+        t = self.t[name]
+        return ctypes.c_void_p(t.data_ptr() if t.numel() else 0)
+
+    def _build_structs(self):
+        p = self.ptr
+        self.cg = nat.GtfGraph(self.n_nodes, self.n_slots, self.n_edges, 0, p("slot_ptr"), p("slot_src"),
+                               p("slot_dst"), p("out_ptr"), p("out_slot"), p("is_edge"), p("rev_edge"), p("solo"),
+                               p("gnn"), p("xyzr"), p("layer"))
+        self.cn = nat.GtfNodes(*[p(f) for f in MUTABLE_NODE])
+        self.cuts = nat.GtfStates(p("uts_rank"), p("uts_sv"), p("uts_tau"), p("uts_cov"), p("uts_xyzr"),
+                                  p("uts_lik"), p("uts_mw"), p("uts_prior"), p("uts_lr"), p("uts_side"),
+                                  p("uts_fresh"))
+        self.ctse = nat.GtfStates(p("tse_rank"), p("tse_sv"), p("tse_tau"), p("tse_cov"), p("tse_xyzr"),
+                                  ctypes.c_void_p(0), p("tse_mw"), p("tse_prior"), ctypes.c_void_p(0),
+                                  ctypes.c_void_p(0), ctypes.c_void_p(0))
+        self.ce = nat.GtfEdges(p("act"), p("edge_mw"), p("send_mw"))
+
+    @property
+    def stream(self):
+        return ctypes.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
+
+    @staticmethod
+    def cparams(p: Params) -> nat.GtfParams:
+        return nat.GtfParams(p.sigma0xy, p.sigma0rz, p.sigma0rz2, p.endcap_boundary, p.chi2_cut,
+                             p.reweight_threshold, p.cluster_chi2, p.cluster_kl)
+
+    # ---------------------------------------------------------------- stages
+    def clear_errors(self):
+        nat.check(self.lib.gtf_clear_errors(self.ptr("ws"), self.stream))
+
+    def errors(self) -> int:
+        f = ctypes.c_uint32(0)
+        nat.check(self.lib.gtf_read_errors(self.ptr("ws"), ctypes.byref(f), self.stream))
+        return int(f.value)
+
+    def raise_errors(self, ignore=0):
+        f = self.errors() & ~ignore
+        if f:
+            msgs = [m for b, m in nat.ERR_FLAGS.items() if f & b]
+            raise ValueError("reference exception reproduced on device: " + "; ".join(msgs))
+
+    def extrapolate(self, p: Params):
+        cp = self.cparams(p)
+        nat.check(self.lib.gtf_extrapolate(ctypes.byref(self.cg), ctypes.byref(self.cn), ctypes.byref(self.cuts),
+                                           ctypes.byref(self.ce), ctypes.byref(cp), self.ptr("ws"), self.stream))
+
+    def update(self, p: Params):
+        cp = self.cparams(p)
+        nat.check(self.lib.gtf_update(ctypes.byref(self.cg), ctypes.byref(self.cn), ctypes.byref(self.ctse),
+                                      ctypes.byref(self.cuts), ctypes.byref(self.ce), ctypes.byref(cp),
+                                      self.ptr("ws"), self.stream))
+
+    def cluster(self, key: str, chi2: float, kl: float, p: Params):
+        cp = self.cparams(p)
+        st = self.cuts if key in ("uts", "updated_track_states") else self.ctse
+        k = 1 if st is self.cuts else 0
+        nat.check(self.lib.gtf_cluster(ctypes.byref(self.cg), ctypes.byref(self.cn), ctypes.byref(st),
+                                       ctypes.byref(self.ce), k, float(chi2), float(kl), ctypes.byref(cp),
+                                       self.ptr("ws"), self.stream))
+
+    def full_pass(self, p: Params):
+        cp = self.cparams(p)
+        nat.check(self.lib.gtf_pass(ctypes.byref(self.cg), ctypes.byref(self.cn), ctypes.byref(self.ctse),
+                                    ctypes.byref(self.cuts), ctypes.byref(self.ce), ctypes.byref(cp),
+                                    self.ptr("ws"), self.stream))
+
+    # ------------------------------------------------------- tag propagation
+    def tag_propagation(self, tags, radius, threshold=0.1, max_sweeps=100000):
+        """Jacobi sweeps until flips / processed <= threshold (tag_propagation.py:137)."""
+        torch = self.torch
+        dev = self.device
+        E = self.n_edges
+        keep = torch.zeros(max(E, 1), dtype=torch.uint8, device=dev)
+        proc = torch.zeros(max(self.n_nodes, 1), dtype=torch.uint8, device=dev)
+        cnt = torch.zeros(2, dtype=torch.int32, device=dev)
+        r = torch.from_numpy(np.ascontiguousarray(radius, dtype=np.float64)).to(dev)
+        ta = torch.from_numpy(np.ascontiguousarray(tags, dtype=np.int64)).to(dev)
+        tb = torch.empty_like(ta)
+        vp = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        nat.check(self.lib.gtf_tag_prepare(ctypes.byref(self.cg), vp(r), vp(keep), vp(proc), vp(cnt), self.stream))
+        total = int(cnt[0].item())
+        flips_hist = []
+        frac = 1.0
+        flips = cnt[1:2]
+        while frac > threshold and len(flips_hist) < max_sweeps:
+            nat.check(self.lib.gtf_tag_sweep(ctypes.byref(self.cg), vp(keep), vp(proc), vp(ta), vp(tb), vp(flips),
+                                             self.stream))
+            f = int(flips.item())
+            flips_hist.append(f)
+            frac = f / total if total else 0.0
+            ta, tb = tb, ta
+        return ta.cpu().numpy(), flips_hist
+
+    # ---------------------------------------------------------------- results
+    def download(self, g: TrackGraph) -> TrackGraph:
+        """copy the mutable arrays back into the host TrackGraph (in place)"""
+        for f in MUTABLE_NODE:
+            g.node[f][...] = self.t[f].cpu().numpy().reshape(g.node[f].shape)
+        for f in SLOT_FIELDS:
+            if f in STATIC_SLOT or f == "slot_key":
+                continue
+            g.slot[f][...] = self.t[f].cpu().numpy().reshape(g.slot[f].shape)
+        return g
+
+    def snapshot(self):
+        """device-side copy of every mutable array (bench: restore between steps)"""
+        return {k: v.clone() for k, v in self.t.items() if k in MUTABLE_NODE or
+                (k in SLOT_FIELDS and k not in STATIC_SLOT and k != "slot_key")}
+
+    def restore(self, snap):
+        for k, v in snap.items():
+            self.t[k].copy_(v, non_blocking=True)

@@ -1,0 +1,223 @@
+"""Seeded TrackML-shaped synthetic events, generated straight into the packed layout.
+
+There is no network and the raw TrackML files are absent, so the benchmark
+configs (C2 ~30k hits / ~90k directed edges, C3 = 64 of them
+fused, C4 pileup-200 ~170k hits / ~1M edges) are synthesised:
+
+* helical tracks from the origin region (pT log-uniform 0.4-10 GeV, B = 2 T,
+  |eta| < 2.5) crossing cylindrical barrel layers and endcap disks of a
+  TrackML-like geometry; one node per hit, Gaussian smearing 0.05 mm;
+* directed edges in both directions between consecutive hits of a track, plus
+  fake edges to hits with a nearby azimuth on the same target layer, tuned to
+  the committed 800' event's E/N ~ 3.0;
+* per node the reference's initial state (helper.compute_track_state_estimates
+  math for its first neighbour, helper.py:238-452, vectorised) as the "full
+  load" merged state (every node extrapolates), all edges active,
+  track_state_estimates keys = all neighbours with mixture weight 1/degree
+  (helper.py:76-96).
+
+Node order: by layer, then azimuth (the reference's CSVs are layer-sorted).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+from .graph import TrackGraph, NODE_FIELDS, SLOT_FIELDS, empty_arrays, check_layout, concat
+
+# TrackML-like geometry (mm)
+BARREL_R = np.array([32., 72., 116., 172., 260., 360., 500., 660., 820., 1020.])
+BARREL_HALF_Z = np.array([490., 490., 490., 490., 1080., 1080., 1080., 1080., 1080., 1080.])
+ENDCAP_Z = np.array([600., 700., 820., 960., 1100., 1300., 1500., 1750., 2000., 2300., 2600., 2950.])
+ENDCAP_RMIN = np.array([30.] * 7 + [230.] * 5)
+ENDCAP_RMAX = np.array([175.] * 7 + [1000.] * 5)
+
+
+def _track_hits(rng, n_tracks, sigma=0.05):
+    """returns hit arrays (x, y, z, layer_code, track, order-along-track)"""
+    pt = np.exp(rng.uniform(np.log(0.4), np.log(10.0), n_tracks))
+    q = rng.choice([-1.0, 1.0], n_tracks)
+    phi0 = rng.uniform(-np.pi, np.pi, n_tracks)
+    eta = rng.uniform(-2.5, 2.5, n_tracks)
+    cot = np.sinh(eta)
+    z0 = rng.normal(0.0, 5.5, n_tracks)
+    R = pt / (0.3 * 2.0) * 1000.0   # helix radius (mm)
+
+    xs, ys, zs, lay, trk, s_all = [], [], [], [], [], []
+    # barrel crossings
+    for li, (rho, hz) in enumerate(zip(BARREL_R, BARREL_HALF_Z)):
+        ok = rho < 2 * R
+        arg = np.clip(rho / (2 * R), -1, 1)
+        psi = np.arcsin(arg)
+        s = 2 * R * psi
+        z = z0 + cot * s
+        ok &= np.abs(z) < hz
+        phi = phi0 + q * psi
+        idx = np.nonzero(ok)[0]
+        xs.append(rho * np.cos(phi[idx])); ys.append(rho * np.sin(phi[idx])); zs.append(z[idx])
+        lay.append(np.full(idx.size, 8000 + 2 * (li + 1))); trk.append(idx); s_all.append(s[idx])
+    # endcap crossings
+    for di, (zd, rmin, rmax) in enumerate(zip(ENDCAP_Z, ENDCAP_RMIN, ENDCAP_RMAX)):
+        for sign in (-1.0, 1.0):
+            zt = sign * zd
+            with np.errstate(divide="ignore", invalid="ignore"):
+                s = (zt - z0) / cot
+            ok = (s > 0) & (s < np.pi * R)
+            psi = np.where(ok, s / (2 * R), 0.0)
+            rho = 2 * R * np.sin(psi)
+            ok &= (rho > rmin) & (rho < rmax) & (psi < np.pi / 2)
+            phi = phi0 + q * psi
+            idx = np.nonzero(ok)[0]
+            vol = 7 if sign < 0 else 9
+            code = vol * 1000 + 2 * (di + 1)
+            xs.append(rho[idx] * np.cos(phi[idx])); ys.append(rho[idx] * np.sin(phi[idx]))
+            zs.append(np.full(idx.size, zt)); lay.append(np.full(idx.size, code)); trk.append(idx)
+            s_all.append(s[idx])
+    x = np.concatenate(xs); y = np.concatenate(ys); z = np.concatenate(zs)
+    layer = np.concatenate(lay); track = np.concatenate(trk); s = np.concatenate(s_all)
+    x = x + rng.normal(0, sigma, x.size); y = y + rng.normal(0, sigma, y.size)
+    z = z + rng.normal(0, sigma, z.size) * (np.abs(z) < 1100)
+    return x, y, z, layer, track, s
+
+
+def _initial_state(gn, gb, p):
+    """helper.compute_track_state_estimates math (helper.py:243-425) for one
+    (node, neighbour) pair, vectorised. Returns state (n,3), cov5 (n,5)."""
+    xA, yA, zA, rA = gn[:, 0], gn[:, 1], gn[:, 2], gn[:, 3]
+    xk, yk, zk, rk = gb[:, 0], gb[:, 1], gb[:, 2], gb[:, 3]
+    ang = np.arctan2(yA, xA)
+    ca, sa = np.cos(ang), np.sin(ang)
+    x0 = (0 - xA) * ca + (0 - yA) * sa
+    xB = (xk - xA) * ca + (yk - yA) * sa
+    mB = -(xk - xA) * sa + (yk - yA) * ca
+    n = gn.shape[0]
+    H = np.zeros((n, 3, 3))
+    H[:, 0, 0] = 0.5 * x0**2; H[:, 0, 1] = x0; H[:, 0, 2] = 1
+    H[:, 1, 2] = 1
+    H[:, 2, 0] = 0.5 * xB**2; H[:, 2, 1] = xB; H[:, 2, 2] = 1
+    Hi = np.linalg.inv(H)
+    sv = Hi @ np.stack([np.zeros(n), np.zeros(n), mB], axis=1)[:, :, None]
+    sv = sv[:, :, 0]
+    S = np.diag([4.0**2, p.sigma0xy**2, p.sigma0xy**2])
+    cov = Hi @ S @ np.transpose(Hi, (0, 2, 1))
+    a, b = sv[:, 0], sv[:, 1]
+    dr = rA - rk
+    dz = zA - zk
+    hyp = np.sqrt(dr**2 + dz**2)
+    sin_t = np.abs(dr) / hyp
+    kappa = (2 * a) / (1 + ((2 * a * xk) + b)**2)**1.5
+    var_ms = sin_t * ((13.6 * 1e-3 * np.sqrt(0.02) * kappa) / 0.3)**2
+    endc = np.abs(zA) >= p.endcap_boundary
+    with np.errstate(divide="ignore", invalid="ignore"):
+        var_ms = np.where(endc, var_ms * np.abs(dr / dz), var_ms)
+    sz = np.where(endc, p.sigma0rz, p.sigma0rz2); sr = np.where(endc, p.sigma0rz2, p.sigma0rz)
+    szn = np.where(np.abs(zk) >= p.endcap_boundary, p.sigma0rz, p.sigma0rz2)
+    srn = np.where(np.abs(zk) >= p.endcap_boundary, p.sigma0rz2, p.sigma0rz)
+    d = rA - rk
+    J = np.stack([1 / d, -1 / d, -(zA - zk) / d**2, (zA - zk) / d**2], axis=1)
+    cov_tau = (J**2 * np.stack([sz**2, szn**2, sr**2, srn**2], axis=1)).sum(1)
+    c5 = np.stack([cov[:, 0, 0], cov[:, 0, 1], cov[:, 1, 0], cov[:, 1, 1] + var_ms, cov_tau**2 + var_ms], axis=1)
+    return sv, c5
+
+
+def event(seed: int = 0, n_tracks: int = 3300, fake_per_edge: float = 0.55, params=None) -> TrackGraph:
+    """One synthetic event. n_tracks 3300 ~ C2 (30k hits, 90k directed edges);
+    18700 ~ C4 pileup-200 (~170k hits, ~1M directed edges)."""
+    from .params import Params
+    p = params or Params()
+    rng = np.random.default_rng(seed)
+    x, y, z, layer, track, s = _track_hits(rng, n_tracks)
+    r = np.sqrt(x**2 + y**2)
+    phi = np.arctan2(y, x)
+    order = np.lexsort((phi, layer))
+    x, y, z, r, phi, layer, track, s = (a[order] for a in (x, y, z, r, phi, layer, track, s))
+    N = x.size
+    # consecutive hits along each track (by path length) -> true edges
+    o2 = np.lexsort((s, track))
+    same = track[o2][1:] == track[o2][:-1]
+    a_true = o2[:-1][same]
+    b_true = o2[1:][same]
+    # fake edges: from the source of a true edge to an azimuthal neighbour on the target layer
+    nf = rng.binomial(1, min(fake_per_edge, 1.0), a_true.size).astype(bool)
+    fa, fb = a_true[nf], b_true[nf]
+    off = rng.choice([-2, -1, 1, 2], fa.size)
+    cand = np.clip(fb + off, 0, N - 1)
+    okf = (layer[cand] == layer[fb]) & (cand != fa)
+    fa, fb = fa[okf], cand[okf]
+    ua = np.concatenate([a_true, fa]); ub = np.concatenate([b_true, fb])
+    lo, hi = np.minimum(ua, ub), np.maximum(ua, ub)
+    key = np.unique(lo.astype(np.int64) * N + hi)
+    lo, hi = (key // N).astype(np.int64), (key % N).astype(np.int64)
+    # both directions; successor order = edge insertion order (helper.py:512-518)
+    src = np.concatenate([lo, hi]); dst = np.concatenate([hi, lo])
+    E = src.size
+
+    g = _assemble(N, src, dst, x, y, z, r, layer, p)
+    return g
+
+
+def _assemble(N, src, dst, x, y, z, r, layer, p) -> TrackGraph:
+    E = src.size
+    # slots: receiver-major, sorted by sender index
+    so = np.lexsort((src, dst))
+    slot_src = src[so].astype(np.int32)
+    slot_dst = dst[so].astype(np.int64)
+    slot_ptr = np.zeros(N + 1, np.int64)
+    np.add.at(slot_ptr, slot_dst + 1, 1)
+    slot_ptr = np.cumsum(slot_ptr)
+    slot_of_edge = np.empty(E, np.int64)
+    slot_of_edge[so] = np.arange(E)
+    # out view: successors in insertion order (stable by source)
+    oo = np.argsort(src, kind="stable")
+    out_ptr = np.zeros(N + 1, np.int64)
+    np.add.at(out_ptr, src.astype(np.int64) + 1, 1)
+    out_ptr = np.cumsum(out_ptr)
+    out_slot = slot_of_edge[oo].astype(np.int32)
+
+    node = empty_arrays(NODE_FIELDS, N)
+    slot = empty_arrays(SLOT_FIELDS, E)
+    gnn = np.stack([x, y, z, r], axis=1)
+    node["gnn"] = gnn
+    node["xyzr"] = gnn.copy()
+    node["layer"] = (layer % 100).astype(np.float64)
+    deg = np.diff(slot_ptr)
+    node["has_tse"] = (deg > 0).astype(np.uint8)
+    node["tag"] = np.arange(N, dtype=np.int64)
+    node["node_id"] = np.arange(N, dtype=np.int64)
+    node["sub_id"] = np.zeros(N, np.int32)
+    node["degree"] = deg.astype(np.int32)
+    slot["slot_src"] = slot_src
+    slot["slot_key"] = slot_src.astype(np.int64)
+    slot["is_edge"][:] = 1
+    slot["rev_edge"][:] = 1
+    slot["act"][:] = 1
+    slot["tse_rank"] = (np.arange(E) - slot_ptr[slot_dst]).astype(np.int32)
+    slot["tse_mw"] = 1.0 / deg[slot_dst]
+    slot["send_mw"] = 1.0 / deg[slot_src]
+    slot["tse_xyzr"] = gnn[slot_src]
+    # full load: merged state = initial state towards the node's first neighbour
+    has = deg > 0
+    first_nb = slot_src[np.minimum(slot_ptr[:-1], E - 1)]
+    vv = np.nonzero(has)[0]
+    sv, c5 = _initial_state(gnn[vv], gnn[first_nb[vv]], p)
+    node["has_merged"][vv] = 1
+    node["merged_state"][vv] = sv
+    node["merged_cov"][vv] = c5
+    node["merged_prior"][vv] = 1.0
+    g = TrackGraph(N, E, slot_ptr.astype(np.int32), out_ptr.astype(np.int32), out_slot, node, slot, 1)
+    check_layout(g)
+    return g
+
+
+def workload(name: str, seed: int = 0) -> TrackGraph:
+    """Benchmark configs of BASELINE.json."""
+    if name == "c2":
+        return event(seed, 3300)
+    if name == "c3":
+        return concat([event(seed + i, 3300) for i in range(64)])
+    if name == "c4":
+        return event(seed, 18700)
+    if name.startswith("tiny"):
+        return event(seed, int(name[4:] or 200))
+    raise ValueError("unknown workload %r (c2, c3, c4, tinyN)" % name)

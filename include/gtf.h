@@ -1,0 +1,149 @@
+/*
+ * gtf.h -- C-ABI of libgtf.so, the MI355X (gfx950) edge-parallel track-finding
+ * pass that drops in behind nishalad95/GNN-track-finding's hot path.
+ *
+ * Every pointer in the structs below is a DEVICE pointer (HBM) owned by the
+ * caller; the library keeps no pointer after a call returns and allocates
+ * nothing on the hot path (scratch comes from the caller's workspace). All
+ * calls are stream-ordered on the hipStream_t passed in (0 = null stream).
+ * Return value: 0 = OK, < 0 = error (gtf_last_error() has the message).
+ * Reference-semantics exceptions detected on the device (the places where the
+ * reference itself raises) are reported as bit flags in the workspace error
+ * word; read them with gtf_read_errors().
+ *
+ * Which reference interface each entry point replaces (file:line in the
+ * reference repository):
+ *   gtf_extrapolate  -> src/extrapolate/extrapolate_merged_states.py:552-566
+ *                       (message_passing :406-451 + extrapolate_validate :26-402,
+ *                        compute_prior_probabilities + reweight x2, node degree)
+ *   gtf_update       -> src/update/remove_state_metadata.py:29-53
+ *   gtf_cluster      -> src/clustering/clustering.py:181-373 (cluster body)
+ *   gtf_pass         -> the three above back to back, one fused node kernel
+ *                       (run_gnn_trackml_mod.sh:101,138,112 stage order)
+ *   gtf_tag_sweep    -> tag_propagation/tag_propagation.py:137-164 (one sweep)
+ *   gtf_tag_prepare  -> tag_propagation/tag_propagation.py:97-110
+ */
+#ifndef GTF_H
+#define GTF_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* gtf_stream_t; /* a hipStream_t */
+
+/* ---- graph structure (read-only on the path) ------------------------------ */
+typedef struct gtf_graph {
+    int32_t n_nodes;
+    int32_t n_slots;          /* slots = (receiver, sender) pairs, receiver-major */
+    int32_t n_edges;          /* directed edges = slots with is_edge == 1 */
+    int32_t pad_;
+    const int32_t* slot_ptr;  /* [N+1] slot segment of each receiver */
+    const int32_t* slot_src;  /* [S]   sender node index, -1 = orphan state key */
+    const int32_t* slot_dst;  /* [S]   receiver node index */
+    const int32_t* out_ptr;   /* [N+1] out-edge segment of each sender */
+    const int32_t* out_slot;  /* [E]   slot of each out-edge, successor order */
+    const uint8_t* is_edge;   /* [S]   edge sender->receiver exists */
+    const uint8_t* rev_edge;  /* [S]   edge receiver->sender exists */
+    const uint8_t* solo;      /* [N]   node is alone in its subgraph */
+    const double*  gnn;       /* [N*4] GNN_Measurement x,y,z,r */
+    const double*  xyzr;      /* [N*4] node attribute 'xyzr' */
+    const double*  layer;     /* [N]   in_volume_layer_id */
+} gtf_graph;
+
+/* ---- per-node mutable state ------------------------------------------------ */
+typedef struct gtf_nodes {
+    uint8_t* has_merged;      /* [N] */
+    double*  merged_state;    /* [N*3] a, b, c */
+    double*  merged_cov;      /* [N*5] c00 c01 c10 c11 c22 (block diagonal) */
+    double*  merged_prior;    /* [N] */
+    uint8_t* has_tse;         /* [N] node has a 'track_state_estimates' dict */
+    uint8_t* has_uts;         /* [N] node has an 'updated_track_states' dict */
+    int32_t* degree;          /* [N] */
+} gtf_nodes;
+
+/* ---- one state dict (track_state_estimates or updated_track_states) -------- */
+typedef struct gtf_states {
+    int32_t* rank;            /* [S] dict position, -1 = key absent */
+    double*  sv;              /* [S*3] edge_state_vector a, b, c */
+    double*  tau;             /* [S]   joint_vector[2] */
+    double*  cov;             /* [S*5] c00 c01 c10 c11 c22 */
+    double*  xyzr;            /* [S*4] sender coordinates stored in the state */
+    double*  lik;             /* [S]   likelihood (UTS only) */
+    double*  mw;              /* [S]   mixture_weight */
+    double*  prior;           /* [S]   prior */
+    double*  lr;              /* [S]   lr_layer_norm (UTS only) */
+    int8_t*  side;            /* [S]   0 left, 1 right (UTS only) */
+    uint8_t* fresh;           /* [S]   entry written by the last message passing (UTS only) */
+} gtf_states;
+
+/* ---- per-edge attributes (stored per slot) --------------------------------- */
+typedef struct gtf_edges {
+    uint8_t*      act;        /* [S] 'activated' */
+    double*       edge_mw;    /* [S] edge 'mixture_weight' */
+    const double* send_mw;    /* [S] sender's track_state_estimates[receiver]['mixture_weight'] */
+} gtf_edges;
+
+typedef struct gtf_params {
+    double sigma0xy;          /* -e */
+    double sigma0rz;          /* -z */
+    double sigma0rz2;         /* -m */
+    double endcap_boundary;   /* -b */
+    double chi2_cut;          /* extrapolation gate -c (extrapolate_merged_states.py:298) */
+    double reweight_threshold;/* 0.1 (helper.py:145) */
+    double cluster_chi2;      /* clustering -c (clustering.py:228) */
+    double cluster_kl;        /* clustering -k (clustering.py:261) */
+} gtf_params;
+
+/* Device-detected reference exceptions (bit flags in the error word). */
+enum {
+    GTF_ERR_SEND_MW_MISSING = 1,   /* KeyError extrapolate_merged_states.py:384 */
+    GTF_ERR_STALE_KEY_NO_EDGE = 2, /* KeyError helper.py:131/138 */
+    GTF_ERR_ALL_ZERO_DIST = 4,     /* ValueError clustering.py:120 (np.min of empty) */
+    GTF_ERR_TIE_EMPTIED = 8,       /* ValueError clustering.py:116 (tie removed every state) */
+    GTF_ERR_EMPTY_DICT_MW = 16,    /* ZeroDivisionError helper.py:90 */
+    GTF_ERR_NAN_KL = 32,           /* ValueError clustering.py:117 (list.index of NaN) */
+    GTF_ERR_NO_STATE_DICT = 64     /* KeyError remove_state_metadata.py:39 */
+};
+
+/* Workspace: caller allocates gtf_workspace_bytes() bytes of device memory. */
+size_t gtf_workspace_bytes(int32_t n_nodes, int32_t n_slots);
+
+/* Zero the error word (stream-ordered). */
+int gtf_clear_errors(void* workspace, gtf_stream_t stream);
+/* Copy the error word to the host (synchronises the stream). */
+int gtf_read_errors(void* workspace, uint32_t* flags, gtf_stream_t stream);
+
+int gtf_extrapolate(const gtf_graph* g, gtf_nodes* n, gtf_states* uts, gtf_edges* e,
+                    const gtf_params* p, void* workspace, gtf_stream_t stream);
+int gtf_update(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts, gtf_edges* e,
+               const gtf_params* p, void* workspace, gtf_stream_t stream);
+/* key: 0 = cluster track_state_estimates, 1 = updated_track_states. Where a
+ * distance tie empties the state list the reference raises ValueError; here the
+ * node keeps the merged state formed so far and GTF_ERR_TIE_EMPTIED is set. */
+int gtf_cluster(const gtf_graph* g, gtf_nodes* n, gtf_states* states, gtf_edges* e, int32_t key,
+                double chi2_threshold, double kl_threshold, const gtf_params* p, void* workspace,
+                gtf_stream_t stream);
+/* extrapolate -> update -> cluster(updated_track_states, p->cluster_chi2, p->cluster_kl) */
+int gtf_pass(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts, gtf_edges* e,
+             const gtf_params* p, void* workspace, gtf_stream_t stream);
+
+/* Tag propagation. radius: [N] node radius (attr 'zr'[1]); keep: [E] output mask of
+ * kept inward neighbours per out-edge (u8, indexed by out-edge position);
+ * processed: [N] u8 output; n_processed: device int32 output. */
+int gtf_tag_prepare(const gtf_graph* g, const double* radius, uint8_t* keep, uint8_t* processed,
+                    int32_t* n_processed, gtf_stream_t stream);
+/* one Jacobi sweep: tags_out[u] = max(tags_in[u], tags_in[kept neighbours]); flips += changes */
+int gtf_tag_sweep(const gtf_graph* g, const uint8_t* keep, const uint8_t* processed,
+                  const int64_t* tags_in, int64_t* tags_out, int32_t* flips, gtf_stream_t stream);
+
+const char* gtf_last_error(void);
+const char* gtf_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GTF_H */

@@ -1,0 +1,73 @@
+"""HIP path (through the C-ABI) vs the pinned oracle and the reference fixtures.
+
+Bar: activation masks, dict membership/order (ranks), merged flags and degree
+bit-exact; floats within 1e-6 relative (north star tolerance).
+"""
+import numpy as np
+import pytest
+
+import gtf_oracle as O
+from compare import compare
+from fixtures import load, expected_graph
+from gtf.params import Params
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-6
+
+
+def _params(meta):
+    return Params(sigma0xy=meta["sigma0xy"], sigma0rz=meta["sigma0rz"], sigma0rz2=meta["sigma0rz2"],
+                  endcap_boundary=meta["endcap_boundary"], chi2_cut=meta.get("chi2_cut", 2.0),
+                  cluster_chi2=meta.get("chi2", 1000.0), cluster_kl=meta.get("kl", 100.0))
+
+
+def _dev(g):
+    from gtf.device import DeviceGraph
+    return DeviceGraph(g)
+
+
+def _run(name, fn):
+    g, out, extra, meta = load(name)
+    exp = expected_graph(g, out)
+    p = _params(meta)
+    d = _dev(g)
+    d.clear_errors()
+    fn(d, p, meta)
+    d.raise_errors()
+    got = d.download(g.copy())
+    errs = compare(got, exp, rtol=RTOL)
+    assert errs == [], "\n".join(errs)
+    return got
+
+
+def test_extrapolate_it2():
+    _run("extrapolate_it2", lambda d, p, m: d.extrapolate(p))
+
+
+def test_extrapolate_full_load():
+    _run("extrapolate_full", lambda d, p, m: d.extrapolate(p))
+
+
+def test_update_with_orphans():
+    _run("update_it2", lambda d, p, m: d.update(p))
+
+
+def test_cluster_tse():
+    _run("cluster_tse", lambda d, p, m: d.cluster("tse", m["chi2"], m["kl"], p))
+
+
+def test_cluster_uts():
+    _run("cluster_uts", lambda d, p, m: d.cluster("uts", m["chi2"], m["kl"], p))
+
+
+def test_full_pass_fused():
+    _run("pass_full", lambda d, p, m: d.full_pass(p))
+
+
+def test_tag_propagation():
+    g, _, extra, _ = load("tags_vol7")
+    d = _dev(g)
+    tags, flips = d.tag_propagation(g.node["tag"], g.node["xyzr"][:, 3])
+    assert list(flips) == list(extra["flips"])
+    kept = extra["tags"] >= 0
+    assert np.array_equal(tags[kept], extra["tags"][kept])

@@ -596,15 +596,30 @@ int gtf_cluster(const gtf_graph* g, gtf_nodes* n, gtf_states* states, gtf_edges*
                        chi2_threshold, kl_threshold, (hipStream_t)stream);
 }
 
-int gtf_pass(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts, gtf_edges* e,
-             const gtf_params* p, void* ws, gtf_stream_t stream) {
+int gtf_pass_ev(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts, gtf_edges* e,
+                const gtf_params* p, void* ws, gtf_stream_t stream, void* const* events) {
     int rc = check_graph(g);
     if (rc) return rc;
+    hipStream_t st = (hipStream_t)stream;
     Ws w = carve(ws, g->n_nodes, g->n_slots);
-    rc = launch_extrap_edges(g, n, uts, e, p, w, (hipStream_t)stream);
-    if (rc) return rc;
-    return launch_node(g, n, tse, uts, e, p, w, ST_EXTRAP | ST_UPDATE | ST_CLUSTER, 1, p->cluster_chi2,
-                       p->cluster_kl, (hipStream_t)stream);
+    if (events) (void)hipEventRecord((hipEvent_t)events[0], st);
+    if (g->n_nodes > 0)
+        hipLaunchKernelGGL(k_sender_scan, dim3(grid(g->n_nodes)), dim3(BLOCK), 0, st, *g, *n, *e, *p, w);
+    if (events) (void)hipEventRecord((hipEvent_t)events[1], st);
+    if (g->n_slots > 0)
+        hipLaunchKernelGGL(k_extrapolate, dim3(grid(g->n_slots)), dim3(BLOCK), 0, st, *g, *n, *uts, *e, *p, w);
+    if (events) (void)hipEventRecord((hipEvent_t)events[2], st);
+    hipError_t err = hipGetLastError();
+    if (err != hipSuccess) return fail("extrapolate launch", err);
+    rc = launch_node(g, n, tse, uts, e, p, w, ST_EXTRAP | ST_UPDATE | ST_CLUSTER, 1, p->cluster_chi2,
+                     p->cluster_kl, st);
+    if (events) (void)hipEventRecord((hipEvent_t)events[3], st);
+    return rc;
+}
+
+int gtf_pass(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts, gtf_edges* e,
+             const gtf_params* p, void* ws, gtf_stream_t stream) {
+    return gtf_pass_ev(g, n, tse, uts, e, p, ws, stream, nullptr);
 }
 
 const char* gtf_last_error(void) { return g_err; }

@@ -52,7 +52,7 @@ ERR_FLAGS = {
 
 # exported symbols (must match include/gtf.h; tests check the .so exports all of them)
 SYMBOLS = ["gtf_workspace_bytes", "gtf_clear_errors", "gtf_read_errors", "gtf_extrapolate", "gtf_update",
-           "gtf_cluster", "gtf_pass", "gtf_tag_prepare", "gtf_tag_sweep", "gtf_last_error", "gtf_version"]
+           "gtf_cluster", "gtf_pass", "gtf_pass_ev", "gtf_tag_prepare", "gtf_tag_sweep", "gtf_last_error", "gtf_version"]
 
 _lib = None
 
@@ -76,11 +76,13 @@ def lib():
     L.gtf_update.argtypes = [G, N, S, S, E, PR, P, P]
     L.gtf_cluster.argtypes = [G, N, S, E, I32, F64, F64, PR, P, P]
     L.gtf_pass.argtypes = [G, N, S, S, E, PR, P, P]
+    L.gtf_pass_ev.argtypes = [G, N, S, S, E, PR, P, P, ctypes.POINTER(P)]
     L.gtf_tag_prepare.argtypes = [G, P, P, P, P, P]
     L.gtf_tag_sweep.argtypes = [G, P, P, P, P, P, P]
     L.gtf_last_error.restype = ctypes.c_char_p
     L.gtf_version.restype = ctypes.c_char_p
     for fn in ("gtf_clear_errors", "gtf_read_errors", "gtf_extrapolate", "gtf_update", "gtf_cluster", "gtf_pass",
+               "gtf_pass_ev",
                "gtf_tag_prepare", "gtf_tag_sweep"):
         getattr(L, fn).restype = ctypes.c_int
     _lib = L

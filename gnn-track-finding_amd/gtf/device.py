@@ -132,11 +132,18 @@ class DeviceGraph:
                                        ctypes.byref(self.ce), k, float(chi2), float(kl), ctypes.byref(cp),
                                        self.ptr("ws"), self.stream))
 
-    def full_pass(self, p: Params):
+    def full_pass(self, p: Params, events=None):
+        """events: optional 4 raw hipEvent_t handles (per-kernel timing)"""
         cp = self.cparams(p)
-        nat.check(self.lib.gtf_pass(ctypes.byref(self.cg), ctypes.byref(self.cn), ctypes.byref(self.ctse),
-                                    ctypes.byref(self.cuts), ctypes.byref(self.ce), ctypes.byref(cp),
-                                    self.ptr("ws"), self.stream))
+        if events is None:
+            nat.check(self.lib.gtf_pass(ctypes.byref(self.cg), ctypes.byref(self.cn), ctypes.byref(self.ctse),
+                                        ctypes.byref(self.cuts), ctypes.byref(self.ce), ctypes.byref(cp),
+                                        self.ptr("ws"), self.stream))
+        else:
+            arr = (ctypes.c_void_p * 4)(*events)
+            nat.check(self.lib.gtf_pass_ev(ctypes.byref(self.cg), ctypes.byref(self.cn), ctypes.byref(self.ctse),
+                                           ctypes.byref(self.cuts), ctypes.byref(self.ce), ctypes.byref(cp),
+                                           self.ptr("ws"), self.stream, arr))
 
     # ------------------------------------------------------- tag propagation
     def tag_propagation(self, tags, radius, threshold=0.1, max_sweeps=100000):
@@ -176,10 +183,15 @@ class DeviceGraph:
             g.slot[f][...] = self.t[f].cpu().numpy().reshape(g.slot[f].shape)
         return g
 
-    def snapshot(self):
-        """device-side copy of every mutable array (bench: restore between steps)"""
-        return {k: v.clone() for k, v in self.t.items() if k in MUTABLE_NODE or
-                (k in SLOT_FIELDS and k not in STATIC_SLOT and k != "slot_key")}
+    # arrays whose values decide how much work the next pass does: restoring
+    # them makes every benchmark step process the same input
+    PASS_INPUTS = ("act", "uts_rank", "has_uts", "has_merged", "merged_state", "merged_cov", "merged_prior")
+
+    def snapshot(self, names=None):
+        """device-side copy of mutable arrays (default: every one)"""
+        names = names or [k for k in self.t if k in MUTABLE_NODE or
+                          (k in SLOT_FIELDS and k not in STATIC_SLOT and k != "slot_key")]
+        return {k: self.t[k].clone() for k in names}
 
     def restore(self, snap):
         for k, v in snap.items():

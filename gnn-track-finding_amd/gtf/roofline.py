@@ -1,0 +1,32 @@
+"""Algorithmic bytes per kernel launch (SURVEY.md §8d byte model, fp64 SoA).
+
+Per pass the survey prices B_alg = 183 B per directed edge + 290 B per node:
+  * extrapolation side (k_sender_scan + k_extrapolate): 94 B per directed edge
+    (read receiver index 4, activation 1, sender TSE mixture weight 8; write
+    state 24, covariance 4 x 8 = 32, tau 8, likelihood 8, weight 8, activation 1)
+    + 104 B per node (GNN coordinates 32, merged state 24, merged covariance 40,
+    write-back of merged_cov[1,1] 8);
+  * fused node kernel (priors, side norm, reweight x2, update, KL clustering):
+    89 B per directed edge (re-read state 3 + 4 doubles = 56, sender coordinates
+    32, deactivation 1) + 186 B per node (xyzr 32, flags/layer 2, merged outputs
+    2 x (3 + 6) x 8 = 144, degree 8).
+Sums: 183 E + 290 N. DESIGN.md "Roofline" states these figures.
+"""
+
+EXTRAP_PER_EDGE, EXTRAP_PER_NODE = 94, 104
+NODE_PER_EDGE, NODE_PER_NODE = 89, 186
+PASS_PER_EDGE, PASS_PER_NODE = 183, 290
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def extrap_bytes(n_edges, n_nodes):
+    return EXTRAP_PER_EDGE * n_edges + EXTRAP_PER_NODE * n_nodes
+
+
+def node_bytes(n_edges, n_nodes):
+    return NODE_PER_EDGE * n_edges + NODE_PER_NODE * n_nodes
+
+
+def pass_bytes(n_edges, n_nodes):
+    return PASS_PER_EDGE * n_edges + PASS_PER_NODE * n_nodes

@@ -121,7 +121,8 @@ def _initial_state(gn, gb, p):
     return sv, c5
 
 
-def event(seed: int = 0, n_tracks: int = 3300, fake_per_edge: float = 0.55, params=None) -> TrackGraph:
+def event(seed: int = 0, n_tracks: int = 3300, fake_mean: float = 0.55, drop_true: float = 0.2,
+          spread: float = 1.3, params=None) -> TrackGraph:
     """One synthetic event. n_tracks 3300 ~ C2 (30k hits, 90k directed edges);
     18700 ~ C4 pileup-200 (~170k hits, ~1M directed edges)."""
     from .params import Params
@@ -138,10 +139,17 @@ def event(seed: int = 0, n_tracks: int = 3300, fake_per_edge: float = 0.55, para
     same = track[o2][1:] == track[o2][:-1]
     a_true = o2[:-1][same]
     b_true = o2[1:][same]
-    # fake edges: from the source of a true edge to an azimuthal neighbour on the target layer
-    nf = rng.binomial(1, min(fake_per_edge, 1.0), a_true.size).astype(bool)
-    fa, fb = a_true[nf], b_true[nf]
-    off = rng.choice([-2, -1, 1, 2], fa.size)
+    # track-finding inefficiency: drop a few true segments (-> more degree-1 ends)
+    keep_t = rng.random(a_true.size) > drop_true
+    a_true, b_true = a_true[keep_t], b_true[keep_t]
+    # fake edges with a heavy-tailed count per true segment: from its source to
+    # azimuthal neighbours of its target on the target layer
+    # per-source mean drawn log-normally: dense-region hubs give the long degree tail
+    mean_i = fake_mean * rng.lognormal(-0.5 * spread**2, spread, N)[a_true]
+    k = rng.geometric(1.0 / (1.0 + mean_i)) - 1
+    fa = np.repeat(a_true, k)
+    fb = np.repeat(b_true, k)
+    off = rng.integers(1, 20, fa.size) * rng.choice([-1, 1], fa.size)
     cand = np.clip(fb + off, 0, N - 1)
     okf = (layer[cand] == layer[fb]) & (cand != fa)
     fa, fb = fa[okf], cand[okf]
@@ -182,10 +190,14 @@ def _assemble(N, src, dst, x, y, z, r, layer, p) -> TrackGraph:
     node["xyzr"] = gnn.copy()
     node["layer"] = (layer % 100).astype(np.float64)
     deg = np.diff(slot_ptr)
-    node["has_tse"] = (deg > 0).astype(np.uint8)
+    node["has_tse"][:] = 1          # every node gets a (possibly empty) dict (helper.py:444)
     node["tag"] = np.arange(N, dtype=np.int64)
     node["node_id"] = np.arange(N, dtype=np.int64)
-    node["sub_id"] = np.zeros(N, np.int32)
+    # subgraphs = weakly connected components (event_conversion.py:84)
+    from scipy.sparse import coo_matrix
+    from scipy.sparse.csgraph import connected_components
+    _, comp = connected_components(coo_matrix((np.ones(E), (src, dst)), shape=(N, N)), directed=False)
+    node["sub_id"] = comp.astype(np.int32)
     node["degree"] = deg.astype(np.int32)
     slot["slot_src"] = slot_src
     slot["slot_key"] = slot_src.astype(np.int64)
@@ -205,19 +217,26 @@ def _assemble(N, src, dst, x, y, z, r, layer, p) -> TrackGraph:
     node["merged_state"][vv] = sv
     node["merged_cov"][vv] = c5
     node["merged_prior"][vv] = 1.0
-    g = TrackGraph(N, E, slot_ptr.astype(np.int32), out_ptr.astype(np.int32), out_slot, node, slot, 1)
+    g = TrackGraph(N, E, slot_ptr.astype(np.int32), out_ptr.astype(np.int32), out_slot, node, slot,
+                   int(comp.max()) + 1 if N else 0)
     check_layout(g)
     return g
+
+
+# calibrated to the committed events: 800' all-volume E/N = 3.0,
+# 134 all-volume E/N = 5.9 (C4 = pileup-200 density, ~1M directed edges)
+C2_TRACKS, C2_FAKE = 3300, 1.2
+C4_TRACKS, C4_FAKE = 19000, 4.0
 
 
 def workload(name: str, seed: int = 0) -> TrackGraph:
     """Benchmark configs of BASELINE.json."""
     if name == "c2":
-        return event(seed, 3300)
+        return event(seed, C2_TRACKS, C2_FAKE)
     if name == "c3":
-        return concat([event(seed + i, 3300) for i in range(64)])
+        return concat([event(seed + i, C2_TRACKS, C2_FAKE) for i in range(64)])
     if name == "c4":
-        return event(seed, 18700)
+        return event(seed, C4_TRACKS, C4_FAKE)
     if name.startswith("tiny"):
         return event(seed, int(name[4:] or 200))
     raise ValueError("unknown workload %r (c2, c3, c4, tinyN)" % name)

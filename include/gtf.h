@@ -130,6 +130,11 @@ int gtf_cluster(const gtf_graph* g, gtf_nodes* n, gtf_states* states, gtf_edges*
 /* extrapolate -> update -> cluster(updated_track_states, p->cluster_chi2, p->cluster_kl) */
 int gtf_pass(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts, gtf_edges* e,
              const gtf_params* p, void* workspace, gtf_stream_t stream);
+/* gtf_pass with hipEvent_t events[4] recorded on the stream before the sender scan,
+ * after it, after the edge extrapolation kernel and after the fused node kernel
+ * (per-kernel timing for the roofline report; events may be NULL). */
+int gtf_pass_ev(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts, gtf_edges* e,
+                const gtf_params* p, void* workspace, gtf_stream_t stream, void* const* events);
 
 /* Tag propagation. radius: [N] node radius (attr 'zr'[1]); keep: [E] output mask of
  * kept inward neighbours per out-edge (u8, indexed by out-edge position);

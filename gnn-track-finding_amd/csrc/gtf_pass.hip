@@ -466,47 +466,59 @@ __device__ void node_cluster(const gtf_graph& g, gtf_nodes& n, const gtf_states&
         }
 }
 
-enum : int { ST_EXTRAP = 1, ST_UPDATE = 2, ST_CLUSTER = 4 };
+// node-local operations, executed in sequence per node by k_node
+enum : int8_t {
+    OP_RANKS = 1,        // append fresh UTS keys to the dict (extrapolate_merged_states.py:443-447)
+    OP_PRIORS_TSE = 2,   // compute_prior_probabilities(.., 'track_state_estimates') helper.py:30-63
+    OP_PRIORS_UTS = 3,   // compute_prior_probabilities(.., 'updated_track_states')
+    OP_REWEIGHT_UTS = 4, // reweight(.., 'updated_track_states') helper.py:143-225
+    OP_DEGREE = 5,       // degree = active in-edges (helper.py:67-73)
+    OP_PRUNE = 6,        // remove_state_metadata.py:31-48
+    OP_MW_TSE = 7,       // compute_mixture_weights helper.py:76-96
+    OP_MW_UTS = 8,
+    OP_CLUSTER_TSE = 9,  // clustering.py:197-321 on track_state_estimates
+    OP_CLUSTER_UTS = 10, // ... on updated_track_states
+};
+
+struct NodeOps {
+    int8_t op[24];
+    int32_t n;
+};
 
 __global__ void __launch_bounds__(BLOCK) k_node(gtf_graph g, gtf_nodes n, gtf_states tse, gtf_states uts,
-                                                gtf_edges e, gtf_params p, Ws w, int stages, int cluster_key,
-                                                double chi2_thr, double kl_thr) {
+                                                gtf_edges e, gtf_params p, Ws w, NodeOps ops, double chi2_thr,
+                                                double kl_thr) {
     const int v = blockIdx.x * BLOCK + threadIdx.x;
     if (v >= g.n_nodes) return;
     const Seg s{g.slot_ptr[v], g.slot_ptr[v + 1]};
-    if (stages & ST_EXTRAP) {  // extrapolate_merged_states.py:554-566
-        node_assign_ranks(uts, s);
-        if (n.has_uts[v]) {
-            node_priors(g, e, uts, s);
-            node_reweight(g, e, uts, s, v, p.reweight_threshold, w.err);
-            node_priors(g, e, uts, s);
-            node_reweight(g, e, uts, s, v, p.reweight_threshold, w.err);
-        }
-        n.degree[v] = node_degree(g, e, s);
-    }
-    if (stages & ST_UPDATE) {  // remove_state_metadata.py:31-53
-        node_prune(g, n, tse, uts, s, v, w.err);
-        if (n.has_tse[v]) node_priors(g, e, tse, s);
-        if (n.has_uts[v]) {
-            node_priors(g, e, uts, s);
-            node_reweight(g, e, uts, s, v, p.reweight_threshold, w.err);
-        }
-    }
-    if (stages & ST_CLUSTER) {  // clustering.py:197-373
-        gtf_states& st = cluster_key ? uts : tse;
-        const bool has = cluster_key ? n.has_uts[v] : n.has_tse[v];
-        if (has) {
-            node_cluster(g, n, st, e, s, v, chi2_thr, kl_thr, p, w.err);
-            // clustering only deactivates the node's OWN in-edges, so degree, mixture
-            // weights and priors can follow in the same thread (:324-327, :372-373)
-        }
-        n.degree[v] = node_degree(g, e, s);
-        if (has) {
-            node_mixture_weights(g, st, s, v, w.err);
-            node_priors(g, e, st, s);
+    for (int i = 0; i < ops.n; i++) {
+        switch (ops.op[i]) {
+            case OP_RANKS: node_assign_ranks(uts, s); break;
+            case OP_PRIORS_TSE: if (n.has_tse[v]) node_priors(g, e, tse, s); break;
+            case OP_PRIORS_UTS: if (n.has_uts[v]) node_priors(g, e, uts, s); break;
+            case OP_REWEIGHT_UTS:
+                if (n.has_uts[v]) node_reweight(g, e, uts, s, v, p.reweight_threshold, w.err);
+                break;
+            case OP_DEGREE: n.degree[v] = node_degree(g, e, s); break;
+            case OP_PRUNE: node_prune(g, n, tse, uts, s, v, w.err); break;
+            case OP_MW_TSE: if (n.has_tse[v]) node_mixture_weights(g, tse, s, v, w.err); break;
+            case OP_MW_UTS: if (n.has_uts[v]) node_mixture_weights(g, uts, s, v, w.err); break;
+            case OP_CLUSTER_TSE:
+                if (n.has_tse[v]) node_cluster(g, n, tse, e, s, v, chi2_thr, kl_thr, p, w.err);
+                break;
+            case OP_CLUSTER_UTS:
+                if (n.has_uts[v]) node_cluster(g, n, uts, e, s, v, chi2_thr, kl_thr, p, w.err);
+                break;
+            default: break;
         }
     }
 }
+
+// stage bodies as op sequences
+const int8_t SEQ_EXTRAP[] = {OP_RANKS, OP_PRIORS_UTS, OP_REWEIGHT_UTS, OP_PRIORS_UTS, OP_REWEIGHT_UTS, OP_DEGREE};
+const int8_t SEQ_UPDATE[] = {OP_PRUNE, OP_PRIORS_TSE, OP_PRIORS_UTS, OP_REWEIGHT_UTS};
+const int8_t SEQ_CLUSTER_UTS[] = {OP_CLUSTER_UTS, OP_DEGREE, OP_MW_UTS, OP_PRIORS_UTS};
+const int8_t SEQ_CLUSTER_TSE[] = {OP_CLUSTER_TSE, OP_DEGREE, OP_MW_TSE, OP_PRIORS_TSE};
 
 thread_local char g_err[512] = "";
 
@@ -538,16 +550,29 @@ int launch_extrap_edges(const gtf_graph* g, gtf_nodes* n, gtf_states* uts, gtf_e
     return err == hipSuccess ? 0 : fail("extrapolate launch", err);
 }
 
-int launch_node(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts, gtf_edges* e,
-                const gtf_params* p, Ws w, int stages, int key, double chi2, double kl, hipStream_t st) {
+int launch_ops(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts, gtf_edges* e,
+               const gtf_params* p, Ws w, const int8_t* const* seqs, const int* lens, int nseq, double chi2,
+               double kl, hipStream_t st) {
+    NodeOps ops;
+    memset(&ops, 0, sizeof(ops));
+    for (int q = 0; q < nseq; q++)
+        for (int i = 0; i < lens[q]; i++) {
+            if (ops.n >= (int)sizeof(ops.op)) {
+                snprintf(g_err, sizeof(g_err), "too many node ops");
+                return -2;
+            }
+            ops.op[ops.n++] = seqs[q][i];
+        }
     gtf_states dummy;
     memset(&dummy, 0, sizeof(dummy));
-    if (g->n_nodes > 0)
+    if (g->n_nodes > 0 && ops.n > 0)
         hipLaunchKernelGGL(k_node, dim3(grid(g->n_nodes)), dim3(BLOCK), 0, st, *g, *n, tse ? *tse : dummy,
-                           uts ? *uts : dummy, *e, *p, w, stages, key, chi2, kl);
+                           uts ? *uts : dummy, *e, *p, w, ops, chi2, kl);
     hipError_t err = hipGetLastError();
     return err == hipSuccess ? 0 : fail("node kernel launch", err);
 }
+
+#define SEQ(x) x, (int)sizeof(x)
 
 }  // namespace
 
@@ -569,6 +594,34 @@ int gtf_read_errors(void* ws, uint32_t* flags, gtf_stream_t stream) {
     return e == hipSuccess ? 0 : fail("read errors", e);
 }
 
+int gtf_message_passing(const gtf_graph* g, gtf_nodes* n, gtf_states* uts, gtf_edges* e, const gtf_params* p,
+                        void* ws, gtf_stream_t stream) {
+    int rc = check_graph(g);
+    if (rc) return rc;
+    Ws w = carve(ws, g->n_nodes, g->n_slots);
+    rc = launch_extrap_edges(g, n, uts, e, p, w, (hipStream_t)stream);
+    if (rc) return rc;
+    const int8_t* seqs[] = {SEQ_EXTRAP};
+    const int lens[] = {1};  // OP_RANKS only
+    return launch_ops(g, n, nullptr, uts, e, p, w, seqs, lens, 1, 0.0, 0.0, (hipStream_t)stream);
+}
+
+int gtf_node_ops(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts, gtf_edges* e,
+                 const gtf_params* p, const int8_t* ops, int32_t n_ops, double chi2_threshold,
+                 double kl_threshold, void* ws, gtf_stream_t stream) {
+    int rc = check_graph(g);
+    if (rc) return rc;
+    for (int i = 0; i < n_ops; i++)
+        if (ops[i] < OP_RANKS || ops[i] > OP_CLUSTER_UTS) {
+            snprintf(g_err, sizeof(g_err), "unknown node op %d", (int)ops[i]);
+            return -2;
+        }
+    Ws w = carve(ws, g->n_nodes, g->n_slots);
+    const int8_t* seqs[] = {ops};
+    const int lens[] = {n_ops};
+    return launch_ops(g, n, tse, uts, e, p, w, seqs, lens, 1, chi2_threshold, kl_threshold, (hipStream_t)stream);
+}
+
 int gtf_extrapolate(const gtf_graph* g, gtf_nodes* n, gtf_states* uts, gtf_edges* e, const gtf_params* p,
                     void* ws, gtf_stream_t stream) {
     int rc = check_graph(g);
@@ -576,7 +629,9 @@ int gtf_extrapolate(const gtf_graph* g, gtf_nodes* n, gtf_states* uts, gtf_edges
     Ws w = carve(ws, g->n_nodes, g->n_slots);
     rc = launch_extrap_edges(g, n, uts, e, p, w, (hipStream_t)stream);
     if (rc) return rc;
-    return launch_node(g, n, nullptr, uts, e, p, w, ST_EXTRAP, 1, 0.0, 0.0, (hipStream_t)stream);
+    const int8_t* seqs[] = {SEQ_EXTRAP};
+    const int lens[] = {(int)sizeof(SEQ_EXTRAP)};
+    return launch_ops(g, n, nullptr, uts, e, p, w, seqs, lens, 1, 0.0, 0.0, (hipStream_t)stream);
 }
 
 int gtf_update(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts, gtf_edges* e,
@@ -584,7 +639,9 @@ int gtf_update(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* ut
     int rc = check_graph(g);
     if (rc) return rc;
     Ws w = carve(ws, g->n_nodes, g->n_slots);
-    return launch_node(g, n, tse, uts, e, p, w, ST_UPDATE, 1, 0.0, 0.0, (hipStream_t)stream);
+    const int8_t* seqs[] = {SEQ_UPDATE};
+    const int lens[] = {(int)sizeof(SEQ_UPDATE)};
+    return launch_ops(g, n, tse, uts, e, p, w, seqs, lens, 1, 0.0, 0.0, (hipStream_t)stream);
 }
 
 int gtf_cluster(const gtf_graph* g, gtf_nodes* n, gtf_states* states, gtf_edges* e, int32_t key,
@@ -592,8 +649,10 @@ int gtf_cluster(const gtf_graph* g, gtf_nodes* n, gtf_states* states, gtf_edges*
     int rc = check_graph(g);
     if (rc) return rc;
     Ws w = carve(ws, g->n_nodes, g->n_slots);
-    return launch_node(g, n, key ? nullptr : states, key ? states : nullptr, e, p, w, ST_CLUSTER, key,
-                       chi2_threshold, kl_threshold, (hipStream_t)stream);
+    const int8_t* seqs[] = {key ? SEQ_CLUSTER_UTS : SEQ_CLUSTER_TSE};
+    const int lens[] = {(int)sizeof(SEQ_CLUSTER_UTS)};
+    return launch_ops(g, n, key ? nullptr : states, key ? states : nullptr, e, p, w, seqs, lens, 1, chi2_threshold,
+                      kl_threshold, (hipStream_t)stream);
 }
 
 int gtf_pass_ev(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts, gtf_edges* e,
@@ -611,8 +670,9 @@ int gtf_pass_ev(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* u
     if (events) (void)hipEventRecord((hipEvent_t)events[2], st);
     hipError_t err = hipGetLastError();
     if (err != hipSuccess) return fail("extrapolate launch", err);
-    rc = launch_node(g, n, tse, uts, e, p, w, ST_EXTRAP | ST_UPDATE | ST_CLUSTER, 1, p->cluster_chi2,
-                     p->cluster_kl, st);
+    const int8_t* seqs[] = {SEQ_EXTRAP, SEQ_UPDATE, SEQ_CLUSTER_UTS};
+    const int lens[] = {(int)sizeof(SEQ_EXTRAP), (int)sizeof(SEQ_UPDATE), (int)sizeof(SEQ_CLUSTER_UTS)};
+    rc = launch_ops(g, n, tse, uts, e, p, w, seqs, lens, 3, p->cluster_chi2, p->cluster_kl, st);
     if (events) (void)hipEventRecord((hipEvent_t)events[3], st);
     return rc;
 }

@@ -52,7 +52,11 @@ ERR_FLAGS = {
 
 # exported symbols (must match include/gtf.h; tests check the .so exports all of them)
 SYMBOLS = ["gtf_workspace_bytes", "gtf_clear_errors", "gtf_read_errors", "gtf_extrapolate", "gtf_update",
+           "gtf_message_passing", "gtf_node_ops",
            "gtf_cluster", "gtf_pass", "gtf_pass_ev", "gtf_tag_prepare", "gtf_tag_sweep", "gtf_last_error", "gtf_version"]
+
+OPS = {"ranks": 1, "priors_tse": 2, "priors_uts": 3, "reweight_uts": 4, "degree": 5, "prune": 6, "mw_tse": 7,
+       "mw_uts": 8, "cluster_tse": 9, "cluster_uts": 10}
 
 _lib = None
 
@@ -74,6 +78,8 @@ def lib():
                       ctypes.POINTER(GtfEdges), ctypes.POINTER(GtfParams))
     L.gtf_extrapolate.argtypes = [G, N, S, E, PR, P, P]
     L.gtf_update.argtypes = [G, N, S, S, E, PR, P, P]
+    L.gtf_message_passing.argtypes = [G, N, S, E, PR, P, P]
+    L.gtf_node_ops.argtypes = [G, N, S, S, E, PR, ctypes.POINTER(ctypes.c_int8), I32, F64, F64, P, P]
     L.gtf_cluster.argtypes = [G, N, S, E, I32, F64, F64, PR, P, P]
     L.gtf_pass.argtypes = [G, N, S, S, E, PR, P, P]
     L.gtf_pass_ev.argtypes = [G, N, S, S, E, PR, P, P, ctypes.POINTER(P)]
@@ -82,7 +88,7 @@ def lib():
     L.gtf_last_error.restype = ctypes.c_char_p
     L.gtf_version.restype = ctypes.c_char_p
     for fn in ("gtf_clear_errors", "gtf_read_errors", "gtf_extrapolate", "gtf_update", "gtf_cluster", "gtf_pass",
-               "gtf_pass_ev",
+               "gtf_pass_ev", "gtf_message_passing", "gtf_node_ops",
                "gtf_tag_prepare", "gtf_tag_sweep"):
         getattr(L, fn).restype = ctypes.c_int
     _lib = L

@@ -118,6 +118,21 @@ class DeviceGraph:
         nat.check(self.lib.gtf_extrapolate(ctypes.byref(self.cg), ctypes.byref(self.cn), ctypes.byref(self.cuts),
                                            ctypes.byref(self.ce), ctypes.byref(cp), self.ptr("ws"), self.stream))
 
+    def message_passing(self, p: Params):
+        cp = self.cparams(p)
+        nat.check(self.lib.gtf_message_passing(ctypes.byref(self.cg), ctypes.byref(self.cn),
+                                               ctypes.byref(self.cuts), ctypes.byref(self.ce), ctypes.byref(cp),
+                                               self.ptr("ws"), self.stream))
+
+    def node_ops(self, ops, p: Params, chi2=0.0, kl=0.0):
+        """run named node-local ops (gtf._native.OPS) in order, one launch"""
+        codes = [nat.OPS[o] for o in ops]
+        arr = (ctypes.c_int8 * len(codes))(*codes)
+        cp = self.cparams(p)
+        nat.check(self.lib.gtf_node_ops(ctypes.byref(self.cg), ctypes.byref(self.cn), ctypes.byref(self.ctse),
+                                        ctypes.byref(self.cuts), ctypes.byref(self.ce), ctypes.byref(cp), arr,
+                                        len(codes), float(chi2), float(kl), self.ptr("ws"), self.stream))
+
     def update(self, p: Params):
         cp = self.cparams(p)
         nat.check(self.lib.gtf_update(ctypes.byref(self.cg), ctypes.byref(self.cn), ctypes.byref(self.ctse),

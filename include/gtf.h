@@ -119,6 +119,28 @@ int gtf_read_errors(void* workspace, uint32_t* flags, gtf_stream_t stream);
 
 int gtf_extrapolate(const gtf_graph* g, gtf_nodes* n, gtf_states* uts, gtf_edges* e,
                     const gtf_params* p, void* workspace, gtf_stream_t stream);
+/* message passing alone (extrapolate_merged_states.py:406-451): extrapolation of every
+ * merged state along active out-edges, gate, Kalman update, UTS dict insertion. */
+int gtf_message_passing(const gtf_graph* g, gtf_nodes* n, gtf_states* uts, gtf_edges* e,
+                        const gtf_params* p, void* workspace, gtf_stream_t stream);
+
+/* Node-local helper operations, run in the given order for every node in one launch. */
+enum {
+    GTF_OP_RANKS = 1,        /* append keys created by message passing to the UTS dict */
+    GTF_OP_PRIORS_TSE = 2,   /* helper.compute_prior_probabilities(.., 'track_state_estimates') :30-63 */
+    GTF_OP_PRIORS_UTS = 3,   /* helper.compute_prior_probabilities(.., 'updated_track_states') */
+    GTF_OP_REWEIGHT_UTS = 4, /* helper.reweight(.., 'updated_track_states') :143-225 */
+    GTF_OP_DEGREE = 5,       /* node 'degree' = helper.query_node_degree_in_edges :67-73 */
+    GTF_OP_PRUNE = 6,        /* remove_state_metadata.py:31-48 */
+    GTF_OP_MW_TSE = 7,       /* helper.compute_mixture_weights(.., 'track_state_estimates') :76-96 */
+    GTF_OP_MW_UTS = 8,
+    GTF_OP_CLUSTER_TSE = 9,  /* clustering.py:197-321 on track_state_estimates */
+    GTF_OP_CLUSTER_UTS = 10
+};
+/* ops: host array of n_ops (<= 24) GTF_OP_* codes; thresholds used by the cluster ops. */
+int gtf_node_ops(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts, gtf_edges* e,
+                 const gtf_params* p, const int8_t* ops, int32_t n_ops, double chi2_threshold,
+                 double kl_threshold, void* workspace, gtf_stream_t stream);
 int gtf_update(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts, gtf_edges* e,
                const gtf_params* p, void* workspace, gtf_stream_t stream);
 /* key: 0 = cluster track_state_estimates, 1 = updated_track_states. Where a

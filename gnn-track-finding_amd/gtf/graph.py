@@ -378,8 +378,18 @@ def unpack(g: TrackGraph, subgraphs, *, states=("tse", "uts"), merged=True,
             if degree and g.node["degree"][vi] >= 0:
                 attr["degree"] = int(g.node["degree"][vi])
             if merged and g.node["has_merged"][vi]:
-                attr["merged_state"] = g.node["merged_state"][vi].copy()
-                attr["merged_cov"] = mat_from_cov5(g.node["merged_cov"][vi])
+                ms, mc = g.node["merged_state"][vi], mat_from_cov5(g.node["merged_cov"][vi])
+                old_ms, old_mc = attr.get("merged_state"), attr.get("merged_cov")
+                # message passing mutates the stored arrays in place (extrapolate_merged_states.py:128);
+                # keep the objects, so aliases held elsewhere see the same values
+                if isinstance(old_ms, np.ndarray) and old_ms.shape == (3,) and old_ms.dtype == F64:
+                    old_ms[...] = ms
+                else:
+                    attr["merged_state"] = ms.copy()
+                if isinstance(old_mc, np.ndarray) and old_mc.shape == (3, 3) and old_mc.dtype == F64:
+                    old_mc[...] = mc
+                else:
+                    attr["merged_cov"] = mc
                 attr["merged_prior"] = g.node["merged_prior"][vi]
             if "tse" in states and g.node["has_tse"][vi]:
                 _write_dict(g, "tse", attr, "track_state_estimates", lo, hi, G)

@@ -160,7 +160,8 @@ def extrapolate_validate(node_gnn, nb_gnn, merged_state, merged_cov, chi2_cut, s
         jcov[:, 2] = 0.0
         jcov[2, :] = 0.0
         jcov[2, 2] = variance_tau + var_ms
-        return True, dict(sv=updated_state, tau=tau, cov=jcov, lik=likelihood), chi2
+        return True, dict(sv=updated_state, tau=tau, cov=jcov, lik=likelihood,
+                          xp_scale=max(np.max(np.abs(extrp_state)), np.max(np.abs(F.dot(extrp_state))))), chi2
     return False, None, chi2
 
 
@@ -177,6 +178,9 @@ def message_passing(g: TrackGraph, p) -> dict:
         r = S["uts_rank"][lo:hi]
         next_rank[v] = (int(r.max()) + 1) if (hi > lo and r.max() >= 0) else 0
     chi2_all = np.full(g.n_slots, np.nan)
+    # diagnostic (tests only): magnitude of the predicted state, the rounding scale of
+    # the updated receiver-frame offset c, which cancels to ~0 by construction
+    S["xp_scale"] = np.zeros(g.n_slots)
     for u in range(g.n_nodes):                                                    # :419
         if not N["has_merged"][u]:
             continue
@@ -202,6 +206,7 @@ def message_passing(g: TrackGraph, p) -> dict:
                 S["uts_cov"][k] = cov5_from_mat(res["cov"])
                 S["uts_xyzr"][k] = N["gnn"][u]                                    # sender coords :377
                 S["uts_lik"][k] = res["lik"]
+                S["xp_scale"][k] = res["xp_scale"]
                 if np.isnan(S["send_mw"][k]):
                     raise ReferenceError_("KeyError: sender TSE has no entry for receiver (:384)")
                 S["uts_mw"][k] = S["send_mw"][k]                                  # :384

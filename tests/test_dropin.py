@@ -1,0 +1,172 @@
+"""End-to-end drop-in tests on the reference's own object format.
+
+tests/golden/dropin_*.pkl hold reference stage inputs and outputs (lists of
+pickled nx.DiGraph with GNN_Measurement nodes, written by
+tests/golden/make_golden_dropin.py from the reference's own functions). The
+drop-in CLIs/functions must turn the inputs into graphs whose attributes equal
+the reference outputs: same dict keys in the same order, same aliasing, masks
+and ints exact, floats within 1e-6 relative.
+"""
+import copy
+import glob
+import os
+import pickle
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from fixtures import GOLDEN
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "gnn-track-finding_amd")
+
+
+def _load(name):
+    with open(os.path.join(GOLDEN, "dropin_%s.pkl" % name), "rb") as f:
+        return pickle.load(f)
+
+
+def _close(a, b, rtol):
+    if isinstance(a, (list, tuple)) or isinstance(a, np.ndarray):
+        a = np.asarray(a, dtype=float)
+        b = np.asarray(b, dtype=float)
+        return a.shape == b.shape and bool(np.all(np.isclose(a, b, rtol=rtol, atol=1e-12) |
+                                                 (np.isnan(a) & np.isnan(b))))
+    if isinstance(a, str) or isinstance(b, str):
+        return a == b
+    if isinstance(a, (int, np.integer)) and isinstance(b, (int, np.integer)):
+        return int(a) == int(b)
+    a, b = float(a), float(b)
+    return (np.isnan(a) and np.isnan(b)) or bool(np.isclose(a, b, rtol=rtol, atol=1e-12))
+
+
+def _cmp_state_dict(got, exp, where, rtol, errs):
+    if [int(k) for k in got.keys()] != [int(k) for k in exp.keys()]:
+        errs.append("%s: keys/order %s != %s" % (where, list(got.keys())[:6], list(exp.keys())[:6]))
+        return
+    for k in exp:
+        ge, ee = got[k], exp[k]
+        if list(ge.keys()) != list(ee.keys()):
+            errs.append("%s[%s]: entry keys %s != %s" % (where, k, list(ge.keys()), list(ee.keys())))
+            continue
+        if ("edge_covariance" in ee and "joint_vector_covariance" in ee and
+                (ee["edge_covariance"] is ee["joint_vector_covariance"]) !=
+                (ge["edge_covariance"] is ge["joint_vector_covariance"])):
+            errs.append("%s[%s]: covariance aliasing differs" % (where, k))
+        for f in ee:
+            if f in ("xyzr", "xy", "zr"):
+                ok = _close(ge[f], ee[f], 0.0)
+            else:
+                ok = _close(ge[f], ee[f], rtol)
+            if not ok:
+                errs.append("%s[%s].%s: %r != %r" % (where, k, f, ge[f], ee[f]))
+
+
+def graphs_equal(got, exp, rtol=1e-6):
+    errs = []
+    by_min = {min(s.nodes): s for s in got if len(s)}
+    for e in exp:
+        if not len(e):
+            continue
+        g = by_min.get(min(e.nodes))
+        if g is None:
+            errs.append("missing subgraph %s" % min(e.nodes))
+            continue
+        if list(g.nodes) != list(e.nodes) or list(g.edges) != list(e.edges):
+            errs.append("structure differs for subgraph %s" % min(e.nodes))
+            continue
+        for u, v in e.edges:
+            ea, ga = e[u][v], g[u][v]
+            if set(ea) != set(ga):
+                errs.append("edge %s attrs %s != %s" % ((u, v), sorted(ga), sorted(ea)))
+            elif ea.get("activated") != ga.get("activated"):
+                errs.append("edge %s activated %s != %s" % ((u, v), ga.get("activated"), ea.get("activated")))
+            elif "mixture_weight" in ea and not _close(ga["mixture_weight"], ea["mixture_weight"], rtol):
+                errs.append("edge %s mixture_weight %r != %r" % ((u, v), ga["mixture_weight"], ea["mixture_weight"]))
+        for n in e.nodes:
+            na, ga = e.nodes[n], g.nodes[n]
+            if list(na.keys()) != list(ga.keys()):
+                errs.append("node %s attr keys %s != %s" % (n, list(ga.keys()), list(na.keys())))
+                continue
+            for f in na:
+                if f in ("track_state_estimates", "updated_track_states"):
+                    _cmp_state_dict(ga[f], na[f], "node %s %s" % (n, f), rtol, errs)
+                elif f in ("degree",):
+                    if int(ga[f]) != int(na[f]):
+                        errs.append("node %s degree %s != %s" % (n, ga[f], na[f]))
+                elif f in ("merged_state", "merged_cov", "merged_prior"):
+                    if not _close(ga[f], na[f], rtol):
+                        errs.append("node %s %s %r != %r" % (n, f, ga[f], na[f]))
+        if len(errs) > 20:
+            break
+    return errs
+
+
+def test_pack_unpack_roundtrip_is_identity():
+    """packing and writing back without running anything leaves every attribute as it was"""
+    from gtf.graph import pack, unpack
+    for name in ("cluster_tse", "extrapolate", "update"):
+        d = _load(name)
+        src = d["out"]
+        g = copy.deepcopy(src)
+        unpack(pack(g), g)
+        errs = graphs_equal(g, src, rtol=0.0)
+        assert errs == [], "\n".join(errs[:10])
+
+
+def _run_cli(module, args, cwd):
+    env = dict(os.environ)
+    env["PYTHONPATH"] = PKG + os.pathsep + env.get("PYTHONPATH", "")
+    r = subprocess.run([sys.executable, os.path.join(PKG, module)] + args, cwd=cwd, env=env,
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+
+
+def _write(graphs, d):
+    os.makedirs(d, exist_ok=True)
+    for i, s in enumerate(graphs):
+        with open(os.path.join(d, "%d_subgraph.gpickle" % i), "wb") as f:
+            pickle.dump(s, f, pickle.HIGHEST_PROTOCOL)
+
+
+def _read(d):
+    out = []
+    for f in glob.glob(os.path.join(d, "*_subgraph.gpickle")):
+        with open(f, "rb") as fh:
+            out.append(pickle.load(fh))
+    return out
+
+
+@pytest.mark.gpu
+def test_dropin_clustering_cli(tmp_path):
+    d = _load("cluster_tse")
+    _write(d["in"], str(tmp_path / "in"))
+    os.makedirs(tmp_path / "out")
+    _run_cli("clustering/clustering.py", ["-i", str(tmp_path / "in") + "/", "-o", str(tmp_path / "out") + "/",
+                                          "-d", "track_state_estimates", "-c", "1.0", "-k", "2.0", "-l", "x.lut",
+                                          "-t", "1", "-z", "0.4", "-m", "0.6", "-b", "550.0"], str(tmp_path))
+    errs = graphs_equal(_read(str(tmp_path / "out")), d["out"])
+    assert errs == [], "\n".join(errs[:20])
+
+
+@pytest.mark.gpu
+def test_dropin_extrapolate_cli(tmp_path):
+    d = _load("extrapolate")
+    _write(d["in"], str(tmp_path / "in"))
+    os.makedirs(tmp_path / "out")
+    _run_cli("extrapolate/extrapolate_merged_states.py", ["-i", str(tmp_path / "in") + "/", "-o",
+                                                          str(tmp_path / "out") + "/", "-c", "2.0", "-e", "0.3",
+                                                          "-z", "0.4", "-m", "0.6", "-b", "550.0"], str(tmp_path))
+    errs = graphs_equal(_read(str(tmp_path / "out")), d["out"])
+    assert errs == [], "\n".join(errs[:20])
+
+
+@pytest.mark.gpu
+def test_dropin_update_cli(tmp_path):
+    d = _load("update")
+    _write(d["in"], str(tmp_path / "rem"))
+    _run_cli("update/remove_state_metadata.py", ["-r", str(tmp_path / "rem") + "/"], str(tmp_path))
+    errs = graphs_equal(_read(str(tmp_path / "rem")), d["out"])
+    assert errs == [], "\n".join(errs[:20])

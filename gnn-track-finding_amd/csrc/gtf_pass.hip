@@ -483,13 +483,15 @@ enum : int8_t {
 struct NodeOps {
     int8_t op[24];
     int32_t n;
+    int32_t uses_tse, uses_uts;
 };
 
 __global__ void __launch_bounds__(BLOCK) k_node(gtf_graph g, gtf_nodes n, gtf_states tse, gtf_states uts,
                                                 gtf_edges e, gtf_params p, Ws w, NodeOps ops, double chi2_thr,
-                                                double kl_thr) {
-    const int v = blockIdx.x * BLOCK + threadIdx.x;
-    if (v >= g.n_nodes) return;
+                                                double kl_thr, const int32_t* list, int count) {
+    const int t = blockIdx.x * BLOCK + threadIdx.x;
+    if (t >= count) return;
+    const int v = list ? list[t] : t;
     const Seg s{g.slot_ptr[v], g.slot_ptr[v + 1]};
     for (int i = 0; i < ops.n; i++) {
         switch (ops.op[i]) {
@@ -513,6 +515,8 @@ __global__ void __launch_bounds__(BLOCK) k_node(gtf_graph g, gtf_nodes n, gtf_st
         }
     }
 }
+
+#include "gtf_node_group.h"
 
 // stage bodies as op sequences
 const int8_t SEQ_EXTRAP[] = {OP_RANKS, OP_PRIORS_UTS, OP_REWEIGHT_UTS, OP_PRIORS_UTS, OP_REWEIGHT_UTS, OP_DEGREE};
@@ -565,9 +569,34 @@ int launch_ops(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* ut
         }
     gtf_states dummy;
     memset(&dummy, 0, sizeof(dummy));
-    if (g->n_nodes > 0 && ops.n > 0)
-        hipLaunchKernelGGL(k_node, dim3(grid(g->n_nodes)), dim3(BLOCK), 0, st, *g, *n, tse ? *tse : dummy,
-                           uts ? *uts : dummy, *e, *p, w, ops, chi2, kl);
+    for (int i = 0; i < ops.n; i++) {
+        const int o = ops.op[i];
+        if (o == OP_PRIORS_TSE || o == OP_MW_TSE || o == OP_CLUSTER_TSE || o == OP_PRUNE) ops.uses_tse = 1;
+        if (o == OP_RANKS || o == OP_PRIORS_UTS || o == OP_REWEIGHT_UTS || o == OP_MW_UTS || o == OP_CLUSTER_UTS ||
+            o == OP_PRUNE)
+            ops.uses_uts = 1;
+    }
+    if (!tse) ops.uses_tse = 0;
+    if (!uts) ops.uses_uts = 0;
+    const gtf_states T = tse ? *tse : dummy, U = uts ? *uts : dummy;
+    if (g->n_nodes > 0 && ops.n > 0) {
+        if (g->sched) {
+            // degree-bucketed schedule: 16-lane groups, 64-lane groups, then one thread per node
+            const int n16 = g->n_g16, n64 = g->n_g64, nbig = g->n_nodes - n16 - n64;
+            if (n16 > 0)
+                hipLaunchKernelGGL(k_node_group<16>, dim3((n16 + BLOCK / 16 - 1) / (BLOCK / 16)), dim3(BLOCK), 0, st,
+                                   *g, *n, T, U, *e, *p, w, ops, chi2, kl, g->sched, n16);
+            if (n64 > 0)
+                hipLaunchKernelGGL(k_node_group<64>, dim3((n64 + BLOCK / 64 - 1) / (BLOCK / 64)), dim3(BLOCK), 0, st,
+                                   *g, *n, T, U, *e, *p, w, ops, chi2, kl, g->sched + n16, n64);
+            if (nbig > 0)
+                hipLaunchKernelGGL(k_node, dim3(grid(nbig)), dim3(BLOCK), 0, st, *g, *n, T, U, *e, *p, w, ops, chi2, kl,
+                                   g->sched + n16 + n64, nbig);
+        } else {
+            hipLaunchKernelGGL(k_node, dim3(grid(g->n_nodes)), dim3(BLOCK), 0, st, *g, *n, T, U, *e, *p, w, ops, chi2,
+                               kl, (const int32_t*)nullptr, g->n_nodes);
+        }
+    }
     hipError_t err = hipGetLastError();
     return err == hipSuccess ? 0 : fail("node kernel launch", err);
 }

@@ -52,6 +52,12 @@ typedef struct gtf_graph {
     const double*  gnn;       /* [N*4] GNN_Measurement x,y,z,r */
     const double*  xyzr;      /* [N*4] node attribute 'xyzr' */
     const double*  layer;     /* [N]   in_volume_layer_id */
+    /* optional node schedule for the node-local stages (NULL = one thread per node):
+     * node indices with <= 16 slots first (n_g16 of them), then <= 64 slots (n_g64),
+     * then the rest. Built once per graph by the host (gtf/device.py). */
+    const int32_t* sched;     /* [N] */
+    int32_t n_g16;
+    int32_t n_g64;
 } gtf_graph;
 
 /* ---- per-node mutable state ------------------------------------------------ */

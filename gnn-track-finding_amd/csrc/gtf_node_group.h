@@ -60,6 +60,8 @@ struct LaneDict {
     int rank;
     double mw, prior;
     bool dirty;
+    int pos;         // cached dict position (-1 absent), valid while pos_ok
+    bool pos_ok;
 };
 
 template <int G>
@@ -70,6 +72,8 @@ struct NodeCtx {
     uint8_t is_edge, rev_edge, act, act0;
     int src;
     double layer;
+    unsigned long long same_layer;  // lanes whose sender has this lane's layer (lazy)
+    bool same_layer_ok;
     LaneDict tse, uts;
     double lik, lr, x0, edge_mw;
     int8_t side;
@@ -79,27 +83,45 @@ struct NodeCtx {
     bool degree_set;
 };
 
-// position of this lane's key in the dict order (number of present keys with a smaller rank)
+// highest set bit index of m (m != 0)
+__device__ __forceinline__ int hibit(unsigned long long m) { return 63 - __clzll((long long)m); }
+
+// dict position of this lane's key = number of present keys with a smaller rank.
+// Fast path: ranks ascending in slot order (fresh UTS dicts) -> popcount.
 template <int G>
-__device__ __forceinline__ int dict_pos(const NodeCtx<G>& c, int rank) {
-    int pos = 0;
-    for (int j = 0; j < G; j++) {
-        const int rj = c.grp.shfl(rank, j);
-        pos += (rj >= 0 && rj < rank) ? 1 : 0;
+__device__ __forceinline__ int dict_pos(const NodeCtx<G>& c, LaneDict& st) {
+    if (st.pos_ok) return st.pos;
+    const bool pres = c.valid && st.rank >= 0;
+    const unsigned long long P = c.grp.bits(pres);
+    const unsigned long long below = P & ((1ull << c.grp.gl) - 1ull);
+    const int prev = below ? hibit(below) : c.grp.gl;
+    const int rprev = c.grp.shfl(st.rank, prev);
+    const bool mono = !pres || !below || rprev < st.rank;
+    int pos;
+    if (!c.grp.any(!mono)) {
+        pos = __popcll(below);
+    } else {
+        pos = 0;
+        for (int j = 0; j < G; j++) {
+            const int rj = c.grp.shfl(st.rank, j);
+            pos += (rj >= 0 && rj < st.rank) ? 1 : 0;
+        }
     }
-    return rank >= 0 ? pos : -1;
+    st.pos = pres ? pos : -1;
+    st.pos_ok = true;
+    return st.pos;
 }
 
-// sequential (dict-order) sum of `term` over lanes where `take`, every lane gets the
+// sequential (dict-order) sum of `term` over lanes where `take`; every lane gets the
 // sum. Lanes write their term at their dict position in a per-group LDS line and
 // every lane adds the line in order; skipped entries add +0.0, which leaves the
 // running sum unchanged (it starts from the integer 0 of helper.py:165).
 template <int G>
-__device__ __forceinline__ double ordered_sum(const NodeCtx<G>& c, volatile double* sval, int rank, bool take,
+__device__ __forceinline__ double ordered_sum(NodeCtx<G>& c, volatile double* sval, LaneDict& st, bool take,
                                              double term) {
-    const int pos = dict_pos(c, rank);
-    const int npres = c.grp.count(rank >= 0);
-    if (rank >= 0) sval[c.grp.gbase + pos] = take ? term : 0.0;
+    const int pos = dict_pos(c, st);
+    const int npres = c.grp.count(c.valid && st.rank >= 0);
+    if (pos >= 0) sval[c.grp.gbase + pos] = take ? term : 0.0;
     __builtin_amdgcn_wave_barrier();
     double s = 0.0;
     for (int i = 0; i < npres; i++) s = s + sval[c.grp.gbase + i];
@@ -112,18 +134,29 @@ __device__ __forceinline__ bool lane_active(const NodeCtx<G>& c, int rank) {
     return c.valid && rank >= 0 && c.is_edge && c.act == 1;
 }
 
-// compute_prior_probabilities (helper.py:30-63)
+// compute_prior_probabilities (helper.py:30-63): prior = 1 / #active keys whose sender
+// shares this key's layer. The same-layer masks are built once per node, one
+// iteration per distinct layer value (leader election with a ballot).
 template <int G>
 __device__ __forceinline__ void g_priors(NodeCtx<G>& c, LaneDict& st) {
-    const bool act = lane_active(c, st.rank);
-    int cnt = 0;
-    for (int j = 0; j < G; j++) {
-        const double lj = c.grp.shfl(c.layer, j);
-        const int aj = c.grp.shfl((int)act, j);
-        cnt += (aj && lj == c.layer) ? 1 : 0;
+    if (!c.same_layer_ok) {
+        bool done = !c.valid || c.layer != c.layer;  // NaN layers (orphans) never match
+        c.same_layer = c.valid ? (1ull << c.grp.gl) : 0ull;
+        while (true) {
+            const unsigned long long todo = c.grp.bits(!done);
+            if (!todo) break;
+            const int leader = __ffsll((long long)todo) - 1;
+            const double L = c.grp.shfl(c.layer, leader);
+            const bool mine = !done && c.layer == L;
+            const unsigned long long m = c.grp.bits(mine);
+            if (mine) { c.same_layer = m; done = true; }
+        }
+        c.same_layer_ok = true;
     }
+    const bool act = lane_active(c, st.rank);
+    const unsigned long long A = c.grp.bits(act);
     if (act) {
-        st.prior = 1.0 / (double)cnt;
+        st.prior = 1.0 / (double)__popcll(A & c.same_layer);
         st.dirty = true;
     }
 }
@@ -142,15 +175,23 @@ __device__ __forceinline__ void g_reweight(NodeCtx<G>& c, volatile double* sval,
     const int last_act = c.grp.shfl((int)c.act, last);
     const double node_x = gnn[4 * (int64_t)c.v];
     const bool left = c.x0 < node_x;
-    bool dup = false;
-    for (int j = 0; j < G; j++) {
-        const double xj = c.grp.shfl(c.x0, j);
-        const int aj = c.grp.shfl((int)act, j);
-        if (j < c.grp.gl && aj && ((xj < node_x) == left) && xj == c.x0) dup = true;
+    // distinct x values per side (len(set(coords))): one iteration per distinct value
+    int dl = 0, dr = 0;
+    {
+        bool done = !act;
+        while (true) {
+            const unsigned long long todo = c.grp.bits(!done);
+            if (!todo) break;
+            const int leader = __ffsll((long long)todo) - 1;
+            const double X = c.grp.shfl(c.x0, leader);
+            if (X < node_x) dl++; else dr++;
+            if (!done && c.x0 == X) done = true;
+            if (X != X) {  // NaN: set() keeps every NaN object -> each counts once
+                if (c.grp.gl == leader) done = true;
+            }
+        }
     }
     const int nact = c.grp.count(act);
-    const int dl = c.grp.count(act && left && !dup);
-    const int dr = c.grp.count(act && !left && !dup);
     if (nact > 0) {
         if (!last_is_edge && c.grp.gl == 0) atomicOr(err, (uint32_t)GTF_ERR_STALE_KEY_NO_EDGE);
         if (act) {
@@ -159,7 +200,7 @@ __device__ __forceinline__ void g_reweight(NodeCtx<G>& c, volatile double* sval,
             c.uts_dirty_lr = true;
         }
     }
-    const double denom = ordered_sum(c, sval, st.rank, act, st.mw * c.lik);
+    const double denom = ordered_sum(c, sval, st, act, st.mw * c.lik);
     if (act) {
         double wgt = (st.mw * c.lik * st.prior) / denom;
         wgt = wgt / c.lr;
@@ -189,6 +230,7 @@ __device__ __forceinline__ void g_prune(NodeCtx<G>& c, bool has_tse, bool has_ut
         st.rank = -1;
         st.dirty = true;
     }
+    st.pos_ok = false;
 }
 
 template <int G>
@@ -215,117 +257,117 @@ __device__ __forceinline__ void g_ranks(NodeCtx<G>& c) {
         st.rank = maxr + 1 + __popcll(below);
         st.dirty = true;
     }
+    st.pos_ok = false;
 }
 
-// pairwise chi2 + greedy KL merging of one node (clustering.py:197-307)
+// lower-triangle pair t (row-major: (1,0) (2,0) (2,1) (3,0) ...) for d <= 15
+__constant__ uint8_t c_pair_i[105] = {
+    1, 2, 2, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 5, 6, 6, 6, 6, 6, 6, 7, 7, 7, 7, 7, 7, 7,
+    8, 8, 8, 8, 8, 8, 8, 8, 9, 9, 9, 9, 9, 9, 9, 9, 9, 10, 10, 10, 10, 10, 10, 10, 10, 10, 10,
+    11, 11, 11, 11, 11, 11, 11, 11, 11, 11, 11, 12, 12, 12, 12, 12, 12, 12, 12, 12, 12, 12, 12,
+    13, 13, 13, 13, 13, 13, 13, 13, 13, 13, 13, 13, 13, 14, 14, 14, 14, 14, 14, 14, 14, 14, 14, 14, 14, 14, 14};
+__constant__ uint8_t c_pair_j[105] = {
+    0, 0, 1, 0, 1, 2, 0, 1, 2, 3, 0, 1, 2, 3, 4, 0, 1, 2, 3, 4, 5, 0, 1, 2, 3, 4, 5, 6,
+    0, 1, 2, 3, 4, 5, 6, 7, 0, 1, 2, 3, 4, 5, 6, 7, 8, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9,
+    0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11,
+    0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13};
+
+// per-group LDS staging of up to 15 states (structure of arrays)
+struct Stage {
+    double a[16], b[16], c[16], tau[16], c00[16], c01[16], c10[16], c11[16], c22[16], x[16], z[16], r[16],
+        prior[16];
+};
+
+__device__ __forceinline__ Cov5 stage_cov(const volatile Stage* s, int i) {
+    return Cov5{s->c00[i], s->c01[i], s->c10[i], s->c11[i], s->c22[i]};
+}
+
+// pairwise chi2 + greedy KL merging of one node (clustering.py:197-307). The
+// d(d-1)/2 pairs are dealt round-robin over the G lanes (row-major pair index t),
+// so the np.where tie order is the order of t.
 template <int G>
 __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf_states& S, LaneDict& st,
-                                          volatile int* slane, const double* xyzr_node, double chi2_thr,
+                                          volatile Stage* stg, const double* xyzr_node, double chi2_thr,
                                           double kl_thr, const gtf_params& p, uint32_t* err) {
     const bool pres = c.valid && st.rank >= 0;
     const int d = c.grp.count(pres);
     if (d <= 2 || d >= 16) return;                                                 // :207
-    const int pos = dict_pos(c, st.rank);
-    if (pres) slane[c.grp.gbase + pos] = c.grp.gl;
-    __builtin_amdgcn_wave_barrier();
-    // this lane's state (joint vector a, b, tau; parabolic c; covariance; sender coords)
-    double a = 0, b = 0, cc = 0, tau = 0, x = 0, z = 0, r = 0, prior = 0;
-    Cov5 cv{1, 0, 0, 1, 1};
+    const int pos = dict_pos(c, st);
     if (pres) {
-        a = S.sv[3 * (int64_t)c.k];
-        b = S.sv[3 * (int64_t)c.k + 1];
-        cc = S.sv[3 * (int64_t)c.k + 2];
-        tau = S.tau[c.k];
-        cv = load_cov5(S.cov, c.k);
-        x = S.xyzr[4 * (int64_t)c.k];
-        z = S.xyzr[4 * (int64_t)c.k + 2];
-        r = S.xyzr[4 * (int64_t)c.k + 3];
-        prior = st.prior;
+        const int64_t k = c.k;
+        stg->a[pos] = S.sv[3 * k];
+        stg->b[pos] = S.sv[3 * k + 1];
+        stg->c[pos] = S.sv[3 * k + 2];
+        stg->tau[pos] = S.tau[k];
+        const double* cv = S.cov + 5 * k;
+        stg->c00[pos] = cv[0]; stg->c01[pos] = cv[1]; stg->c10[pos] = cv[2]; stg->c11[pos] = cv[3];
+        stg->c22[pos] = cv[4];
+        stg->x[pos] = S.xyzr[4 * k];
+        stg->z[pos] = S.xyzr[4 * k + 2];
+        stg->r[pos] = S.xyzr[4 * k + 3];
+        stg->prior[pos] = st.prior;
     }
+    __builtin_amdgcn_wave_barrier();
     const double na[4] = {xyzr_node[0], xyzr_node[1], xyzr_node[2], xyzr_node[3]};
-    const double mine[4] = {x, 0.0, z, r};
-    // row `pos` of the lower triangle: D[pos][j], j < pos
-    double rmin = INFINITY;
-    int rj0 = -1, rties = 0;
-    unsigned rmask = 0;
-    bool rnan = false, rnz = false;
-    for (int j = 0; j < d - 1; j++) {
-        const int lj = slane[c.grp.gbase + j];
-        const double aj = c.grp.shfl(a, lj), bj = c.grp.shfl(b, lj);
-        const Cov5 cj{c.grp.shfl(cv.c00, lj), c.grp.shfl(cv.c01, lj), c.grp.shfl(cv.c10, lj),
-                      c.grp.shfl(cv.c11, lj), c.grp.shfl(cv.c22, lj)};
-        const double oth[4] = {c.grp.shfl(x, lj), 0.0, c.grp.shfl(z, lj), c.grp.shfl(r, lj)};
-        if (pres && j < pos) {
-            const double D = mahalanobis(a, b, cv, aj, bj, cj, na, mine, oth, p.sigma0rz2, p.sigma0rz, p.sigma0rz,
-                                         p.sigma0rz2, p.endcap_boundary);
-            if (D != 0.0) {
-                rnz = true;
-                if (isnan(D)) {
-                    rnan = true;
-                } else if (D < rmin) {
-                    rmin = D; rj0 = j; rties = 1; rmask = 1u << j;
-                } else if (D == rmin) {
-                    rties++; rmask |= 1u << j;
-                }
-            }
+    const int npairs = d * (d - 1) / 2;
+    double lmin = INFINITY;
+    int lt0 = 1 << 20, lt1 = 1 << 20;
+    unsigned lmask = 0;
+    bool lnan = false, lnz = false;
+    for (int t = c.grp.gl; t < npairs; t += G) {
+        const int i = c_pair_i[t], j = c_pair_j[t];
+        const double ni[4] = {stg->x[i], 0.0, stg->z[i], stg->r[i]};
+        const double nj[4] = {stg->x[j], 0.0, stg->z[j], stg->r[j]};
+        const double D = mahalanobis(stg->a[i], stg->b[i], stage_cov(stg, i), stg->a[j], stg->b[j], stage_cov(stg, j),
+                                     na, ni, nj, p.sigma0rz2, p.sigma0rz, p.sigma0rz, p.sigma0rz2, p.endcap_boundary);
+        if (D == 0.0) continue;  // zeros are excluded (np.nonzero)
+        lnz = true;
+        if (D != D) { lnan = true; continue; }
+        if (D < lmin) {
+            lmin = D; lt0 = t; lt1 = 1 << 20; lmask = (1u << i) | (1u << j);
+        } else if (D == lmin) {
+            if (lt1 == (1 << 20)) lt1 = t;
+            lmask |= (1u << i) | (1u << j);
         }
     }
-    if (!c.grp.any(rnz)) {
+    if (!c.grp.any(lnz)) {
         if (c.grp.gl == 0) atomicOr(err, (uint32_t)GTF_ERR_ALL_ZERO_DIST);
         return;
     }
-    if (c.grp.any(rnan)) return;                       // np.min over a NaN -> no merge (:228)
-    const double best = c.grp.min_d(rmin);
+    if (c.grp.any(lnan)) return;                       // np.min over a NaN -> no merge (:228)
+    const double best = c.grp.min_d(lmin);
     if (!(best < chi2_thr)) return;
-    // np.where(D == best) in row-major order: rows ascend with pos
-    const bool tie_row = pres && rmin == best;
-    const unsigned long long trb = c.grp.bits(tie_row);
-    // row index (dict position) of each tie row, found via the lane map
-    int ti0 = 99, tj0 = -1, ti1 = 99, t0ties = 0;
-    {
-        // first tie row = smallest pos among tie rows
-        const int mypos_if = tie_row ? pos : 99;
-        ti0 = c.grp.min_i(mypos_if);
-        const int l0 = slane[c.grp.gbase + ti0];
-        tj0 = c.grp.shfl(rj0, l0);
-        t0ties = c.grp.shfl(rties, l0);
-        const int second = (tie_row && pos != ti0) ? pos : 99;
-        ti1 = (t0ties >= 2) ? ti0 : c.grp.min_i(second);
-    }
-    (void)trb;
-    unsigned tiemask = tie_row ? (rmask | (1u << pos)) : 0u;
-    tiemask = c.grp.or_u(tiemask);
-    const int p0 = ti0, p1 = (ti1 < 99) ? ti1 : tj0;
-    // merge the pair (every lane computes the same merge: uniform work)
-    const int l0 = slane[c.grp.gbase + p0], l1 = slane[c.grp.gbase + p1];
-    double ps0[3] = {c.grp.shfl(a, l0), c.grp.shfl(b, l0), c.grp.shfl(cc, l0)};
-    double ps1[3] = {c.grp.shfl(a, l1), c.grp.shfl(b, l1), c.grp.shfl(cc, l1)};
-    const double t0 = c.grp.shfl(tau, l0), t1 = c.grp.shfl(tau, l1);
-    const Cov5 c0{c.grp.shfl(cv.c00, l0), c.grp.shfl(cv.c01, l0), c.grp.shfl(cv.c10, l0), c.grp.shfl(cv.c11, l0),
-                  c.grp.shfl(cv.c22, l0)};
-    const Cov5 c1{c.grp.shfl(cv.c00, l1), c.grp.shfl(cv.c01, l1), c.grp.shfl(cv.c10, l1), c.grp.shfl(cv.c11, l1),
-                  c.grp.shfl(cv.c22, l1)};
+    const bool tl = lmin == best;
+    const int t0 = c.grp.min_i(tl ? lt0 : (1 << 20));
+    const int t1 = c.grp.min_i(tl ? (lt0 == t0 ? lt1 : lt0) : (1 << 20));
+    const unsigned tiemask = c.grp.or_u(tl ? lmask : 0u);
+    const int ti0 = c_pair_i[t0], tj0 = c_pair_j[t0];
+    // merged pair = (idx[0], idx[1]) of concatenate((rows, cols)) (:231-233)
+    const int p0 = ti0, p1 = (t1 < (1 << 20)) ? (int)c_pair_i[t1] : tj0;
     double pm[3], jm[3];
     Cov5 pc, jc;
     {
-        const double js0[3] = {ps0[0], ps0[1], t0};
-        const double js1[3] = {ps1[0], ps1[1], t1};
+        const double ps0[3] = {stg->a[p0], stg->b[p0], stg->c[p0]};
+        const double ps1[3] = {stg->a[p1], stg->b[p1], stg->c[p1]};
+        const double js0[3] = {ps0[0], ps0[1], stg->tau[p0]};
+        const double js1[3] = {ps1[0], ps1[1], stg->tau[p1]};
+        const Cov5 c0 = stage_cov(stg, p0), c1 = stage_cov(stg, p1);
         merge_states(ps0, c0, ps1, c1, pm, pc);
         merge_states(js0, c0, js1, c1, jm, jc);
     }
-    double mprior = c.grp.shfl(prior, l0) + c.grp.shfl(prior, l1);
+    double mprior = stg->prior[p0] + stg->prior[p1];
     unsigned alive = ((1u << d) - 1u) & ~tiemask;
-    bool my_alive = pres && (alive >> pos & 1u);
     if (alive == 0) {
         if (c.grp.gl == 0) atomicOr(err, (uint32_t)GTF_ERR_TIE_EMPTIED);
     } else {
-        const double js_me[3] = {a, b, tau};
         while (true) {                                                             // :251-287
+            const bool me = pres && (alive >> pos & 1u);
             double D = INFINITY;
             bool dn = false;
-            if (my_alive) {
-                D = kl_distance(js_me, cv, jm, jc);
-                if (isnan(D)) { dn = true; D = INFINITY; }
+            if (me) {
+                const double js_me[3] = {stg->a[pos], stg->b[pos], stg->tau[pos]};
+                D = kl_distance(js_me, stage_cov(stg, pos), jm, jc);
+                if (D != D) { dn = true; D = INFINITY; }
             }
             if (c.grp.any(dn)) {
                 if (c.grp.gl == 0) atomicOr(err, (uint32_t)GTF_ERR_NAN_KL);
@@ -333,25 +375,22 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
             }
             const double mind = c.grp.min_d(D);
             if (!(mind < kl_thr)) break;
-            // first minimum in dict order
-            const int mpos = c.grp.min_i((my_alive && D == mind) ? pos : 99);
-            const int lm = slane[c.grp.gbase + mpos];
-            const double ps[3] = {c.grp.shfl(a, lm), c.grp.shfl(b, lm), c.grp.shfl(cc, lm)};
-            const double js[3] = {ps[0], ps[1], c.grp.shfl(tau, lm)};
-            const Cov5 ci{c.grp.shfl(cv.c00, lm), c.grp.shfl(cv.c01, lm), c.grp.shfl(cv.c10, lm),
-                          c.grp.shfl(cv.c11, lm), c.grp.shfl(cv.c22, lm)};
+            const int m = c.grp.min_i((me && D == mind) ? pos : 99);  // first minimum (list.index)
+            const double ps[3] = {stg->a[m], stg->b[m], stg->c[m]};
+            const double js[3] = {ps[0], ps[1], stg->tau[m]};
+            const Cov5 ci = stage_cov(stg, m);
             double npm[3], njm[3];
             Cov5 npc, njc;
             merge_states(ps, ci, pm, pc, npm, npc);
             merge_states(js, ci, jm, jc, njm, njc);
             pm[0] = npm[0]; pm[1] = npm[1]; pm[2] = npm[2]; pc = npc;
             jm[0] = njm[0]; jm[1] = njm[1]; jm[2] = njm[2]; jc = njc;
-            mprior = c.grp.shfl(prior, lm) + mprior;
-            alive &= ~(1u << mpos);
-            my_alive = pres && (alive >> pos & 1u);
+            mprior = stg->prior[m] + mprior;
+            alive &= ~(1u << m);
             if (alive == 0) break;
         }
     }
+    __builtin_amdgcn_wave_barrier();
     if (c.grp.gl == 0) {                                                           // :291-293
         n.has_merged[c.v] = 1;
         n.merged_state[3 * (int64_t)c.v + 0] = pm[0];
@@ -360,21 +399,18 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
         store_cov5(n.merged_cov, c.v, pc);
         n.merged_prior[c.v] = mprior;
     }
-    if (my_alive && c.is_edge) c.act = 0;                                          // :311-321
+    if (pres && (alive >> pos & 1u) && c.is_edge) c.act = 0;                       // :311-321
 }
 
+// ---------------------------------------------------------------------------
+// kernels: load a node's slots into lane registers, run the ops, write back
+// ---------------------------------------------------------------------------
 template <int G>
-__global__ void __launch_bounds__(BLOCK) k_node_group(gtf_graph g, gtf_nodes n, gtf_states tse, gtf_states uts,
-                                                      gtf_edges e, gtf_params p, Ws w, NodeOps ops,
-                                                      double chi2_thr, double kl_thr, const int32_t* list,
-                                                      int count) {
-    __shared__ volatile double s_val[BLOCK];
-    __shared__ volatile int s_lane[BLOCK];
+__device__ __forceinline__ bool node_load(NodeCtx<G>& c, const gtf_graph& g, const gtf_nodes& n,
+                                          const gtf_states& tse, const gtf_states& uts, const gtf_edges& e,
+                                          const int32_t* list, int count, bool uses_tse, bool uses_uts) {
     const int gi = (blockIdx.x * BLOCK + (int)threadIdx.x) / G;
-    if (gi >= count) return;  // group-uniform
-    NodeCtx<G> c;
-    volatile double* sval = s_val + (threadIdx.x & ~63);
-    volatile int* slane = s_lane + (threadIdx.x & ~63);
+    if (gi >= count) return false;  // group-uniform
     c.v = list[gi];
     c.lo = g.slot_ptr[c.v];
     c.d = g.slot_ptr[c.v + 1] - c.lo;
@@ -387,17 +423,18 @@ __global__ void __launch_bounds__(BLOCK) k_node_group(gtf_graph g, gtf_nodes n, 
     c.act0 = c.act;
     c.src = c.valid ? g.slot_src[k] : -1;
     c.layer = c.src >= 0 ? g.layer[c.src] : NAN;
-    const bool has_tse = n.has_tse[c.v], has_uts_in = n.has_uts[c.v];
-    c.tse = LaneDict{-1, 0.0, 0.0, false};
-    c.uts = LaneDict{-1, 0.0, 0.0, false};
+    c.same_layer = 0;
+    c.same_layer_ok = false;
+    c.tse = LaneDict{-1, 0.0, 0.0, false, -1, false};
+    c.uts = LaneDict{-1, 0.0, 0.0, false, -1, false};
     c.lik = 0; c.lr = 0; c.x0 = 0; c.edge_mw = 0; c.side = -1; c.fresh = 0;
     c.uts_dirty_lr = false; c.edge_mw_dirty = false; c.degree = 0; c.degree_set = false;
-    if (ops.uses_tse && c.valid) {
+    if (uses_tse && c.valid) {
         c.tse.rank = tse.rank[k];
         c.tse.mw = tse.mw[k];
         c.tse.prior = tse.prior[k];
     }
-    if (ops.uses_uts && c.valid) {
+    if (uses_uts && c.valid) {
         c.uts.rank = uts.rank[k];
         c.uts.mw = uts.mw[k];
         c.uts.prior = uts.prior[k];
@@ -407,27 +444,13 @@ __global__ void __launch_bounds__(BLOCK) k_node_group(gtf_graph g, gtf_nodes n, 
         c.x0 = uts.xyzr[4 * (int64_t)k];
         c.fresh = uts.fresh[k];
     }
-    bool has_uts = has_uts_in;
-    for (int i = 0; i < ops.n; i++) {
-        switch (ops.op[i]) {
-            case OP_RANKS: g_ranks(c); break;
-            case OP_PRIORS_TSE: if (has_tse) g_priors(c, c.tse); break;
-            case OP_PRIORS_UTS: if (has_uts) g_priors(c, c.uts); break;
-            case OP_REWEIGHT_UTS: if (has_uts) g_reweight(c, sval, g.gnn, p.reweight_threshold, w.err); break;
-            case OP_DEGREE: g_degree(c); break;
-            case OP_PRUNE: g_prune(c, has_tse, has_uts, w.err); break;
-            case OP_MW_TSE: if (has_tse) g_mixture_weights(c, c.tse, g.solo[c.v], w.err); break;
-            case OP_MW_UTS: if (has_uts) g_mixture_weights(c, c.uts, g.solo[c.v], w.err); break;
-            case OP_CLUSTER_TSE:
-                if (has_tse) g_cluster(c, n, tse, c.tse, slane, g.xyzr + 4 * (int64_t)c.v, chi2_thr, kl_thr, p, w.err);
-                break;
-            case OP_CLUSTER_UTS:
-                if (has_uts) g_cluster(c, n, uts, c.uts, slane, g.xyzr + 4 * (int64_t)c.v, chi2_thr, kl_thr, p, w.err);
-                break;
-            default: break;
-        }
-    }
-    // write back what changed
+    return true;
+}
+
+template <int G>
+__device__ __forceinline__ void node_store(NodeCtx<G>& c, gtf_nodes& n, gtf_states& tse, gtf_states& uts,
+                                           gtf_edges& e) {
+    const int k = c.k;
     if (c.valid) {
         if (c.act != c.act0) e.act[k] = c.act;
         if (c.edge_mw_dirty) e.edge_mw[k] = c.edge_mw;
@@ -436,4 +459,85 @@ __global__ void __launch_bounds__(BLOCK) k_node_group(gtf_graph g, gtf_nodes n, 
         if (c.uts_dirty_lr) { uts.lr[k] = c.lr; uts.side[k] = c.side; }
     }
     if (c.degree_set && c.grp.gl == 0) n.degree[c.v] = c.degree;
+}
+
+template <int G, int OP>
+__device__ __forceinline__ void node_op(NodeCtx<G>& c, const gtf_graph& g, gtf_nodes& n, gtf_states& tse,
+                                        gtf_states& uts, const gtf_params& p, const Ws& w, volatile double* sval,
+                                        volatile Stage* stg, double chi2_thr, double kl_thr, bool has_tse,
+                                        bool has_uts) {
+    if constexpr (OP == OP_RANKS) g_ranks(c);
+    if constexpr (OP == OP_PRIORS_TSE) { if (has_tse) g_priors(c, c.tse); }
+    if constexpr (OP == OP_PRIORS_UTS) { if (has_uts) g_priors(c, c.uts); }
+    if constexpr (OP == OP_REWEIGHT_UTS) { if (has_uts) g_reweight(c, sval, g.gnn, p.reweight_threshold, w.err); }
+    if constexpr (OP == OP_DEGREE) g_degree(c);
+    if constexpr (OP == OP_PRUNE) g_prune(c, has_tse, has_uts, w.err);
+    if constexpr (OP == OP_MW_TSE) { if (has_tse) g_mixture_weights(c, c.tse, g.solo[c.v], w.err); }
+    if constexpr (OP == OP_MW_UTS) { if (has_uts) g_mixture_weights(c, c.uts, g.solo[c.v], w.err); }
+    if constexpr (OP == OP_CLUSTER_TSE) {
+        if (has_tse) g_cluster(c, n, tse, c.tse, stg, g.xyzr + 4 * (int64_t)c.v, chi2_thr, kl_thr, p, w.err);
+    }
+    if constexpr (OP == OP_CLUSTER_UTS) {
+        if (has_uts) g_cluster(c, n, uts, c.uts, stg, g.xyzr + 4 * (int64_t)c.v, chi2_thr, kl_thr, p, w.err);
+    }
+}
+
+template <int... OPS>
+struct OpSeq {
+    static constexpr bool uses_tse =
+        ((OPS == OP_PRIORS_TSE || OPS == OP_MW_TSE || OPS == OP_CLUSTER_TSE || OPS == OP_PRUNE) || ...);
+    static constexpr bool uses_uts = ((OPS == OP_RANKS || OPS == OP_PRIORS_UTS || OPS == OP_REWEIGHT_UTS ||
+                                       OPS == OP_MW_UTS || OPS == OP_CLUSTER_UTS || OPS == OP_PRUNE) || ...);
+    static constexpr bool cluster = ((OPS == OP_CLUSTER_TSE || OPS == OP_CLUSTER_UTS) || ...);
+};
+
+// compile-time op sequence: dead ops are compiled out, registers sized for the sequence
+template <int G, int... OPS>
+__global__ void __launch_bounds__(BLOCK) k_node_seq(gtf_graph g, gtf_nodes n, gtf_states tse, gtf_states uts,
+                                                    gtf_edges e, gtf_params p, Ws w, double chi2_thr, double kl_thr,
+                                                    const int32_t* list, int count) {
+    using Q = OpSeq<OPS...>;
+    __shared__ volatile double s_val[BLOCK];
+    __shared__ volatile Stage s_stage[Q::cluster ? BLOCK / G : 1];
+    NodeCtx<G> c;
+    if (!node_load(c, g, n, tse, uts, e, list, count, Q::uses_tse, Q::uses_uts)) return;
+    volatile double* sval = s_val + (threadIdx.x & ~63);
+    volatile Stage* stg = s_stage + (Q::cluster ? (int)threadIdx.x / G : 0);
+    const bool has_tse = n.has_tse[c.v], has_uts = n.has_uts[c.v];
+    (node_op<G, OPS>(c, g, n, tse, uts, p, w, sval, stg, chi2_thr, kl_thr, has_tse, has_uts), ...);
+    node_store(c, n, tse, uts, e);
+}
+
+// run-time op sequence (gtf_node_ops): any order of any ops
+template <int G>
+__global__ void __launch_bounds__(BLOCK) k_node_group(gtf_graph g, gtf_nodes n, gtf_states tse, gtf_states uts,
+                                                      gtf_edges e, gtf_params p, Ws w, NodeOps ops,
+                                                      double chi2_thr, double kl_thr, const int32_t* list,
+                                                      int count) {
+    __shared__ volatile double s_val[BLOCK];
+    __shared__ volatile Stage s_stage[BLOCK / G];
+    NodeCtx<G> c;
+    if (!node_load(c, g, n, tse, uts, e, list, count, ops.uses_tse, ops.uses_uts)) return;
+    volatile double* sval = s_val + (threadIdx.x & ~63);
+    volatile Stage* stg = s_stage + (int)threadIdx.x / G;
+    const bool has_tse = n.has_tse[c.v], has_uts = n.has_uts[c.v];
+    for (int i = 0; i < ops.n; i++) {
+        switch (ops.op[i]) {
+#define GTF_CASE(OPC) \
+    case OPC: node_op<G, OPC>(c, g, n, tse, uts, p, w, sval, stg, chi2_thr, kl_thr, has_tse, has_uts); break;
+            GTF_CASE(OP_RANKS)
+            GTF_CASE(OP_PRIORS_TSE)
+            GTF_CASE(OP_PRIORS_UTS)
+            GTF_CASE(OP_REWEIGHT_UTS)
+            GTF_CASE(OP_DEGREE)
+            GTF_CASE(OP_PRUNE)
+            GTF_CASE(OP_MW_TSE)
+            GTF_CASE(OP_MW_UTS)
+            GTF_CASE(OP_CLUSTER_TSE)
+            GTF_CASE(OP_CLUSTER_UTS)
+#undef GTF_CASE
+            default: break;
+        }
+    }
+    node_store(c, n, tse, uts, e);
 }

@@ -518,12 +518,6 @@ __global__ void __launch_bounds__(BLOCK) k_node(gtf_graph g, gtf_nodes n, gtf_st
 
 #include "gtf_node_group.h"
 
-// stage bodies as op sequences
-const int8_t SEQ_EXTRAP[] = {OP_RANKS, OP_PRIORS_UTS, OP_REWEIGHT_UTS, OP_PRIORS_UTS, OP_REWEIGHT_UTS, OP_DEGREE};
-const int8_t SEQ_UPDATE[] = {OP_PRUNE, OP_PRIORS_TSE, OP_PRIORS_UTS, OP_REWEIGHT_UTS};
-const int8_t SEQ_CLUSTER_UTS[] = {OP_CLUSTER_UTS, OP_DEGREE, OP_MW_UTS, OP_PRIORS_UTS};
-const int8_t SEQ_CLUSTER_TSE[] = {OP_CLUSTER_TSE, OP_DEGREE, OP_MW_TSE, OP_PRIORS_TSE};
-
 thread_local char g_err[512] = "";
 
 int fail(const char* what, hipError_t e) {
@@ -554,6 +548,33 @@ int launch_extrap_edges(const gtf_graph* g, gtf_nodes* n, gtf_states* uts, gtf_e
     return err == hipSuccess ? 0 : fail("extrapolate launch", err);
 }
 
+void finish_ops(NodeOps& ops, const gtf_states* tse, const gtf_states* uts) {
+    for (int i = 0; i < ops.n; i++) {
+        const int o = ops.op[i];
+        if (o == OP_PRIORS_TSE || o == OP_MW_TSE || o == OP_CLUSTER_TSE || o == OP_PRUNE) ops.uses_tse = 1;
+        if (o == OP_RANKS || o == OP_PRIORS_UTS || o == OP_REWEIGHT_UTS || o == OP_MW_UTS || o == OP_CLUSTER_UTS ||
+            o == OP_PRUNE)
+            ops.uses_uts = 1;
+    }
+    if (!tse) ops.uses_tse = 0;
+    if (!uts) ops.uses_uts = 0;
+}
+
+// nodes the group kernels do not cover (> 64 slots, or no schedule) run one thread per node
+void launch_serial_rest(const gtf_graph* g, gtf_nodes* n, const gtf_states& T, const gtf_states& U, gtf_edges* e,
+                        const gtf_params* p, Ws w, const NodeOps& ops, double chi2, double kl, hipStream_t st) {
+    if (g->sched) {
+        const int nbig = g->n_nodes - g->n_g16 - g->n_g64;
+        if (nbig > 0)
+            hipLaunchKernelGGL(k_node, dim3(grid(nbig)), dim3(BLOCK), 0, st, *g, *n, T, U, *e, *p, w, ops, chi2, kl,
+                               g->sched + g->n_g16 + g->n_g64, nbig);
+    } else if (g->n_nodes > 0) {
+        hipLaunchKernelGGL(k_node, dim3(grid(g->n_nodes)), dim3(BLOCK), 0, st, *g, *n, T, U, *e, *p, w, ops, chi2, kl,
+                           (const int32_t*)nullptr, g->n_nodes);
+    }
+}
+
+// run-time op list (gtf_node_ops)
 int launch_ops(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts, gtf_edges* e,
                const gtf_params* p, Ws w, const int8_t* const* seqs, const int* lens, int nseq, double chi2,
                double kl, hipStream_t st) {
@@ -567,39 +588,56 @@ int launch_ops(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* ut
             }
             ops.op[ops.n++] = seqs[q][i];
         }
+    finish_ops(ops, tse, uts);
     gtf_states dummy;
     memset(&dummy, 0, sizeof(dummy));
-    for (int i = 0; i < ops.n; i++) {
-        const int o = ops.op[i];
-        if (o == OP_PRIORS_TSE || o == OP_MW_TSE || o == OP_CLUSTER_TSE || o == OP_PRUNE) ops.uses_tse = 1;
-        if (o == OP_RANKS || o == OP_PRIORS_UTS || o == OP_REWEIGHT_UTS || o == OP_MW_UTS || o == OP_CLUSTER_UTS ||
-            o == OP_PRUNE)
-            ops.uses_uts = 1;
-    }
-    if (!tse) ops.uses_tse = 0;
-    if (!uts) ops.uses_uts = 0;
     const gtf_states T = tse ? *tse : dummy, U = uts ? *uts : dummy;
     if (g->n_nodes > 0 && ops.n > 0) {
         if (g->sched) {
-            // degree-bucketed schedule: 16-lane groups, 64-lane groups, then one thread per node
-            const int n16 = g->n_g16, n64 = g->n_g64, nbig = g->n_nodes - n16 - n64;
-            if (n16 > 0)
-                hipLaunchKernelGGL(k_node_group<16>, dim3((n16 + BLOCK / 16 - 1) / (BLOCK / 16)), dim3(BLOCK), 0, st,
-                                   *g, *n, T, U, *e, *p, w, ops, chi2, kl, g->sched, n16);
-            if (n64 > 0)
-                hipLaunchKernelGGL(k_node_group<64>, dim3((n64 + BLOCK / 64 - 1) / (BLOCK / 64)), dim3(BLOCK), 0, st,
-                                   *g, *n, T, U, *e, *p, w, ops, chi2, kl, g->sched + n16, n64);
-            if (nbig > 0)
-                hipLaunchKernelGGL(k_node, dim3(grid(nbig)), dim3(BLOCK), 0, st, *g, *n, T, U, *e, *p, w, ops, chi2, kl,
-                                   g->sched + n16 + n64, nbig);
-        } else {
-            hipLaunchKernelGGL(k_node, dim3(grid(g->n_nodes)), dim3(BLOCK), 0, st, *g, *n, T, U, *e, *p, w, ops, chi2,
-                               kl, (const int32_t*)nullptr, g->n_nodes);
+            if (g->n_g16 > 0)
+                hipLaunchKernelGGL(k_node_group<16>, dim3((g->n_g16 + BLOCK / 16 - 1) / (BLOCK / 16)), dim3(BLOCK), 0,
+                                   st, *g, *n, T, U, *e, *p, w, ops, chi2, kl, g->sched, g->n_g16);
+            if (g->n_g64 > 0)
+                hipLaunchKernelGGL(k_node_group<64>, dim3((g->n_g64 + BLOCK / 64 - 1) / (BLOCK / 64)), dim3(BLOCK), 0,
+                                   st, *g, *n, T, U, *e, *p, w, ops, chi2, kl, g->sched + g->n_g16, g->n_g64);
         }
+        launch_serial_rest(g, n, T, U, e, p, w, ops, chi2, kl, st);
     }
     hipError_t err = hipGetLastError();
     return err == hipSuccess ? 0 : fail("node kernel launch", err);
 }
+
+// compile-time op sequence (the stage entry points)
+template <int... OPS>
+int launch_seq(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts, gtf_edges* e, const gtf_params* p,
+               Ws w, double chi2, double kl, hipStream_t st) {
+    NodeOps ops;
+    memset(&ops, 0, sizeof(ops));
+    const int8_t list[] = {(int8_t)OPS...};
+    for (int8_t o : list) ops.op[ops.n++] = o;
+    finish_ops(ops, tse, uts);
+    gtf_states dummy;
+    memset(&dummy, 0, sizeof(dummy));
+    const gtf_states T = tse ? *tse : dummy, U = uts ? *uts : dummy;
+    if (g->n_nodes > 0) {
+        if (g->sched) {
+            if (g->n_g16 > 0)
+                hipLaunchKernelGGL((k_node_seq<16, OPS...>), dim3((g->n_g16 + BLOCK / 16 - 1) / (BLOCK / 16)),
+                                   dim3(BLOCK), 0, st, *g, *n, T, U, *e, *p, w, chi2, kl, g->sched, g->n_g16);
+            if (g->n_g64 > 0)
+                hipLaunchKernelGGL((k_node_seq<64, OPS...>), dim3((g->n_g64 + BLOCK / 64 - 1) / (BLOCK / 64)),
+                                   dim3(BLOCK), 0, st, *g, *n, T, U, *e, *p, w, chi2, kl, g->sched + g->n_g16, g->n_g64);
+        }
+        launch_serial_rest(g, n, T, U, e, p, w, ops, chi2, kl, st);
+    }
+    hipError_t err = hipGetLastError();
+    return err == hipSuccess ? 0 : fail("node kernel launch", err);
+}
+
+#define EXTRAP_OPS OP_RANKS, OP_PRIORS_UTS, OP_REWEIGHT_UTS, OP_PRIORS_UTS, OP_REWEIGHT_UTS, OP_DEGREE
+#define UPDATE_OPS OP_PRUNE, OP_PRIORS_TSE, OP_PRIORS_UTS, OP_REWEIGHT_UTS
+#define CLUSTER_UTS_OPS OP_CLUSTER_UTS, OP_DEGREE, OP_MW_UTS, OP_PRIORS_UTS
+#define CLUSTER_TSE_OPS OP_CLUSTER_TSE, OP_DEGREE, OP_MW_TSE, OP_PRIORS_TSE
 
 #define SEQ(x) x, (int)sizeof(x)
 
@@ -630,9 +668,7 @@ int gtf_message_passing(const gtf_graph* g, gtf_nodes* n, gtf_states* uts, gtf_e
     Ws w = carve(ws, g->n_nodes, g->n_slots);
     rc = launch_extrap_edges(g, n, uts, e, p, w, (hipStream_t)stream);
     if (rc) return rc;
-    const int8_t* seqs[] = {SEQ_EXTRAP};
-    const int lens[] = {1};  // OP_RANKS only
-    return launch_ops(g, n, nullptr, uts, e, p, w, seqs, lens, 1, 0.0, 0.0, (hipStream_t)stream);
+    return launch_seq<OP_RANKS>(g, n, nullptr, uts, e, p, w, 0.0, 0.0, (hipStream_t)stream);
 }
 
 int gtf_node_ops(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts, gtf_edges* e,
@@ -658,9 +694,7 @@ int gtf_extrapolate(const gtf_graph* g, gtf_nodes* n, gtf_states* uts, gtf_edges
     Ws w = carve(ws, g->n_nodes, g->n_slots);
     rc = launch_extrap_edges(g, n, uts, e, p, w, (hipStream_t)stream);
     if (rc) return rc;
-    const int8_t* seqs[] = {SEQ_EXTRAP};
-    const int lens[] = {(int)sizeof(SEQ_EXTRAP)};
-    return launch_ops(g, n, nullptr, uts, e, p, w, seqs, lens, 1, 0.0, 0.0, (hipStream_t)stream);
+    return launch_seq<EXTRAP_OPS>(g, n, nullptr, uts, e, p, w, 0.0, 0.0, (hipStream_t)stream);
 }
 
 int gtf_update(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts, gtf_edges* e,
@@ -668,9 +702,7 @@ int gtf_update(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* ut
     int rc = check_graph(g);
     if (rc) return rc;
     Ws w = carve(ws, g->n_nodes, g->n_slots);
-    const int8_t* seqs[] = {SEQ_UPDATE};
-    const int lens[] = {(int)sizeof(SEQ_UPDATE)};
-    return launch_ops(g, n, tse, uts, e, p, w, seqs, lens, 1, 0.0, 0.0, (hipStream_t)stream);
+    return launch_seq<UPDATE_OPS>(g, n, tse, uts, e, p, w, 0.0, 0.0, (hipStream_t)stream);
 }
 
 int gtf_cluster(const gtf_graph* g, gtf_nodes* n, gtf_states* states, gtf_edges* e, int32_t key,
@@ -678,10 +710,11 @@ int gtf_cluster(const gtf_graph* g, gtf_nodes* n, gtf_states* states, gtf_edges*
     int rc = check_graph(g);
     if (rc) return rc;
     Ws w = carve(ws, g->n_nodes, g->n_slots);
-    const int8_t* seqs[] = {key ? SEQ_CLUSTER_UTS : SEQ_CLUSTER_TSE};
-    const int lens[] = {(int)sizeof(SEQ_CLUSTER_UTS)};
-    return launch_ops(g, n, key ? nullptr : states, key ? states : nullptr, e, p, w, seqs, lens, 1, chi2_threshold,
-                      kl_threshold, (hipStream_t)stream);
+    if (key)
+        return launch_seq<CLUSTER_UTS_OPS>(g, n, nullptr, states, e, p, w, chi2_threshold, kl_threshold,
+                                           (hipStream_t)stream);
+    return launch_seq<CLUSTER_TSE_OPS>(g, n, states, nullptr, e, p, w, chi2_threshold, kl_threshold,
+                                       (hipStream_t)stream);
 }
 
 int gtf_pass_ev(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts, gtf_edges* e,
@@ -699,9 +732,11 @@ int gtf_pass_ev(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* u
     if (events) (void)hipEventRecord((hipEvent_t)events[2], st);
     hipError_t err = hipGetLastError();
     if (err != hipSuccess) return fail("extrapolate launch", err);
-    const int8_t* seqs[] = {SEQ_EXTRAP, SEQ_UPDATE, SEQ_CLUSTER_UTS};
-    const int lens[] = {(int)sizeof(SEQ_EXTRAP), (int)sizeof(SEQ_UPDATE), (int)sizeof(SEQ_CLUSTER_UTS)};
-    rc = launch_ops(g, n, tse, uts, e, p, w, seqs, lens, 3, p->cluster_chi2, p->cluster_kl, st);
+    // node-local work in two launches: the light reweight/update sequence at high
+    // occupancy, then clustering (register-heavy) with its LDS state staging
+    rc = launch_seq<EXTRAP_OPS, UPDATE_OPS>(g, n, tse, uts, e, p, w, 0.0, 0.0, st);
+    if (rc) return rc;
+    rc = launch_seq<CLUSTER_UTS_OPS>(g, n, tse, uts, e, p, w, p->cluster_chi2, p->cluster_kl, st);
     if (events) (void)hipEventRecord((hipEvent_t)events[3], st);
     return rc;
 }

@@ -17,35 +17,25 @@ struct Cov5 {
     double c00, c01, c10, c11, c22;
 };
 
-// LAPACK-style 2x2 inverse (dgetrf partial pivoting, then solve A X = I), the
-// path np.linalg.inv takes; keeps the result close to the reference's bits.
+// 2x2 inverse the way np.linalg.inv gets it from OpenBLAS (dgesv = getf2 LU with
+// partial pivoting, then triangular solves): the pivot and u22 are inverted once
+// and multiplied (getf2 scales by 1/pivot, the trsm kernels store the inverted
+// diagonal), so each inverse costs two divisions.
 __device__ __forceinline__ void inv2(double a, double b, double c, double d, double& i00, double& i01,
                                      double& i10, double& i11) {
-    if (fabs(c) > fabs(a)) {
-        // rows swapped: P A = [[c d][a b]]
-        double l = a / c;
-        double u22 = b - l * d;
-        // solve for columns of P^-1 ... P A X = P I ; P I = [[0 1][1 0]]
-        // column 0 of X: rhs (0, 1)
-        double y1 = 1.0 - l * 0.0;
-        double x1 = y1 / u22;
-        double x0 = (0.0 - d * x1) / c;
-        // column 1 of X: rhs (1, 0)
-        double z1 = 0.0 - l * 1.0;
-        double w1 = z1 / u22;
-        double w0 = (1.0 - d * w1) / c;
-        i00 = x0; i10 = x1; i01 = w0; i11 = w1;
-    } else {
-        double l = c / a;
-        double u22 = d - l * b;
-        double y1 = 0.0 - l * 1.0;
-        double x1 = y1 / u22;
-        double x0 = (1.0 - b * x1) / a;
-        double z1 = 1.0 - l * 0.0;
-        double w1 = z1 / u22;
-        double w0 = (0.0 - b * w1) / a;
-        i00 = x0; i10 = x1; i01 = w0; i11 = w1;
-    }
+    const bool sw = fabs(c) > fabs(a);
+    const double p0 = sw ? c : a, p1 = sw ? d : b;   // pivot row
+    const double q0 = sw ? a : c, q1 = sw ? b : d;   // other row
+    const double rp = 1.0 / p0;
+    const double l = q0 * rp;
+    const double u22 = q1 - l * p1;
+    const double ru = 1.0 / u22;
+    // columns of P*I: e0 -> (sw ? (0,1) : (1,0)), e1 -> (sw ? (1,0) : (0,1))
+    const double y0a = sw ? 0.0 : 1.0, y1a = (sw ? 1.0 : 0.0) - l * y0a;
+    const double x1a = y1a * ru, x0a = (y0a - p1 * x1a) * rp;
+    const double y0b = sw ? 1.0 : 0.0, y1b = (sw ? 0.0 : 1.0) - l * y0b;
+    const double x1b = y1b * ru, x0b = (y0b - p1 * x1b) * rp;
+    i00 = x0a; i10 = x1a; i01 = x0b; i11 = x1b;
 }
 
 __device__ __forceinline__ Cov5 inv_cov5(const Cov5& m) {
@@ -66,13 +56,10 @@ __device__ __forceinline__ void mv_cov5(const Cov5& m, const double x[3], double
     y[2] = m.c22 * x[2];
 }
 
-// merge_states (clustering.py:97-105): inverse-variance weighted mean
-__device__ __forceinline__ void merge_states(const double m1[3], const Cov5& c1, const double m2[3], const Cov5& c2,
-                                             double mo[3], Cov5& co) {
-    Cov5 i1 = inv_cov5(c1);
-    Cov5 i2 = inv_cov5(c2);
-    Cov5 s = add_cov5(i1, i2);
-    co = inv_cov5(s);
+// merge_states (clustering.py:97-105) given the two inverses already computed:
+// merged_cov = (I1 + I2)^-1, merged_mean = merged_cov (I1 m1 + I2 m2)
+__device__ __forceinline__ void merge_with_inv(const double m1[3], const Cov5& i1, const double m2[3], const Cov5& i2,
+                                               const Cov5& co, double mo[3]) {
     double a[3], b[3], t[3];
     mv_cov5(i1, m1, a);
     mv_cov5(i2, m2, b);
@@ -82,61 +69,95 @@ __device__ __forceinline__ void merge_states(const double m1[3], const Cov5& c1,
     mv_cov5(co, t, mo);
 }
 
-// KLDistance (clustering.py:90-94): trace((C1-C2) .* (I2-I1)) + dm' (I1+I2) dm
-__device__ __forceinline__ double kl_distance(const double m1[3], const Cov5& c1, const double m2[3], const Cov5& c2) {
-    Cov5 i1 = inv_cov5(c1);
-    Cov5 i2 = inv_cov5(c2);
+__device__ __forceinline__ void merge_states(const double m1[3], const Cov5& c1, const double m2[3], const Cov5& c2,
+                                             double mo[3], Cov5& co) {
+    const Cov5 i1 = inv_cov5(c1);
+    const Cov5 i2 = inv_cov5(c2);
+    co = inv_cov5(add_cov5(i1, i2));
+    merge_with_inv(m1, i1, m2, i2, co, mo);
+}
+
+// KLDistance (clustering.py:90-94) given both inverses:
+// trace((C1-C2) .* (I2-I1)) + dm' (I1+I2) dm
+__device__ __forceinline__ double kl_with_inv(const double m1[3], const Cov5& c1, const Cov5& i1, const double m2[3],
+                                              const Cov5& c2, const Cov5& i2) {
     double tr = (c1.c00 - c2.c00) * (i2.c00 - i1.c00);
     tr = tr + (c1.c11 - c2.c11) * (i2.c11 - i1.c11);
     tr = tr + (c1.c22 - c2.c22) * (i2.c22 - i1.c22);
-    Cov5 s = add_cov5(i1, i2);
-    double d0 = m1[0] - m2[0], d1 = m1[1] - m2[1], d2 = m1[2] - m2[2];
-    double w0 = d0 * s.c00 + d1 * s.c10;
-    double w1 = d0 * s.c01 + d1 * s.c11;
-    double w2 = d2 * s.c22;
+    const Cov5 s = add_cov5(i1, i2);
+    const double d0 = m1[0] - m2[0], d1 = m1[1] - m2[1], d2 = m1[2] - m2[2];
+    const double w0 = d0 * s.c00 + d1 * s.c10;
+    const double w1 = d0 * s.c01 + d1 * s.c11;
+    const double w2 = d2 * s.c22;
     double q = w0 * d0 + w1 * d1;
     q = q + w2 * d2;
     return tr + q;
 }
 
-// mahalanobis_distance (clustering.py:11-78); variant=1 is the updated-state
-// flavour of calculate_distance_between_updated_track_states.py:27-104.
+__device__ __forceinline__ double kl_distance(const double m1[3], const Cov5& c1, const double m2[3], const Cov5& c2) {
+    return kl_with_inv(m1, c1, inv_cov5(c1), m2, c2, inv_cov5(c2));
+}
+
+// Per-neighbour geometry of the tau term of mahalanobis_distance (clustering.py:37-75),
+// computed once per state instead of once per pair; every pair value is built from
+// these with the reference's operation order (j1 = -j3 - j2 = q_j - q_i, j4 = -j5 - j6).
+struct TauGeo {
+    double q;    // 1 / (r - r_a)             (j2 of the pair's first state, -j3 of its second)
+    double w;    // (z - z_a) / (r - r_a)**2  (-j5 / j6)
+    double tau;  // (z - z_a) / (r - r_a)
+    double sz2, sr2;  // sigma_z**2, sigma_r**2 of this hit (endcap swap on |x|)
+};
+
+__device__ __forceinline__ TauGeo tau_geo(double x, double z, double r, double za, double ra, double sz_barrel,
+                                          double sr_barrel, double sz_endcap, double sr_endcap, double boundary) {
+    TauGeo t;
+    const double dr = r - ra, dz = z - za;
+    t.q = 1.0 / dr;
+    t.w = dz / (dr * dr);
+    t.tau = dz / dr;
+    const bool ec = fabs(x) >= boundary;
+    const double sz = ec ? sz_endcap : sz_barrel, sr = ec ? sr_endcap : sr_barrel;
+    t.sz2 = sz * sz;
+    t.sr2 = sr * sr;
+    return t;
+}
+
+// mahalanobis_distance (clustering.py:11-78) from [a, b], the 2x2 covariance blocks,
+// the node's sigma pair and the two neighbours' TauGeo.
+__device__ __forceinline__ double mahalanobis_geo(double a1, double b1, const Cov5& c1, double a2, double b2,
+                                                  const Cov5& c2, double sza2, double sra2, const TauGeo& gb,
+                                                  const TauGeo& gc) {
+    const double r0 = a1 - a2, r1 = b1 - b2;
+    double i00, i01, i10, i11;
+    inv2(c1.c00 + c2.c00, c1.c01 + c2.c01, c1.c10 + c2.c10, c1.c11 + c2.c11, i00, i01, i10, i11);
+    const double t0 = r0 * i00 + r1 * i10;
+    const double t1 = r0 * i01 + r1 * i11;
+    const double d1 = t0 * r0 + t1 * r1;
+    const double j2 = gb.q, j3 = -gc.q;
+    const double j1 = -j3 - j2;
+    const double j5 = -gb.w, j6 = gc.w;
+    const double j4 = -j5 - j6;
+    double cdt = (j1 * sza2) * j1;
+    cdt = cdt + (j2 * gb.sz2) * j2;
+    cdt = cdt + (j3 * gc.sz2) * j3;
+    cdt = cdt + (j4 * sra2) * j4;
+    cdt = cdt + (j5 * gb.sr2) * j5;
+    cdt = cdt + (j6 * gc.sr2) * j6;
+    const double res = gb.tau - gc.tau;
+    const double d2 = (res * res) * (1.0 / cdt);
+    return d1 + d2;
+}
+
+// mahalanobis from raw coordinates (thread-per-node path)
 __device__ __forceinline__ double mahalanobis(double a1, double b1, const Cov5& c1, double a2, double b2,
                                               const Cov5& c2, const double* na, const double* nb,
                                               const double* nc, double sz_barrel, double sr_barrel,
                                               double sz_endcap, double sr_endcap, double boundary) {
-    double r0 = a1 - a2, r1 = b1 - b2;
-    double i00, i01, i10, i11;
-    inv2(c1.c00 + c2.c00, c1.c01 + c2.c01, c1.c10 + c2.c10, c1.c11 + c2.c11, i00, i01, i10, i11);
-    double t0 = r0 * i00 + r1 * i10;
-    double t1 = r0 * i01 + r1 * i11;
-    double d1 = t0 * r0 + t1 * r1;
-    double x_a = na[0], x_b = nb[0], x_c = nc[0];
-    double z_a = na[2], r_a = na[3], z_b = nb[2], r_b = nb[3], z_c = nc[2], r_c = nc[3];
-    double j2 = 1.0 / (r_b - r_a);
-    double j3 = -1.0 / (r_c - r_a);
-    double j1 = -j3 - j2;
-    double drb = r_b - r_a, drc = r_c - r_a;
-    double j5 = -(z_b - z_a) / (drb * drb);
-    double j6 = (z_c - z_a) / (drc * drc);
-    double j4 = -j5 - j6;
-    double sza = sz_barrel, szb = sz_barrel, szc = sz_barrel;
-    double sra = sr_barrel, srb = sr_barrel, src = sr_barrel;
-    if (fabs(x_a) >= boundary) { sza = sz_endcap; sra = sr_endcap; }
-    if (fabs(x_b) >= boundary) { szb = sz_endcap; srb = sr_endcap; }
-    if (fabs(x_c) >= boundary) { szc = sz_endcap; src = sr_endcap; }
-    double cdt = (j1 * (sza * sza)) * j1;
-    cdt = cdt + (j2 * (szb * szb)) * j2;
-    cdt = cdt + (j3 * (szc * szc)) * j3;
-    cdt = cdt + (j4 * (sra * sra)) * j4;
-    cdt = cdt + (j5 * (srb * srb)) * j5;
-    cdt = cdt + (j6 * (src * src)) * j6;
-    double inv_cdt = 1.0 / cdt;
-    double tau1 = (z_b - z_a) / drb;
-    double tau2 = (z_c - z_a) / drc;
-    double res = tau1 - tau2;
-    double d2 = (res * res) * inv_cdt;
-    return d1 + d2;
+    const TauGeo gb = tau_geo(nb[0], nb[2], nb[3], na[2], na[3], sz_barrel, sr_barrel, sz_endcap, sr_endcap, boundary);
+    const TauGeo gc = tau_geo(nc[0], nc[2], nc[3], na[2], na[3], sz_barrel, sr_barrel, sz_endcap, sr_endcap, boundary);
+    const bool ec = fabs(na[0]) >= boundary;
+    const double sza = ec ? sz_endcap : sz_barrel, sra = ec ? sr_endcap : sr_barrel;
+    return mahalanobis_geo(a1, b1, c1, a2, b2, c2, sza * sza, sra * sra, gb, gc);
 }
 
 struct Mat3 {

@@ -272,19 +272,34 @@ __constant__ uint8_t c_pair_j[105] = {
     0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11,
     0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13};
 
-// per-group LDS staging of up to 15 states (structure of arrays)
+// per-group LDS staging of up to 15 states (structure of arrays): the state, its
+// covariance and inverse (computed once per state: np.linalg.inv of a state's
+// covariance is the same value every time the reference recomputes it), and the
+// per-neighbour tau geometry of the pairwise chi2
 struct Stage {
-    double a[16], b[16], c[16], tau[16], c00[16], c01[16], c10[16], c11[16], c22[16], x[16], z[16], r[16],
-        prior[16];
+    double a[16], b[16], c[16], tau[16];
+    double c00[16], c01[16], c10[16], c11[16], c22[16];
+    double i00[16], i01[16], i10[16], i11[16], i22[16];
+    double q[16], w[16], tg[16], sz2[16], sr2[16], prior[16];
 };
 
 __device__ __forceinline__ Cov5 stage_cov(const volatile Stage* s, int i) {
     return Cov5{s->c00[i], s->c01[i], s->c10[i], s->c11[i], s->c22[i]};
 }
+__device__ __forceinline__ Cov5 stage_inv(const volatile Stage* s, int i) {
+    return Cov5{s->i00[i], s->i01[i], s->i10[i], s->i11[i], s->i22[i]};
+}
+__device__ __forceinline__ TauGeo stage_geo(const volatile Stage* s, int i) {
+    TauGeo t;
+    t.q = s->q[i]; t.w = s->w[i]; t.tau = s->tg[i]; t.sz2 = s->sz2[i]; t.sr2 = s->sr2[i];
+    return t;
+}
 
 // pairwise chi2 + greedy KL merging of one node (clustering.py:197-307). The
 // d(d-1)/2 pairs are dealt round-robin over the G lanes (row-major pair index t),
-// so the np.where tie order is the order of t.
+// so the np.where tie order is the order of t. The parabolic and the joint merge
+// share their covariance (both merge the same aliased covariances), so one
+// (I1 + I2)^-1 serves both means.
 template <int G>
 __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf_states& S, LaneDict& st,
                                           volatile Stage* stg, const double* xyzr_node, double chi2_thr,
@@ -293,6 +308,7 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
     const int d = c.grp.count(pres);
     if (d <= 2 || d >= 16) return;                                                 // :207
     const int pos = dict_pos(c, st);
+    const double xa = xyzr_node[0], za = xyzr_node[2], ra = xyzr_node[3];
     if (pres) {
         const int64_t k = c.k;
         stg->a[pos] = S.sv[3 * k];
@@ -300,15 +316,21 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
         stg->c[pos] = S.sv[3 * k + 2];
         stg->tau[pos] = S.tau[k];
         const double* cv = S.cov + 5 * k;
-        stg->c00[pos] = cv[0]; stg->c01[pos] = cv[1]; stg->c10[pos] = cv[2]; stg->c11[pos] = cv[3];
-        stg->c22[pos] = cv[4];
-        stg->x[pos] = S.xyzr[4 * k];
-        stg->z[pos] = S.xyzr[4 * k + 2];
-        stg->r[pos] = S.xyzr[4 * k + 3];
+        const Cov5 C{cv[0], cv[1], cv[2], cv[3], cv[4]};
+        const Cov5 I = inv_cov5(C);
+        stg->c00[pos] = C.c00; stg->c01[pos] = C.c01; stg->c10[pos] = C.c10; stg->c11[pos] = C.c11;
+        stg->c22[pos] = C.c22;
+        stg->i00[pos] = I.c00; stg->i01[pos] = I.c01; stg->i10[pos] = I.c10; stg->i11[pos] = I.c11;
+        stg->i22[pos] = I.c22;
+        const TauGeo t = tau_geo(S.xyzr[4 * k], S.xyzr[4 * k + 2], S.xyzr[4 * k + 3], za, ra, p.sigma0rz2, p.sigma0rz,
+                                 p.sigma0rz, p.sigma0rz2, p.endcap_boundary);
+        stg->q[pos] = t.q; stg->w[pos] = t.w; stg->tg[pos] = t.tau; stg->sz2[pos] = t.sz2; stg->sr2[pos] = t.sr2;
         stg->prior[pos] = st.prior;
     }
     __builtin_amdgcn_wave_barrier();
-    const double na[4] = {xyzr_node[0], xyzr_node[1], xyzr_node[2], xyzr_node[3]};
+    const bool ec = fabs(xa) >= p.endcap_boundary;
+    const double sza = ec ? p.sigma0rz : p.sigma0rz2, sra = ec ? p.sigma0rz2 : p.sigma0rz;
+    const double sza2 = sza * sza, sra2 = sra * sra;
     const int npairs = d * (d - 1) / 2;
     double lmin = INFINITY;
     int lt0 = 1 << 20, lt1 = 1 << 20;
@@ -316,10 +338,8 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
     bool lnan = false, lnz = false;
     for (int t = c.grp.gl; t < npairs; t += G) {
         const int i = c_pair_i[t], j = c_pair_j[t];
-        const double ni[4] = {stg->x[i], 0.0, stg->z[i], stg->r[i]};
-        const double nj[4] = {stg->x[j], 0.0, stg->z[j], stg->r[j]};
-        const double D = mahalanobis(stg->a[i], stg->b[i], stage_cov(stg, i), stg->a[j], stg->b[j], stage_cov(stg, j),
-                                     na, ni, nj, p.sigma0rz2, p.sigma0rz, p.sigma0rz, p.sigma0rz2, p.endcap_boundary);
+        const double D = mahalanobis_geo(stg->a[i], stg->b[i], stage_cov(stg, i), stg->a[j], stg->b[j],
+                                         stage_cov(stg, j), sza2, sra2, stage_geo(stg, i), stage_geo(stg, j));
         if (D == 0.0) continue;  // zeros are excluded (np.nonzero)
         lnz = true;
         if (D != D) { lnan = true; continue; }
@@ -345,15 +365,16 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
     // merged pair = (idx[0], idx[1]) of concatenate((rows, cols)) (:231-233)
     const int p0 = ti0, p1 = (t1 < (1 << 20)) ? (int)c_pair_i[t1] : tj0;
     double pm[3], jm[3];
-    Cov5 pc, jc;
+    Cov5 mc;
     {
+        const Cov5 i0 = stage_inv(stg, p0), i1 = stage_inv(stg, p1);
+        mc = inv_cov5(add_cov5(i0, i1));
         const double ps0[3] = {stg->a[p0], stg->b[p0], stg->c[p0]};
         const double ps1[3] = {stg->a[p1], stg->b[p1], stg->c[p1]};
         const double js0[3] = {ps0[0], ps0[1], stg->tau[p0]};
         const double js1[3] = {ps1[0], ps1[1], stg->tau[p1]};
-        const Cov5 c0 = stage_cov(stg, p0), c1 = stage_cov(stg, p1);
-        merge_states(ps0, c0, ps1, c1, pm, pc);
-        merge_states(js0, c0, js1, c1, jm, jc);
+        merge_with_inv(ps0, i0, ps1, i1, mc, pm);
+        merge_with_inv(js0, i0, js1, i1, mc, jm);
     }
     double mprior = stg->prior[p0] + stg->prior[p1];
     unsigned alive = ((1u << d) - 1u) & ~tiemask;
@@ -361,12 +382,13 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
         if (c.grp.gl == 0) atomicOr(err, (uint32_t)GTF_ERR_TIE_EMPTIED);
     } else {
         while (true) {                                                             // :251-287
+            const Cov5 im = inv_cov5(mc);   // the merged state's inverse, shared by KL and the next merge
             const bool me = pres && (alive >> pos & 1u);
             double D = INFINITY;
             bool dn = false;
             if (me) {
                 const double js_me[3] = {stg->a[pos], stg->b[pos], stg->tau[pos]};
-                D = kl_distance(js_me, stage_cov(stg, pos), jm, jc);
+                D = kl_with_inv(js_me, stage_cov(stg, pos), stage_inv(stg, pos), jm, mc, im);
                 if (D != D) { dn = true; D = INFINITY; }
             }
             if (c.grp.any(dn)) {
@@ -376,15 +398,16 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
             const double mind = c.grp.min_d(D);
             if (!(mind < kl_thr)) break;
             const int m = c.grp.min_i((me && D == mind) ? pos : 99);  // first minimum (list.index)
+            const Cov5 ii = stage_inv(stg, m);
+            const Cov5 nmc = inv_cov5(add_cov5(ii, im));
             const double ps[3] = {stg->a[m], stg->b[m], stg->c[m]};
             const double js[3] = {ps[0], ps[1], stg->tau[m]};
-            const Cov5 ci = stage_cov(stg, m);
             double npm[3], njm[3];
-            Cov5 npc, njc;
-            merge_states(ps, ci, pm, pc, npm, npc);
-            merge_states(js, ci, jm, jc, njm, njc);
-            pm[0] = npm[0]; pm[1] = npm[1]; pm[2] = npm[2]; pc = npc;
-            jm[0] = njm[0]; jm[1] = njm[1]; jm[2] = njm[2]; jc = njc;
+            merge_with_inv(ps, ii, pm, im, nmc, npm);
+            merge_with_inv(js, ii, jm, im, nmc, njm);
+            pm[0] = npm[0]; pm[1] = npm[1]; pm[2] = npm[2];
+            jm[0] = njm[0]; jm[1] = njm[1]; jm[2] = njm[2];
+            mc = nmc;
             mprior = stg->prior[m] + mprior;
             alive &= ~(1u << m);
             if (alive == 0) break;
@@ -396,7 +419,7 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
         n.merged_state[3 * (int64_t)c.v + 0] = pm[0];
         n.merged_state[3 * (int64_t)c.v + 1] = pm[1];
         n.merged_state[3 * (int64_t)c.v + 2] = pm[2];
-        store_cov5(n.merged_cov, c.v, pc);
+        store_cov5(n.merged_cov, c.v, mc);
         n.merged_prior[c.v] = mprior;
     }
     if (pres && (alive >> pos & 1u) && c.is_edge) c.act = 0;                       // :311-321

@@ -2,10 +2,11 @@
 // gfx950 (MI355X), behind the C-ABI of include/gtf.h.
 //
 // Work decomposition (DESIGN.md "Kernels"):
-//   k_sender_scan     1 thread / sender node: walks the node's active out-edges in
-//                     successor order and forms the running merged_cov[1,1] += var_ms
-//                     that each extrapolation sees (the in-place mutation of
-//                     extrapolate_merged_states.py:127-128, an inclusive sequential scan).
+//   k_varms           1 thread / slot: Highland var_ms of every active out-edge of a
+//                     merged sender (extrapolate_merged_states.py:114-124).
+//   (k_extrapolate then forms the running merged_cov[1,1] += var_ms each extrapolation
+//                     sees -- the in-place mutation of :127-128 -- as the sequential
+//                     prefix over the sender's out-edges up to itself, in successor order.)
 //   k_extrapolate     1 thread / slot (receiver-major, coalesced writes of the new
 //                     updated_track_states entry): parabolic extrapolation, chi2 gate,
 //                     Kalman predict + update (extrapolate_merged_states.py:26-402).
@@ -29,21 +30,21 @@ constexpr int MAX_CLUSTER = 15;  // clustering.py:207 (2 < d < 16)
 
 struct Ws {
     uint32_t* err;     // error word
-    double* c11_seen;  // [S] merged_cov[1,1] value seen by the extrapolation of out-edge (slot)
-    double* var_ms;    // [S] var_ms of that extrapolation
+    double* var_ms;    // [S] var_ms of the extrapolation along this slot's edge (-1 = edge was inactive)
+    double* c11_base;  // [N] merged_cov[1,1] before message passing
 };
 
 __host__ inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
 __host__ inline Ws carve(void* base, int32_t n_nodes, int32_t n_slots) {
-    (void)n_nodes;
     char* p = (char*)base;
     Ws w;
     w.err = (uint32_t*)p;
     p += 256;
-    w.c11_seen = (double*)p;
-    p += align256(sizeof(double) * (size_t)(n_slots > 0 ? n_slots : 1));
     w.var_ms = (double*)p;
+    p += align256(sizeof(double) * (size_t)(n_slots > 0 ? n_slots : 1));
+    w.c11_base = (double*)p;
+    (void)n_nodes;
     return w;
 }
 
@@ -79,26 +80,36 @@ __device__ __forceinline__ double highland_var_ms(double a, double b, const doub
 }
 
 // ---------------------------------------------------------------------------
-// k_sender_scan
+// k_varms: one thread per slot. Records, for every out-edge of a sender with a
+// merged state, the Highland var_ms of its extrapolation (or -1 when the edge was
+// inactive before message passing, so it does not take part in the in-place sum of
+// extrapolate_merged_states.py:127-128), and the sender's merged_cov[1,1] before it.
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(BLOCK) k_sender_scan(gtf_graph g, gtf_nodes n, gtf_edges e, gtf_params p, Ws w) {
-    int u = blockIdx.x * BLOCK + threadIdx.x;
-    if (u >= g.n_nodes || !n.has_merged[u]) return;
-    const double a = n.merged_state[3 * u + 0];
-    const double b = n.merged_state[3 * u + 1];
-    const double* ng = g.gnn + 4 * (int64_t)u;
-    double c11 = n.merged_cov[5 * (int64_t)u + 3];
-    const int lo = g.out_ptr[u], hi = g.out_ptr[u + 1];
-    for (int i = lo; i < hi; i++) {
-        const int k = g.out_slot[i];
-        if (e.act[k] != 1) continue;  // :431
-        const int v = g.slot_dst[k];
-        const double vm = highland_var_ms(a, b, ng, g.gnn + 4 * (int64_t)v, p.endcap_boundary);
-        c11 = c11 + vm;  // :128 cumulative, in successor order
-        w.c11_seen[k] = c11;
-        w.var_ms[k] = vm;
+__global__ void __launch_bounds__(BLOCK) k_varms(gtf_graph g, gtf_nodes n, gtf_edges e, gtf_params p, Ws w) {
+    const int k = blockIdx.x * BLOCK + threadIdx.x;
+    if (k >= g.n_slots || !g.is_edge[k]) return;
+    const int u = g.slot_src[k];
+    if (!n.has_merged[u]) return;
+    if (g.slot_outpos[k] == 0) w.c11_base[u] = n.merged_cov[5 * (int64_t)u + 3];
+    if (e.act[k] != 1) {
+        w.var_ms[k] = -1.0;
+        return;
     }
-    n.merged_cov[5 * (int64_t)u + 3] = c11;  // the mutated array is what the stage saves
+    const double a = n.merged_state[3 * (int64_t)u + 0];
+    const double b = n.merged_state[3 * (int64_t)u + 1];
+    w.var_ms[k] = highland_var_ms(a, b, g.gnn + 4 * (int64_t)u, g.gnn + 4 * (int64_t)g.slot_dst[k], p.endcap_boundary);
+}
+
+// merged_cov[1,1] seen by out-edge number `upto` of sender u: the base plus the
+// var_ms of the active out-edges before it and itself, summed in successor order
+__device__ __forceinline__ double c11_prefix(const gtf_graph& g, const Ws& w, int u, int upto) {
+    double c11 = w.c11_base[u];
+    const int ob = g.out_ptr[u];
+    for (int i = ob; i <= ob + upto; i++) {
+        const double vm = w.var_ms[g.out_slot[i]];
+        if (vm != -1.0) c11 = c11 + vm;
+    }
+    return c11;
 }
 
 // ---------------------------------------------------------------------------
@@ -111,7 +122,11 @@ __global__ void __launch_bounds__(BLOCK) k_extrapolate(gtf_graph g, gtf_nodes n,
     uts.fresh[k] = 0;
     if (!g.is_edge[k]) return;
     const int u = g.slot_src[k];
-    if (!n.has_merged[u] || e.act[k] != 1) return;
+    if (!n.has_merged[u]) return;
+    const int opos = g.slot_outpos[k];
+    if (opos == g.out_ptr[u + 1] - g.out_ptr[u] - 1)  // the array the stage saves: base + every active var_ms
+        n.merged_cov[5 * (int64_t)u + 3] = c11_prefix(g, w, u, opos);
+    if (e.act[k] != 1) return;
     const int v = g.slot_dst[k];
     const double* ng = g.gnn + 4 * (int64_t)u;  // sender ("node" in the reference)
     const double* nb = g.gnn + 4 * (int64_t)v;  // receiver ("neighbour")
@@ -150,8 +165,8 @@ __global__ void __launch_bounds__(BLOCK) k_extrapolate(gtf_graph g, gtf_nodes n,
     const Mat3 F = {{{da_da, da_db, da_dc}, {db_da, db_db, db_dc}, {dc_da, dc_db, dc_dc}}};
 
     const double var_ms = w.var_ms[k];
-    const Cov5 mc = load_cov5(n.merged_cov, u);
-    const Mat3 C = {{{mc.c00, mc.c01, 0.0}, {mc.c10, w.c11_seen[k], 0.0}, {0.0, 0.0, mc.c22}}};  // :128
+    const double* mcp = n.merged_cov + 5 * (int64_t)u;   // c11 is rewritten by the last out-edge: not read here
+    const Mat3 C = {{{mcp[0], mcp[1], 0.0}, {mcp[2], c11_prefix(g, w, u, opos), 0.0}, {0.0, 0.0, mcp[4]}}};  // :128
     const double m[3] = {a, b, c};
     double xe[3];
     mv3(F, m, xe);                                                                 // :129
@@ -540,10 +555,10 @@ inline int grid(int n) { return (n + BLOCK - 1) / BLOCK; }
 
 int launch_extrap_edges(const gtf_graph* g, gtf_nodes* n, gtf_states* uts, gtf_edges* e, const gtf_params* p,
                         Ws w, hipStream_t st) {
-    if (g->n_nodes > 0)
-        hipLaunchKernelGGL(k_sender_scan, dim3(grid(g->n_nodes)), dim3(BLOCK), 0, st, *g, *n, *e, *p, w);
-    if (g->n_slots > 0)
+    if (g->n_slots > 0) {
+        hipLaunchKernelGGL(k_varms, dim3(grid(g->n_slots)), dim3(BLOCK), 0, st, *g, *n, *e, *p, w);
         hipLaunchKernelGGL(k_extrapolate, dim3(grid(g->n_slots)), dim3(BLOCK), 0, st, *g, *n, *uts, *e, *p, w);
+    }
     hipError_t err = hipGetLastError();
     return err == hipSuccess ? 0 : fail("extrapolate launch", err);
 }
@@ -646,8 +661,8 @@ int launch_seq(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* ut
 extern "C" {
 
 size_t gtf_workspace_bytes(int32_t n_nodes, int32_t n_slots) {
-    (void)n_nodes;
-    return 256 + 2 * align256(sizeof(double) * (size_t)(n_slots > 0 ? n_slots : 1));
+    return 256 + align256(sizeof(double) * (size_t)(n_slots > 0 ? n_slots : 1)) +
+           align256(sizeof(double) * (size_t)(n_nodes > 0 ? n_nodes : 1));
 }
 
 int gtf_clear_errors(void* ws, gtf_stream_t stream) {
@@ -724,8 +739,8 @@ int gtf_pass_ev(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* u
     hipStream_t st = (hipStream_t)stream;
     Ws w = carve(ws, g->n_nodes, g->n_slots);
     if (events) (void)hipEventRecord((hipEvent_t)events[0], st);
-    if (g->n_nodes > 0)
-        hipLaunchKernelGGL(k_sender_scan, dim3(grid(g->n_nodes)), dim3(BLOCK), 0, st, *g, *n, *e, *p, w);
+    if (g->n_slots > 0)
+        hipLaunchKernelGGL(k_varms, dim3(grid(g->n_slots)), dim3(BLOCK), 0, st, *g, *n, *e, *p, w);
     if (events) (void)hipEventRecord((hipEvent_t)events[1], st);
     if (g->n_slots > 0)
         hipLaunchKernelGGL(k_extrapolate, dim3(grid(g->n_slots)), dim3(BLOCK), 0, st, *g, *n, *uts, *e, *p, w);

@@ -18,6 +18,7 @@ F64 = ctypes.c_double
 class GtfGraph(ctypes.Structure):
     _fields_ = [("n_nodes", I32), ("n_slots", I32), ("n_edges", I32), ("pad_", I32),
                 ("slot_ptr", P), ("slot_src", P), ("slot_dst", P), ("out_ptr", P), ("out_slot", P),
+                ("slot_outpos", P),
                 ("is_edge", P), ("rev_edge", P), ("solo", P), ("gnn", P), ("xyzr", P), ("layer", P),
                 ("sched", P), ("n_g16", I32), ("n_g64", I32)]
 

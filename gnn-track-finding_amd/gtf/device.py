@@ -48,6 +48,11 @@ class DeviceGraph:
         up("out_ptr", g.out_ptr.astype(np.int32))
         up("out_slot", g.out_slot.astype(np.int32))
         up("slot_dst", g.slot_dst().astype(np.int32))
+        outpos = np.full(g.n_slots, -1, np.int32)
+        if g.n_edges:
+            owner = np.repeat(np.arange(g.n_nodes, dtype=np.int64), np.diff(g.out_ptr.astype(np.int64)))
+            outpos[g.out_slot] = (np.arange(g.n_edges) - g.out_ptr[owner]).astype(np.int32)
+        up("slot_outpos", outpos)
         sub = g.node["sub_id"].astype(np.int64)
         if g.n_nodes:
             sizes = np.bincount(sub - sub.min())
@@ -86,7 +91,7 @@ class DeviceGraph:
     def _build_structs(self):
         p = self.ptr
         self.cg = nat.GtfGraph(self.n_nodes, self.n_slots, self.n_edges, 0, p("slot_ptr"), p("slot_src"),
-                               p("slot_dst"), p("out_ptr"), p("out_slot"), p("is_edge"), p("rev_edge"), p("solo"),
+                               p("slot_dst"), p("out_ptr"), p("out_slot"), p("slot_outpos"), p("is_edge"), p("rev_edge"), p("solo"),
                                p("gnn"), p("xyzr"), p("layer"),
                                p("sched") if self.use_sched else ctypes.c_void_p(0), self.n_g16, self.n_g64)
         self.cn = nat.GtfNodes(*[p(f) for f in MUTABLE_NODE])

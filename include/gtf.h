@@ -46,6 +46,7 @@ typedef struct gtf_graph {
     const int32_t* slot_dst;  /* [S]   receiver node index */
     const int32_t* out_ptr;   /* [N+1] out-edge segment of each sender */
     const int32_t* out_slot;  /* [E]   slot of each out-edge, successor order */
+    const int32_t* slot_outpos; /* [S] position of the slot's edge in its sender's out-list (-1 = none) */
     const uint8_t* is_edge;   /* [S]   edge sender->receiver exists */
     const uint8_t* rev_edge;  /* [S]   edge receiver->sender exists */
     const uint8_t* solo;      /* [N]   node is alone in its subgraph */

@@ -276,19 +276,23 @@ __constant__ uint8_t c_pair_j[105] = {
 // covariance and inverse (computed once per state: np.linalg.inv of a state's
 // covariance is the same value every time the reference recomputes it), and the
 // per-neighbour tau geometry of the pairwise chi2
-struct Stage {
-    double a[16], b[16], c[16], tau[16];
-    double c00[16], c01[16], c10[16], c11[16], c22[16];
-    double i00[16], i01[16], i10[16], i11[16], i22[16];
-    double q[16], w[16], tg[16], sz2[16], sr2[16], prior[16];
+template <int CAP>
+struct StageT {
+    double a[CAP], b[CAP], c[CAP], tau[CAP];
+    double c00[CAP], c01[CAP], c10[CAP], c11[CAP], c22[CAP];
+    double i00[CAP], i01[CAP], i10[CAP], i11[CAP], i22[CAP];
+    double q[CAP], w[CAP], tg[CAP], sz2[CAP], sr2[CAP], prior[CAP];
 };
 
+template <typename Stage>
 __device__ __forceinline__ Cov5 stage_cov(const volatile Stage* s, int i) {
     return Cov5{s->c00[i], s->c01[i], s->c10[i], s->c11[i], s->c22[i]};
 }
+template <typename Stage>
 __device__ __forceinline__ Cov5 stage_inv(const volatile Stage* s, int i) {
     return Cov5{s->i00[i], s->i01[i], s->i10[i], s->i11[i], s->i22[i]};
 }
+template <typename Stage>
 __device__ __forceinline__ TauGeo stage_geo(const volatile Stage* s, int i) {
     TauGeo t;
     t.q = s->q[i]; t.w = s->w[i]; t.tau = s->tg[i]; t.sz2 = s->sz2[i]; t.sr2 = s->sr2[i];
@@ -300,7 +304,7 @@ __device__ __forceinline__ TauGeo stage_geo(const volatile Stage* s, int i) {
 // so the np.where tie order is the order of t. The parabolic and the joint merge
 // share their covariance (both merge the same aliased covariances), so one
 // (I1 + I2)^-1 serves both means.
-template <int G>
+template <int G, typename Stage>
 __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf_states& S, LaneDict& st,
                                           volatile Stage* stg, const double* xyzr_node, double chi2_thr,
                                           double kl_thr, const gtf_params& p, uint32_t* err) {
@@ -484,7 +488,7 @@ __device__ __forceinline__ void node_store(NodeCtx<G>& c, gtf_nodes& n, gtf_stat
     if (c.degree_set && c.grp.gl == 0) n.degree[c.v] = c.degree;
 }
 
-template <int G, int OP>
+template <int G, int OP, typename Stage>
 __device__ __forceinline__ void node_op(NodeCtx<G>& c, const gtf_graph& g, gtf_nodes& n, gtf_states& tse,
                                         gtf_states& uts, const gtf_params& p, const Ws& w, volatile double* sval,
                                         volatile Stage* stg, double chi2_thr, double kl_thr, bool has_tse,
@@ -520,6 +524,7 @@ __global__ void __launch_bounds__(BLOCK) k_node_seq(gtf_graph g, gtf_nodes n, gt
                                                     gtf_edges e, gtf_params p, Ws w, double chi2_thr, double kl_thr,
                                                     const int32_t* list, int count) {
     using Q = OpSeq<OPS...>;
+    using Stage = StageT<(G < 16 ? G : 16)>;
     __shared__ volatile double s_val[BLOCK];
     __shared__ volatile Stage s_stage[Q::cluster ? BLOCK / G : 1];
     NodeCtx<G> c;
@@ -527,7 +532,7 @@ __global__ void __launch_bounds__(BLOCK) k_node_seq(gtf_graph g, gtf_nodes n, gt
     volatile double* sval = s_val + (threadIdx.x & ~63);
     volatile Stage* stg = s_stage + (Q::cluster ? (int)threadIdx.x / G : 0);
     const bool has_tse = n.has_tse[c.v], has_uts = n.has_uts[c.v];
-    (node_op<G, OPS>(c, g, n, tse, uts, p, w, sval, stg, chi2_thr, kl_thr, has_tse, has_uts), ...);
+    (node_op<G, OPS, Stage>(c, g, n, tse, uts, p, w, sval, stg, chi2_thr, kl_thr, has_tse, has_uts), ...);
     node_store(c, n, tse, uts, e);
 }
 
@@ -537,6 +542,7 @@ __global__ void __launch_bounds__(BLOCK) k_node_group(gtf_graph g, gtf_nodes n, 
                                                       gtf_edges e, gtf_params p, Ws w, NodeOps ops,
                                                       double chi2_thr, double kl_thr, const int32_t* list,
                                                       int count) {
+    using Stage = StageT<(G < 16 ? G : 16)>;
     __shared__ volatile double s_val[BLOCK];
     __shared__ volatile Stage s_stage[BLOCK / G];
     NodeCtx<G> c;
@@ -547,7 +553,7 @@ __global__ void __launch_bounds__(BLOCK) k_node_group(gtf_graph g, gtf_nodes n, 
     for (int i = 0; i < ops.n; i++) {
         switch (ops.op[i]) {
 #define GTF_CASE(OPC) \
-    case OPC: node_op<G, OPC>(c, g, n, tse, uts, p, w, sval, stg, chi2_thr, kl_thr, has_tse, has_uts); break;
+    case OPC: node_op<G, OPC, Stage>(c, g, n, tse, uts, p, w, sval, stg, chi2_thr, kl_thr, has_tse, has_uts); break;
             GTF_CASE(OP_RANKS)
             GTF_CASE(OP_PRIORS_TSE)
             GTF_CASE(OP_PRIORS_UTS)

@@ -30,8 +30,9 @@ constexpr int MAX_CLUSTER = 15;  // clustering.py:207 (2 < d < 16)
 
 struct Ws {
     uint32_t* err;     // error word
-    double* var_ms;    // [S] var_ms of the extrapolation along this slot's edge (-1 = edge was inactive)
+    double* var_ms;    // [E] var_ms of each out-edge, in out-list order (-1 = edge was inactive)
     double* c11_base;  // [N] merged_cov[1,1] before message passing
+    double* c11_seen;  // [E] merged_cov[1,1] seen by each out-edge's extrapolation (out-list order)
 };
 
 __host__ inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
@@ -44,7 +45,8 @@ __host__ inline Ws carve(void* base, int32_t n_nodes, int32_t n_slots) {
     w.var_ms = (double*)p;
     p += align256(sizeof(double) * (size_t)(n_slots > 0 ? n_slots : 1));
     w.c11_base = (double*)p;
-    (void)n_nodes;
+    p += align256(sizeof(double) * (size_t)(n_nodes > 0 ? n_nodes : 1));
+    w.c11_seen = (double*)p;
     return w;
 }
 
@@ -90,26 +92,35 @@ __global__ void __launch_bounds__(BLOCK) k_varms(gtf_graph g, gtf_nodes n, gtf_e
     if (k >= g.n_slots || !g.is_edge[k]) return;
     const int u = g.slot_src[k];
     if (!n.has_merged[u]) return;
-    if (g.slot_outpos[k] == 0) w.c11_base[u] = n.merged_cov[5 * (int64_t)u + 3];
+    if (g.slot_outpos[k] == 0) w.c11_base[u] = n.merged_cov[5 * (int64_t)u + 3];  // read before k_prefix writes
+    const int i = g.out_ptr[u] + g.slot_outpos[k];
     if (e.act[k] != 1) {
-        w.var_ms[k] = -1.0;
+        w.var_ms[i] = -1.0;
         return;
     }
     const double a = n.merged_state[3 * (int64_t)u + 0];
     const double b = n.merged_state[3 * (int64_t)u + 1];
-    w.var_ms[k] = highland_var_ms(a, b, g.gnn + 4 * (int64_t)u, g.gnn + 4 * (int64_t)g.slot_dst[k], p.endcap_boundary);
+    w.var_ms[i] = highland_var_ms(a, b, g.gnn + 4 * (int64_t)u, g.gnn + 4 * (int64_t)g.slot_dst[k], p.endcap_boundary);
 }
 
-// merged_cov[1,1] seen by out-edge number `upto` of sender u: the base plus the
-// var_ms of the active out-edges before it and itself, summed in successor order
-__device__ __forceinline__ double c11_prefix(const gtf_graph& g, const Ws& w, int u, int upto) {
+// ---------------------------------------------------------------------------
+// k_prefix: one thread per merged sender: the running merged_cov[1,1] each of its
+// active out-edges sees, summed sequentially in successor order (the in-place
+// "merged_cov[1, 1] += var_ms" of extrapolate_merged_states.py:127-128), and the
+// final value the stage saves. Only additions over contiguous out-list arrays.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(BLOCK) k_prefix(gtf_graph g, gtf_nodes n, Ws w) {
+    const int u = blockIdx.x * BLOCK + threadIdx.x;
+    if (u >= g.n_nodes || !n.has_merged[u]) return;
+    const int ob = g.out_ptr[u], oe = g.out_ptr[u + 1];
+    if (ob == oe) return;
     double c11 = w.c11_base[u];
-    const int ob = g.out_ptr[u];
-    for (int i = ob; i <= ob + upto; i++) {
-        const double vm = w.var_ms[g.out_slot[i]];
+    for (int i = ob; i < oe; i++) {
+        const double vm = w.var_ms[i];
         if (vm != -1.0) c11 = c11 + vm;
+        w.c11_seen[i] = c11;
     }
-    return c11;
+    n.merged_cov[5 * (int64_t)u + 3] = c11;
 }
 
 // ---------------------------------------------------------------------------
@@ -123,10 +134,8 @@ __global__ void __launch_bounds__(BLOCK) k_extrapolate(gtf_graph g, gtf_nodes n,
     if (!g.is_edge[k]) return;
     const int u = g.slot_src[k];
     if (!n.has_merged[u]) return;
-    const int opos = g.slot_outpos[k];
-    if (opos == g.out_ptr[u + 1] - g.out_ptr[u] - 1)  // the array the stage saves: base + every active var_ms
-        n.merged_cov[5 * (int64_t)u + 3] = c11_prefix(g, w, u, opos);
     if (e.act[k] != 1) return;
+    const int oi = g.out_ptr[u] + g.slot_outpos[k];
     const int v = g.slot_dst[k];
     const double* ng = g.gnn + 4 * (int64_t)u;  // sender ("node" in the reference)
     const double* nb = g.gnn + 4 * (int64_t)v;  // receiver ("neighbour")
@@ -164,9 +173,9 @@ __global__ void __launch_bounds__(BLOCK) k_extrapolate(gtf_graph g, gtf_nodes n,
     const double dc_dc = (ds_dc * bracket) + cp;
     const Mat3 F = {{{da_da, da_db, da_dc}, {db_da, db_db, db_dc}, {dc_da, dc_db, dc_dc}}};
 
-    const double var_ms = w.var_ms[k];
-    const double* mcp = n.merged_cov + 5 * (int64_t)u;   // c11 is rewritten by the last out-edge: not read here
-    const Mat3 C = {{{mcp[0], mcp[1], 0.0}, {mcp[2], c11_prefix(g, w, u, opos), 0.0}, {0.0, 0.0, mcp[4]}}};  // :128
+    const double var_ms = w.var_ms[oi];
+    const double* mcp = n.merged_cov + 5 * (int64_t)u;
+    const Mat3 C = {{{mcp[0], mcp[1], 0.0}, {mcp[2], w.c11_seen[oi], 0.0}, {0.0, 0.0, mcp[4]}}};  // :128
     const double m[3] = {a, b, c};
     double xe[3];
     mv3(F, m, xe);                                                                 // :129
@@ -557,6 +566,7 @@ int launch_extrap_edges(const gtf_graph* g, gtf_nodes* n, gtf_states* uts, gtf_e
                         Ws w, hipStream_t st) {
     if (g->n_slots > 0) {
         hipLaunchKernelGGL(k_varms, dim3(grid(g->n_slots)), dim3(BLOCK), 0, st, *g, *n, *e, *p, w);
+        hipLaunchKernelGGL(k_prefix, dim3(grid(g->n_nodes)), dim3(BLOCK), 0, st, *g, *n, w);
         hipLaunchKernelGGL(k_extrapolate, dim3(grid(g->n_slots)), dim3(BLOCK), 0, st, *g, *n, *uts, *e, *p, w);
     }
     hipError_t err = hipGetLastError();
@@ -579,10 +589,11 @@ void finish_ops(NodeOps& ops, const gtf_states* tse, const gtf_states* uts) {
 void launch_serial_rest(const gtf_graph* g, gtf_nodes* n, const gtf_states& T, const gtf_states& U, gtf_edges* e,
                         const gtf_params* p, Ws w, const NodeOps& ops, double chi2, double kl, hipStream_t st) {
     if (g->sched) {
-        const int nbig = g->n_nodes - g->n_g16 - g->n_g64;
+        const int ng = g->n_g8 + g->n_g16 + g->n_g32 + g->n_g64;
+        const int nbig = g->n_nodes - ng;
         if (nbig > 0)
             hipLaunchKernelGGL(k_node, dim3(grid(nbig)), dim3(BLOCK), 0, st, *g, *n, T, U, *e, *p, w, ops, chi2, kl,
-                               g->sched + g->n_g16 + g->n_g64, nbig);
+                               g->sched + ng, nbig);
     } else if (g->n_nodes > 0) {
         hipLaunchKernelGGL(k_node, dim3(grid(g->n_nodes)), dim3(BLOCK), 0, st, *g, *n, T, U, *e, *p, w, ops, chi2, kl,
                            (const int32_t*)nullptr, g->n_nodes);
@@ -609,12 +620,22 @@ int launch_ops(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* ut
     const gtf_states T = tse ? *tse : dummy, U = uts ? *uts : dummy;
     if (g->n_nodes > 0 && ops.n > 0) {
         if (g->sched) {
+            const int32_t* l = g->sched;
+            if (g->n_g8 > 0)
+                hipLaunchKernelGGL(k_node_group<8>, dim3((g->n_g8 + BLOCK / 8 - 1) / (BLOCK / 8)), dim3(BLOCK), 0, st,
+                                   *g, *n, T, U, *e, *p, w, ops, chi2, kl, l, g->n_g8);
+            l += g->n_g8;
             if (g->n_g16 > 0)
                 hipLaunchKernelGGL(k_node_group<16>, dim3((g->n_g16 + BLOCK / 16 - 1) / (BLOCK / 16)), dim3(BLOCK), 0,
-                                   st, *g, *n, T, U, *e, *p, w, ops, chi2, kl, g->sched, g->n_g16);
+                                   st, *g, *n, T, U, *e, *p, w, ops, chi2, kl, l, g->n_g16);
+            l += g->n_g16;
+            if (g->n_g32 > 0)
+                hipLaunchKernelGGL(k_node_group<32>, dim3((g->n_g32 + BLOCK / 32 - 1) / (BLOCK / 32)), dim3(BLOCK), 0,
+                                   st, *g, *n, T, U, *e, *p, w, ops, chi2, kl, l, g->n_g32);
+            l += g->n_g32;
             if (g->n_g64 > 0)
                 hipLaunchKernelGGL(k_node_group<64>, dim3((g->n_g64 + BLOCK / 64 - 1) / (BLOCK / 64)), dim3(BLOCK), 0,
-                                   st, *g, *n, T, U, *e, *p, w, ops, chi2, kl, g->sched + g->n_g16, g->n_g64);
+                                   st, *g, *n, T, U, *e, *p, w, ops, chi2, kl, l, g->n_g64);
         }
         launch_serial_rest(g, n, T, U, e, p, w, ops, chi2, kl, st);
     }
@@ -636,12 +657,22 @@ int launch_seq(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* ut
     const gtf_states T = tse ? *tse : dummy, U = uts ? *uts : dummy;
     if (g->n_nodes > 0) {
         if (g->sched) {
+            const int32_t* l = g->sched;
+            if (g->n_g8 > 0)
+                hipLaunchKernelGGL((k_node_seq<8, OPS...>), dim3((g->n_g8 + BLOCK / 8 - 1) / (BLOCK / 8)), dim3(BLOCK),
+                                   0, st, *g, *n, T, U, *e, *p, w, chi2, kl, l, g->n_g8);
+            l += g->n_g8;
             if (g->n_g16 > 0)
                 hipLaunchKernelGGL((k_node_seq<16, OPS...>), dim3((g->n_g16 + BLOCK / 16 - 1) / (BLOCK / 16)),
-                                   dim3(BLOCK), 0, st, *g, *n, T, U, *e, *p, w, chi2, kl, g->sched, g->n_g16);
+                                   dim3(BLOCK), 0, st, *g, *n, T, U, *e, *p, w, chi2, kl, l, g->n_g16);
+            l += g->n_g16;
+            if (g->n_g32 > 0)
+                hipLaunchKernelGGL((k_node_seq<32, OPS...>), dim3((g->n_g32 + BLOCK / 32 - 1) / (BLOCK / 32)),
+                                   dim3(BLOCK), 0, st, *g, *n, T, U, *e, *p, w, chi2, kl, l, g->n_g32);
+            l += g->n_g32;
             if (g->n_g64 > 0)
                 hipLaunchKernelGGL((k_node_seq<64, OPS...>), dim3((g->n_g64 + BLOCK / 64 - 1) / (BLOCK / 64)),
-                                   dim3(BLOCK), 0, st, *g, *n, T, U, *e, *p, w, chi2, kl, g->sched + g->n_g16, g->n_g64);
+                                   dim3(BLOCK), 0, st, *g, *n, T, U, *e, *p, w, chi2, kl, l, g->n_g64);
         }
         launch_serial_rest(g, n, T, U, e, p, w, ops, chi2, kl, st);
     }
@@ -661,7 +692,7 @@ int launch_seq(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* ut
 extern "C" {
 
 size_t gtf_workspace_bytes(int32_t n_nodes, int32_t n_slots) {
-    return 256 + align256(sizeof(double) * (size_t)(n_slots > 0 ? n_slots : 1)) +
+    return 256 + 2 * align256(sizeof(double) * (size_t)(n_slots > 0 ? n_slots : 1)) +
            align256(sizeof(double) * (size_t)(n_nodes > 0 ? n_nodes : 1));
 }
 
@@ -739,8 +770,10 @@ int gtf_pass_ev(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* u
     hipStream_t st = (hipStream_t)stream;
     Ws w = carve(ws, g->n_nodes, g->n_slots);
     if (events) (void)hipEventRecord((hipEvent_t)events[0], st);
-    if (g->n_slots > 0)
+    if (g->n_slots > 0) {
         hipLaunchKernelGGL(k_varms, dim3(grid(g->n_slots)), dim3(BLOCK), 0, st, *g, *n, *e, *p, w);
+        hipLaunchKernelGGL(k_prefix, dim3(grid(g->n_nodes)), dim3(BLOCK), 0, st, *g, *n, w);
+    }
     if (events) (void)hipEventRecord((hipEvent_t)events[1], st);
     if (g->n_slots > 0)
         hipLaunchKernelGGL(k_extrapolate, dim3(grid(g->n_slots)), dim3(BLOCK), 0, st, *g, *n, *uts, *e, *p, w);

@@ -60,13 +60,14 @@ class DeviceGraph:
         else:
             solo = np.zeros(0, np.uint8)
         up("solo", solo)
-        # degree-bucketed node schedule for the node-local kernels
+        # slot-count-bucketed node schedule for the node-local kernels (G lanes per node)
         deg = np.diff(g.slot_ptr.astype(np.int64))
         idx = np.arange(g.n_nodes, dtype=np.int32)
-        b16, b64 = idx[deg <= 16], idx[(deg > 16) & (deg <= 64)]
-        big = idx[deg > 64]
-        up("sched", np.concatenate([b16, b64, big]).astype(np.int32))
-        self.n_g16, self.n_g64 = (int(b16.size), int(b64.size)) if schedule else (0, 0)
+        edges = [(0, 8), (9, 16), (17, 32), (33, 64)]
+        buckets = [idx[(deg >= lo) & (deg <= hi)] for lo, hi in edges]
+        rest = idx[deg > 64]
+        up("sched", np.concatenate(buckets + [rest]).astype(np.int32))
+        self.n_g = [int(b.size) for b in buckets] if schedule else [0, 0, 0, 0]
         self.use_sched = schedule
         for f in ("gnn", "xyzr", "layer") + MUTABLE_NODE:
             up(f, g.node[f])
@@ -93,7 +94,7 @@ class DeviceGraph:
         self.cg = nat.GtfGraph(self.n_nodes, self.n_slots, self.n_edges, 0, p("slot_ptr"), p("slot_src"),
                                p("slot_dst"), p("out_ptr"), p("out_slot"), p("slot_outpos"), p("is_edge"), p("rev_edge"), p("solo"),
                                p("gnn"), p("xyzr"), p("layer"),
-                               p("sched") if self.use_sched else ctypes.c_void_p(0), self.n_g16, self.n_g64)
+                               p("sched") if self.use_sched else ctypes.c_void_p(0), *self.n_g)
         self.cn = nat.GtfNodes(*[p(f) for f in MUTABLE_NODE])
         self.cuts = nat.GtfStates(p("uts_rank"), p("uts_sv"), p("uts_tau"), p("uts_cov"), p("uts_xyzr"),
                                   p("uts_lik"), p("uts_mw"), p("uts_prior"), p("uts_lr"), p("uts_side"),

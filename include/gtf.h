@@ -54,10 +54,13 @@ typedef struct gtf_graph {
     const double*  xyzr;      /* [N*4] node attribute 'xyzr' */
     const double*  layer;     /* [N]   in_volume_layer_id */
     /* optional node schedule for the node-local stages (NULL = one thread per node):
-     * node indices with <= 16 slots first (n_g16 of them), then <= 64 slots (n_g64),
-     * then the rest. Built once per graph by the host (gtf/device.py). */
+     * node indices bucketed by slot count -- n_g8 nodes with <= 8 slots, then n_g16 with
+     * 9..16, n_g32 with 17..32, n_g64 with 33..64 (a group of that many lanes per node),
+     * then the rest (one thread per node). Built once per graph (gtf/device.py). */
     const int32_t* sched;     /* [N] */
+    int32_t n_g8;
     int32_t n_g16;
+    int32_t n_g32;
     int32_t n_g64;
 } gtf_graph;
 

@@ -39,7 +39,7 @@ def main():
     g = synth.workload(wl)
     d = DeviceGraph(g, schedule=sched)
     snap0 = d.snapshot()
-    out = {"workload": wl, "edges": g.n_edges, "nodes": g.n_nodes, "n_g16": d.n_g16, "n_g64": d.n_g64}
+    out = {"workload": wl, "edges": g.n_edges, "nodes": g.n_nodes, "n_g": d.n_g}
     out["full_pass"] = timeit(d, snap0, lambda: d.full_pass(p))
     out["message_passing"] = timeit(d, snap0, lambda: d.message_passing(p))
     d.restore(snap0)

@@ -435,8 +435,7 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
 template <int G>
 __device__ __forceinline__ bool node_load(NodeCtx<G>& c, const gtf_graph& g, const gtf_nodes& n,
                                           const gtf_states& tse, const gtf_states& uts, const gtf_edges& e,
-                                          const int32_t* list, int count, bool uses_tse, bool uses_uts) {
-    const int gi = (blockIdx.x * BLOCK + (int)threadIdx.x) / G;
+                                          const int32_t* list, int count, int gi, bool uses_tse, bool uses_uts) {
     if (gi >= count) return false;  // group-uniform
     c.v = list[gi];
     c.lo = g.slot_ptr[c.v];
@@ -518,22 +517,65 @@ struct OpSeq {
     static constexpr bool cluster = ((OPS == OP_CLUSTER_TSE || OPS == OP_CLUSTER_UTS) || ...);
 };
 
-// compile-time op sequence: dead ops are compiled out, registers sized for the sequence
+// compile-time op sequence for one group size: dead ops are compiled out.
+// `bid` is the block index inside this bucket's range of the launch.
 template <int G, int... OPS>
-__global__ void __launch_bounds__(BLOCK) k_node_seq(gtf_graph g, gtf_nodes n, gtf_states tse, gtf_states uts,
-                                                    gtf_edges e, gtf_params p, Ws w, double chi2_thr, double kl_thr,
-                                                    const int32_t* list, int count) {
+__device__ __forceinline__ void node_seq_body(const gtf_graph& g, gtf_nodes& n, gtf_states& tse, gtf_states& uts,
+                                              gtf_edges& e, const gtf_params& p, const Ws& w, double chi2_thr,
+                                              double kl_thr, const int32_t* list, int count, int bid,
+                                              char* smem) {
     using Q = OpSeq<OPS...>;
     using Stage = StageT<(G < 16 ? G : 16)>;
-    __shared__ volatile double s_val[BLOCK];
-    __shared__ volatile Stage s_stage[Q::cluster ? BLOCK / G : 1];
     NodeCtx<G> c;
-    if (!node_load(c, g, n, tse, uts, e, list, count, Q::uses_tse, Q::uses_uts)) return;
-    volatile double* sval = s_val + (threadIdx.x & ~63);
-    volatile Stage* stg = s_stage + (Q::cluster ? (int)threadIdx.x / G : 0);
+    const int gi = (bid * BLOCK + (int)threadIdx.x) / G;
+    if (!node_load(c, g, n, tse, uts, e, list, count, gi, Q::uses_tse, Q::uses_uts)) return;
+    volatile double* sval = (volatile double*)smem + (threadIdx.x & ~63);
+    volatile Stage* stg = (volatile Stage*)(smem + BLOCK * sizeof(double)) + (Q::cluster ? (int)threadIdx.x / G : 0);
     const bool has_tse = n.has_tse[c.v], has_uts = n.has_uts[c.v];
     (node_op<G, OPS, Stage>(c, g, n, tse, uts, p, w, sval, stg, chi2_thr, kl_thr, has_tse, has_uts), ...);
     node_store(c, n, tse, uts, e);
+}
+
+struct Buckets {
+    const int32_t* list[4];  // node lists for G = 64, 32, 16, 8 (slowest first)
+    int32_t count[4];
+    int32_t blocks[4];
+};
+
+constexpr size_t stage_bytes(int G) { return (size_t)(BLOCK / G) * 20 * (G < 16 ? G : 16) * sizeof(double); }
+constexpr size_t node_smem_bytes() {
+    size_t m = stage_bytes(8);
+    m = stage_bytes(16) > m ? stage_bytes(16) : m;
+    m = stage_bytes(32) > m ? stage_bytes(32) : m;
+    m = stage_bytes(64) > m ? stage_bytes(64) : m;
+    return BLOCK * sizeof(double) + m;
+}
+
+// one launch over every bucket: blocks of the long-running buckets (many slots per node)
+// are dealt first so they overlap the bulk of small nodes instead of trailing it
+template <int... OPS>
+__global__ void __launch_bounds__(BLOCK) k_node_multi(gtf_graph g, gtf_nodes n, gtf_states tse, gtf_states uts,
+                                                      gtf_edges e, gtf_params p, Ws w, double chi2_thr,
+                                                      double kl_thr, Buckets bk) {
+    using Q = OpSeq<OPS...>;
+    __shared__ __attribute__((aligned(16))) char smem[Q::cluster ? node_smem_bytes() : BLOCK * sizeof(double)];
+    int b = blockIdx.x;
+    if (b < bk.blocks[0]) {
+        node_seq_body<64, OPS...>(g, n, tse, uts, e, p, w, chi2_thr, kl_thr, bk.list[0], bk.count[0], b, smem);
+        return;
+    }
+    b -= bk.blocks[0];
+    if (b < bk.blocks[1]) {
+        node_seq_body<32, OPS...>(g, n, tse, uts, e, p, w, chi2_thr, kl_thr, bk.list[1], bk.count[1], b, smem);
+        return;
+    }
+    b -= bk.blocks[1];
+    if (b < bk.blocks[2]) {
+        node_seq_body<16, OPS...>(g, n, tse, uts, e, p, w, chi2_thr, kl_thr, bk.list[2], bk.count[2], b, smem);
+        return;
+    }
+    b -= bk.blocks[2];
+    node_seq_body<8, OPS...>(g, n, tse, uts, e, p, w, chi2_thr, kl_thr, bk.list[3], bk.count[3], b, smem);
 }
 
 // run-time op sequence (gtf_node_ops): any order of any ops
@@ -546,7 +588,8 @@ __global__ void __launch_bounds__(BLOCK) k_node_group(gtf_graph g, gtf_nodes n, 
     __shared__ volatile double s_val[BLOCK];
     __shared__ volatile Stage s_stage[BLOCK / G];
     NodeCtx<G> c;
-    if (!node_load(c, g, n, tse, uts, e, list, count, ops.uses_tse, ops.uses_uts)) return;
+    const int gi = (blockIdx.x * BLOCK + (int)threadIdx.x) / G;
+    if (!node_load(c, g, n, tse, uts, e, list, count, gi, ops.uses_tse, ops.uses_uts)) return;
     volatile double* sval = s_val + (threadIdx.x & ~63);
     volatile Stage* stg = s_stage + (int)threadIdx.x / G;
     const bool has_tse = n.has_tse[c.v], has_uts = n.has_uts[c.v];

@@ -71,7 +71,8 @@ __device__ __forceinline__ double highland_var_ms(double a, double b, const doub
     double hyp = sqrt(dr * dr + dz * dz);
     double sin_t = fabs(dr) / hyp;
     double q = (2.0 * a * nb[0]) + b;
-    double kappa = (2.0 * a) / pow(1.0 + q * q, 1.5);
+    const double t15 = 1.0 + q * q;
+    double kappa = (2.0 * a) / (t15 * sqrt(t15));  // (1 + q^2)**1.5
     double t = ((13.6 * 1e-3 * sqrt(0.02)) * kappa) / 0.3;
     double var_ms = sin_t * (t * t);
     if (fabs(ng[2]) >= boundary) {
@@ -143,25 +144,30 @@ __global__ void __launch_bounds__(BLOCK) k_extrapolate(gtf_graph g, gtf_nodes n,
     const double nbx = nb[0], nby = nb[1], nbz = nb[2];
     const double a = n.merged_state[3 * u + 0], b = n.merged_state[3 * u + 1], c = n.merged_state[3 * u + 2];
 
-    const double ang = atan2(node_y, node_x);                                    // :41
-    const double x_A = (nbx - node_x) * cos(ang) + (nby - node_y) * sin(ang);     // :52
-    const double phi = atan2((node_x * nby) - (node_y * nbx), (node_x * nbx) + (node_y * nby));  // :59
-    const double sp = sin(phi), cp = cos(phi);
+    // cos/sin of atan2(y, x) as x/h, y/h (h = |(x, y)|): the same angles as the
+    // reference's atan2 -> cos/sin round trips, to a couple of ulps, without fp64 libm
+    const double rA = sqrt(node_x * node_x + node_y * node_y);
+    const double ca = rA > 0.0 ? node_x / rA : 1.0, sa = rA > 0.0 ? node_y / rA : 0.0;       // :41
+    const double x_A = (nbx - node_x) * ca + (nby - node_y) * sa;                              // :52
+    const double py = (node_x * nby) - (node_y * nbx), px = (node_x * nbx) + (node_y * nby);  // :59
+    const double hp = sqrt(px * px + py * py);
+    const double sp = hp > 0.0 ? py / hp : 0.0, cp = hp > 0.0 ? px / hp : 1.0;
     const double x_prime = x_A + (c * sp);                                        // :63
     const double Vx = cp + (b * sp);
     const double Ax = a * sp;
-    const double s_star = (-x_prime * ((2.0 * (Vx * Vx)) + (Ax * x_prime))) / (2.0 * pow(Vx, 3.0));  // :68
+    const double s_star = (-x_prime * ((2.0 * (Vx * Vx)) + (Ax * x_prime))) / (2.0 * (Vx * Vx * Vx));  // :68
 
     double numer = x_A + c * sp;                                                  // :82
     double denom = cp + b * sp;
     const double d2 = denom * denom;
-    const double ds_da = -(sp * (numer * numer)) / pow(denom, 3.0);
+    const double ds_da = -(sp * (numer * numer)) / (d2 * denom);
     const double ds_db = ((sp * numer) * (1.0 + ((3.0 * a * sp * numer) / d2))) / d2;
     const double ds_dc = (-sp * (1.0 + ((2.0 * a * sp * numer) / d2))) / denom;
     denom = cp + ((2.0 * a + b) * sp);                                             // :89
-    const double da_da = (1.0 / pow(denom, 3.0)) * (1.0 - ((6.0 * a * sp) * (s_star + a * ds_da) / denom));
-    const double da_db = (-3.0 * a * sp * ((2.0 * a * ds_db) + 1.0)) / pow(denom, 4.0);
-    const double da_dc = (-6.0 * sp * ds_dc * (a * a)) / pow(denom, 4.0);
+    const double e2 = denom * denom;
+    const double da_da = (1.0 / (e2 * denom)) * (1.0 - ((6.0 * a * sp) * (s_star + a * ds_da) / denom));
+    const double da_db = (-3.0 * a * sp * ((2.0 * a * ds_db) + 1.0)) / (e2 * e2);
+    const double da_dc = (-6.0 * sp * ds_dc * (a * a)) / (e2 * e2);
     denom = cp + ((2.0 * a * s_star + b) * sp);                                    // :95
     double bracket = cp - ((sp * (-sp + ((2.0 * a * s_star + b) * cp))) / denom);
     const double db_da = (2.0 * (s_star + a * ds_da) * bracket) / denom;
@@ -189,7 +195,7 @@ __global__ void __launch_bounds__(BLOCK) k_extrapolate(gtf_graph g, gtf_nodes n,
         e.act[k] = 0;                                                              // :393
         return;
     }
-    const double lik = pow((2.0 * M_PI) * fabs(S), -0.5) * exp(-0.5 * chi2);      // :302-304
+    const double lik = (1.0 / sqrt((2.0 * M_PI) * fabs(S))) * exp(-0.5 * chi2);  // :302-304
 
     // filterpy 1.4.5 predict() + update(0)  (:307-323): F applied a second time
     double xp[3];
@@ -657,22 +663,21 @@ int launch_seq(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* ut
     const gtf_states T = tse ? *tse : dummy, U = uts ? *uts : dummy;
     if (g->n_nodes > 0) {
         if (g->sched) {
-            const int32_t* l = g->sched;
-            if (g->n_g8 > 0)
-                hipLaunchKernelGGL((k_node_seq<8, OPS...>), dim3((g->n_g8 + BLOCK / 8 - 1) / (BLOCK / 8)), dim3(BLOCK),
-                                   0, st, *g, *n, T, U, *e, *p, w, chi2, kl, l, g->n_g8);
-            l += g->n_g8;
-            if (g->n_g16 > 0)
-                hipLaunchKernelGGL((k_node_seq<16, OPS...>), dim3((g->n_g16 + BLOCK / 16 - 1) / (BLOCK / 16)),
-                                   dim3(BLOCK), 0, st, *g, *n, T, U, *e, *p, w, chi2, kl, l, g->n_g16);
-            l += g->n_g16;
-            if (g->n_g32 > 0)
-                hipLaunchKernelGGL((k_node_seq<32, OPS...>), dim3((g->n_g32 + BLOCK / 32 - 1) / (BLOCK / 32)),
-                                   dim3(BLOCK), 0, st, *g, *n, T, U, *e, *p, w, chi2, kl, l, g->n_g32);
-            l += g->n_g32;
-            if (g->n_g64 > 0)
-                hipLaunchKernelGGL((k_node_seq<64, OPS...>), dim3((g->n_g64 + BLOCK / 64 - 1) / (BLOCK / 64)),
-                                   dim3(BLOCK), 0, st, *g, *n, T, U, *e, *p, w, chi2, kl, l, g->n_g64);
+            Buckets bk;
+            const int cnt[4] = {g->n_g64, g->n_g32, g->n_g16, g->n_g8};
+            const int gs[4] = {64, 32, 16, 8};
+            const int32_t* starts[4] = {g->sched + g->n_g8 + g->n_g16 + g->n_g32, g->sched + g->n_g8 + g->n_g16,
+                                        g->sched + g->n_g8, g->sched};
+            int total = 0;
+            for (int q = 0; q < 4; q++) {
+                bk.list[q] = starts[q];
+                bk.count[q] = cnt[q];
+                bk.blocks[q] = (cnt[q] + BLOCK / gs[q] - 1) / (BLOCK / gs[q]);
+                total += bk.blocks[q];
+            }
+            if (total > 0)
+                hipLaunchKernelGGL((k_node_multi<OPS...>), dim3(total), dim3(BLOCK), 0, st, *g, *n, T, U, *e, *p, w,
+                                   chi2, kl, bk);
         }
         launch_serial_rest(g, n, T, U, e, p, w, ops, chi2, kl, st);
     }

@@ -224,5 +224,6 @@ class DeviceGraph:
         return {k: self.t[k].clone() for k in names}
 
     def restore(self, snap):
-        for k, v in snap.items():
-            self.t[k].copy_(v, non_blocking=True)
+        """copy a snapshot back (one multi-tensor copy launch)"""
+        keys = list(snap)
+        self.torch._foreach_copy_([self.t[k] for k in keys], [snap[k] for k in keys])

@@ -113,12 +113,12 @@ def main():
     scan = np.mean([evs[i][0].elapsed_time(evs[i][1]) for i in range(K)])
     extr = np.mean([evs[i][1].elapsed_time(evs[i][2]) for i in range(K)])
     node = np.mean([evs[i][2].elapsed_time(evs[i][3]) for i in range(K)])
-    kernels = {"k_varms": scan, "k_extrapolate": extr, "k_node_seq": node}
+    kernels = {"k_sender": scan, "k_extrapolate": extr, "k_node_seq": node}
     # roofline for the dominant kernel (algorithmic bytes, gtf/roofline.py)
     if node >= scan + extr:
         name, ms, nbytes = "k_node_seq (node-local stages)", node, rf.node_bytes(g.n_edges, g.n_nodes)
     else:
-        name, ms, nbytes = "k_varms+k_extrapolate", scan + extr, rf.extrap_bytes(g.n_edges, g.n_nodes)
+        name, ms, nbytes = "k_sender+k_extrapolate", scan + extr, rf.extrap_bytes(g.n_edges, g.n_nodes)
     achieved = nbytes / (ms * 1e-3) / 1e9
 
     cpu = None

@@ -2,11 +2,10 @@
 // gfx950 (MI355X), behind the C-ABI of include/gtf.h.
 //
 // Work decomposition (DESIGN.md "Kernels"):
-//   k_varms           1 thread / slot: Highland var_ms of every active out-edge of a
-//                     merged sender (extrapolate_merged_states.py:114-124).
-//   (k_extrapolate then forms the running merged_cov[1,1] += var_ms each extrapolation
-//                     sees -- the in-place mutation of :127-128 -- as the sequential
-//                     prefix over the sender's out-edges up to itself, in successor order.)
+//   k_sender         8 lanes / sender node over its out-edges (successor order): Highland
+//                     var_ms per edge and the running merged_cov[1,1] += var_ms each
+//                     extrapolation sees -- the in-place mutation of
+//                     extrapolate_merged_states.py:127-128 -- as a sequential scan.
 //   k_extrapolate     1 thread / slot (receiver-major, coalesced writes of the new
 //                     updated_track_states entry): parabolic extrapolation, chi2 gate,
 //                     Kalman predict + update (extrapolate_merged_states.py:26-402).
@@ -83,45 +82,42 @@ __device__ __forceinline__ double highland_var_ms(double a, double b, const doub
 }
 
 // ---------------------------------------------------------------------------
-// k_varms: one thread per slot. Records, for every out-edge of a sender with a
-// merged state, the Highland var_ms of its extrapolation (or -1 when the edge was
-// inactive before message passing, so it does not take part in the in-place sum of
-// extrapolate_merged_states.py:127-128), and the sender's merged_cov[1,1] before it.
+// k_sender: one 8-lane group per sender node, lanes over its out-edges in
+// successor order (chunks of 8). Each lane computes the Highland var_ms of its
+// out-edge (extrapolate_merged_states.py:114-124); then every lane forms the
+// running "merged_cov[1, 1] += var_ms" its extrapolation sees (:127-128) as the
+// sequential sum over the lanes before it (shuffles, the reference's addition
+// order), and the last value is the array the stage saves. Inactive out-edges do
+// not take part (:431). Out-list arrays are contiguous per sender: coalesced.
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(BLOCK) k_varms(gtf_graph g, gtf_nodes n, gtf_edges e, gtf_params p, Ws w) {
-    const int k = blockIdx.x * BLOCK + threadIdx.x;
-    if (k >= g.n_slots || !g.is_edge[k]) return;
-    const int u = g.slot_src[k];
-    if (!n.has_merged[u]) return;
-    if (g.slot_outpos[k] == 0) w.c11_base[u] = n.merged_cov[5 * (int64_t)u + 3];  // read before k_prefix writes
-    const int i = g.out_ptr[u] + g.slot_outpos[k];
-    if (e.act[k] != 1) {
-        w.var_ms[i] = -1.0;
-        return;
-    }
-    const double a = n.merged_state[3 * (int64_t)u + 0];
-    const double b = n.merged_state[3 * (int64_t)u + 1];
-    w.var_ms[i] = highland_var_ms(a, b, g.gnn + 4 * (int64_t)u, g.gnn + 4 * (int64_t)g.slot_dst[k], p.endcap_boundary);
-}
-
-// ---------------------------------------------------------------------------
-// k_prefix: one thread per merged sender: the running merged_cov[1,1] each of its
-// active out-edges sees, summed sequentially in successor order (the in-place
-// "merged_cov[1, 1] += var_ms" of extrapolate_merged_states.py:127-128), and the
-// final value the stage saves. Only additions over contiguous out-list arrays.
-// ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(BLOCK) k_prefix(gtf_graph g, gtf_nodes n, Ws w) {
-    const int u = blockIdx.x * BLOCK + threadIdx.x;
-    if (u >= g.n_nodes || !n.has_merged[u]) return;
+constexpr int SG = 8;
+__global__ void __launch_bounds__(BLOCK) k_sender(gtf_graph g, gtf_nodes n, gtf_edges e, gtf_params p, Ws w) {
+    const int u = (blockIdx.x * BLOCK + (int)threadIdx.x) / SG;
+    const int gl = threadIdx.x & (SG - 1);
+    if (u >= g.n_nodes || !n.has_merged[u]) return;  // group-uniform
     const int ob = g.out_ptr[u], oe = g.out_ptr[u + 1];
     if (ob == oe) return;
-    double c11 = w.c11_base[u];
-    for (int i = ob; i < oe; i++) {
-        const double vm = w.var_ms[i];
-        if (vm != -1.0) c11 = c11 + vm;
-        w.c11_seen[i] = c11;
+    const double a = n.merged_state[3 * (int64_t)u + 0];
+    const double b = n.merged_state[3 * (int64_t)u + 1];
+    const double* ng = g.gnn + 4 * (int64_t)u;
+    double carry = n.merged_cov[5 * (int64_t)u + 3];
+    for (int base = ob; base < oe; base += SG) {
+        const int i = base + gl;
+        double vm = -1.0;
+        if (i < oe) {
+            const int k = g.out_slot[i];
+            if (e.act[k] == 1) vm = highland_var_ms(a, b, ng, g.gnn + 4 * (int64_t)g.slot_dst[k], p.endcap_boundary);
+            w.var_ms[i] = vm;
+        }
+        double c = carry;
+        for (int m = 0; m < SG; m++) {
+            const double vmm = __shfl(vm, m, SG);
+            if (m <= gl && vmm != -1.0) c = c + vmm;
+        }
+        if (i < oe) w.c11_seen[i] = c;
+        carry = __shfl(c, SG - 1, SG);  // lanes past the end carry the full sum
     }
-    n.merged_cov[5 * (int64_t)u + 3] = c11;
+    if (gl == 0) n.merged_cov[5 * (int64_t)u + 3] = carry;
 }
 
 // ---------------------------------------------------------------------------
@@ -571,8 +567,8 @@ inline int grid(int n) { return (n + BLOCK - 1) / BLOCK; }
 int launch_extrap_edges(const gtf_graph* g, gtf_nodes* n, gtf_states* uts, gtf_edges* e, const gtf_params* p,
                         Ws w, hipStream_t st) {
     if (g->n_slots > 0) {
-        hipLaunchKernelGGL(k_varms, dim3(grid(g->n_slots)), dim3(BLOCK), 0, st, *g, *n, *e, *p, w);
-        hipLaunchKernelGGL(k_prefix, dim3(grid(g->n_nodes)), dim3(BLOCK), 0, st, *g, *n, w);
+        hipLaunchKernelGGL(k_sender, dim3((g->n_nodes + BLOCK / SG - 1) / (BLOCK / SG)), dim3(BLOCK), 0, st, *g, *n,
+                           *e, *p, w);
         hipLaunchKernelGGL(k_extrapolate, dim3(grid(g->n_slots)), dim3(BLOCK), 0, st, *g, *n, *uts, *e, *p, w);
     }
     hipError_t err = hipGetLastError();
@@ -775,10 +771,9 @@ int gtf_pass_ev(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* u
     hipStream_t st = (hipStream_t)stream;
     Ws w = carve(ws, g->n_nodes, g->n_slots);
     if (events) (void)hipEventRecord((hipEvent_t)events[0], st);
-    if (g->n_slots > 0) {
-        hipLaunchKernelGGL(k_varms, dim3(grid(g->n_slots)), dim3(BLOCK), 0, st, *g, *n, *e, *p, w);
-        hipLaunchKernelGGL(k_prefix, dim3(grid(g->n_nodes)), dim3(BLOCK), 0, st, *g, *n, w);
-    }
+    if (g->n_slots > 0)
+        hipLaunchKernelGGL(k_sender, dim3((g->n_nodes + BLOCK / SG - 1) / (BLOCK / SG)), dim3(BLOCK), 0, st, *g, *n,
+                           *e, *p, w);
     if (events) (void)hipEventRecord((hipEvent_t)events[1], st);
     if (g->n_slots > 0)
         hipLaunchKernelGGL(k_extrapolate, dim3(grid(g->n_slots)), dim3(BLOCK), 0, st, *g, *n, *uts, *e, *p, w);

@@ -75,11 +75,31 @@ class DeviceGraph:
             if f in ("slot_key",):
                 continue
             up(f, g.slot[f])
+        self._make_arena(self.PASS_INPUTS)
         ws_bytes = int(self.lib.gtf_workspace_bytes(g.n_nodes, g.n_slots))
         self.t["ws"] = torch.zeros(ws_bytes, dtype=torch.uint8, device=self.device)
         self._build_structs()
 
     # ---------------------------------------------------------------- memory
+    def _make_arena(self, names):
+        """place the arrays a pass mutates in one contiguous allocation, so a
+        benchmark restore of the pass input is a single device copy"""
+        torch = self.torch
+        offs, total = {}, 0
+        for k in names:
+            nb = self.t[k].numel() * self.t[k].element_size()
+            offs[k] = total
+            total += (nb + 255) // 256 * 256
+        arena = torch.zeros(max(total, 256), dtype=torch.uint8, device=self.device)
+        for k in names:
+            t = self.t[k]
+            nb = t.numel() * t.element_size()
+            view = arena[offs[k]:offs[k] + nb].view(t.dtype)
+            view.copy_(t)
+            self.t[k] = view
+        self.arena = arena
+
+
     def _up(self, name, arr):
         arr = np.ascontiguousarray(arr)
         t = self.torch.from_numpy(arr.reshape(-1) if arr.size else arr.reshape(0)).to(self.device)
@@ -218,12 +238,18 @@ class DeviceGraph:
     PASS_INPUTS = ("act", "uts_rank", "has_uts", "has_merged", "merged_state", "merged_cov", "merged_prior")
 
     def snapshot(self, names=None):
-        """device-side copy of mutable arrays (default: every one)"""
+        """device-side copy of mutable arrays (default: every one). The pass inputs
+        (PASS_INPUTS) live in one arena and snapshot as a single buffer."""
+        if names is not None and tuple(names) == tuple(self.PASS_INPUTS):
+            return {"__arena__": self.arena.clone()}
         names = names or [k for k in self.t if k in MUTABLE_NODE or
                           (k in SLOT_FIELDS and k not in STATIC_SLOT and k != "slot_key")]
         return {k: self.t[k].clone() for k in names}
 
     def restore(self, snap):
-        """copy a snapshot back (one multi-tensor copy launch)"""
-        keys = list(snap)
-        self.torch._foreach_copy_([self.t[k] for k in keys], [snap[k] for k in keys])
+        """copy a snapshot back (the pass-input arena is one device copy)"""
+        if "__arena__" in snap:
+            self.arena.copy_(snap["__arena__"], non_blocking=True)
+            return
+        for k, v in snap.items():
+            self.t[k].copy_(v, non_blocking=True)

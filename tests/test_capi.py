@@ -1,0 +1,77 @@
+"""C-ABI library checks that need no GPU: the shared library loads and exports
+every entry point include/gtf.h declares; the ctypes structs match the header."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HDR = os.path.join(ROOT, "include", "gtf.h")
+
+
+def _declared():
+    src = open(HDR).read()
+    return sorted(set(re.findall(r"^\s*(?:int|size_t|const char\*)\s+(gtf_\w+)\s*\(", src, re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+    from gtf import _native
+    if not os.path.exists(_native.LIB_PATH):
+        pytest.skip("libgtf.so not built (run __graft_entry__.build())")
+    out = subprocess.run(["nm", "-D", "--defined-only", _native.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r" T (gtf_\w+)", out))
+    missing = [s for s in _declared() if s not in exported]
+    assert not missing, missing
+    assert set(_native.SYMBOLS) <= exported
+
+
+def test_library_loads_and_binds():
+    from gtf import _native
+    if not os.path.exists(_native.LIB_PATH):
+        pytest.skip("libgtf.so not built")
+    L = _native.lib()
+    assert L.gtf_version().decode().startswith("gtf")
+    # workspace size is a pure host function
+    assert L.gtf_workspace_bytes(100, 1000) >= 256 + 8 * 1000
+
+
+def test_struct_layout_matches_header():
+    """compile a tiny C probe of offsetof() against the header and compare with ctypes"""
+    from gtf import _native as nat
+    probe = r'''
+#include <stdio.h>
+#include <stddef.h>
+#include "gtf.h"
+#define P(T, f) printf(#T "." #f " %zu\n", offsetof(T, f));
+int main(void) {
+  P(gtf_graph, slot_ptr) P(gtf_graph, slot_outpos) P(gtf_graph, layer) P(gtf_graph, sched) P(gtf_graph, n_g64)
+  P(gtf_nodes, degree) P(gtf_states, fresh) P(gtf_edges, send_mw) P(gtf_params, cluster_kl)
+  printf("sizeof.gtf_graph %zu\n", sizeof(gtf_graph));
+  return 0;
+}'''
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "p.c")
+        open(c, "w").write(probe)
+        exe = os.path.join(d, "p")
+        subprocess.check_call(["gcc", "-I", os.path.dirname(HDR), c, "-o", exe])
+        got = dict(l.rsplit(" ", 1) for l in subprocess.check_output([exe], text=True).split("\n") if l)
+    py = {"gtf_graph": nat.GtfGraph, "gtf_nodes": nat.GtfNodes, "gtf_states": nat.GtfStates,
+          "gtf_edges": nat.GtfEdges, "gtf_params": nat.GtfParams}
+    for k, v in got.items():
+        t, f = k.split(".")
+        if t == "sizeof":
+            assert ctypes.sizeof(py[f]) == int(v), k
+        else:
+            assert getattr(py[t], f).offset == int(v), k
+
+
+def test_no_fallback_without_library(monkeypatch, tmp_path):
+    """the product path fails loudly when the HIP library is missing"""
+    from gtf import _native
+    monkeypatch.setattr(_native, "LIB_PATH", str(tmp_path / "missing.so"))
+    monkeypatch.setattr(_native, "_lib", None)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        _native.lib()

@@ -45,6 +45,24 @@ def cpu_baseline(n_tracks, params):
                       "%d directed edges (pileup-200 density), %.1f s" % (g.n_nodes, g.n_edges, dt)}
 
 
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc", "pmc_c4.json")
+
+
+def committed_traffic(workload, kernel):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
+    (separate FETCH_SIZE / WRITE_SIZE passes, tools/gpu_profile.sh; corrections in
+    DESIGN.md), or None when no summary matches this workload/kernel."""
+    try:
+        with open(PMC_SUMMARY) as f:
+            s = json.load(f)
+    except OSError:
+        return None
+    if s.get("workload") != workload:
+        return None
+    k = s.get("kernels", {}).get(kernel)
+    return None if k is None else k.get("hbm_bytes_per_launch")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -79,7 +97,8 @@ def main():
     d = DeviceGraph(g, dev)
     snap = d.snapshot(DeviceGraph.PASS_INPUTS)
     K, W = args.steps, args.warmup
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(K)]
+    NE = 5
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(NE)] for _ in range(K)]
     for row in evs:      # torch creates the HIP event on first record
         for e in row:
             e.record()
@@ -110,16 +129,29 @@ def main():
     elapsed = float(t.item())
     total_edges = float(edges.item())
 
-    scan = np.mean([evs[i][0].elapsed_time(evs[i][1]) for i in range(K)])
-    extr = np.mean([evs[i][1].elapsed_time(evs[i][2]) for i in range(K)])
-    node = np.mean([evs[i][2].elapsed_time(evs[i][3]) for i in range(K)])
-    kernels = {"k_sender": scan, "k_extrapolate": extr, "k_node_seq": node}
-    # roofline for the dominant kernel (algorithmic bytes, gtf/roofline.py)
-    if node >= scan + extr:
-        name, ms, nbytes = "k_node_seq (node-local stages)", node, rf.node_bytes(g.n_edges, g.n_nodes)
-    else:
-        name, ms, nbytes = "k_sender+k_extrapolate", scan + extr, rf.extrap_bytes(g.n_edges, g.n_nodes)
+    def avg(a, b):
+        return float(np.mean([evs[i][a].elapsed_time(evs[i][b]) for i in range(K)]))
+
+    # eligible nodes of the KL clustering (3 <= |updated_track_states| <= 15), from the
+    # state after a pass (clustering does not change dict membership)
+    nst = np.add.reduceat((d.t["uts_rank"] >= 0).to(torch.int32).cpu().numpy(), g.slot_ptr[:-1]) \
+        if g.n_slots else np.zeros(0)
+    nst = np.where(np.diff(g.slot_ptr) > 0, nst, 0)
+    elig = (nst >= 3) & (nst <= 15) & (d.t["has_uts"].cpu().numpy() == 1)
+    e_elig = int(np.diff(g.slot_ptr)[elig].sum())
+    kern = {
+        "k_sender": (avg(0, 1), None),
+        "k_extrapolate": (avg(1, 2), None),
+        "k_node_multi<reweight,update>": (avg(2, 3), rf.reweight_bytes(g.n_slots, g.n_nodes)),
+        "k_node_multi<cluster> (KL-distance kernel)": (avg(3, 4), rf.kl_bytes(e_elig, int(elig.sum()))),
+    }
+    ext_ms = kern["k_sender"][0] + kern["k_extrapolate"][0]
+    cands = {"k_sender+k_extrapolate": (ext_ms, rf.extrap_bytes(g.n_edges, g.n_nodes))}
+    cands.update({k: v for k, v in kern.items() if v[1] is not None})
+    name = max(cands, key=lambda k: cands[k][0])
+    ms, nbytes = cands[name]
     achieved = nbytes / (ms * 1e-3) / 1e9
+    traffic = committed_traffic(args.workload, name)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -145,10 +177,11 @@ def main():
                        "nodes_per_gpu": g.n_nodes, "directed_edges_per_gpu": g.n_edges,
                        "parallelism": "event-parallel x%d (no collective)" % world,
                        "pass": "gtf_pass: extrapolate (a6-a8) + update (a3,a9,a10x2,a11) + KL cluster (a12-a14)"},
-            "kernel_ms": {k: round(float(v), 5) for k, v in kernels.items()},
+            "kernel_ms": {k: round(v[0], 5) for k, v in kern.items()},
             "roofline": {"bound": "hbm", "kernel": name, "achieved": achieved, "peak": rf.HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": achieved / rf.HBM_PEAK_GBS, "traffic": None,
-                         "algorithmic_bytes": nbytes},
+                         "unit": "GB/s", "frac": achieved / rf.HBM_PEAK_GBS, "traffic": traffic,
+                         "algorithmic_bytes_per_launch": nbytes, "kernel_ms": ms,
+                         "kl_eligible_nodes": int(elig.sum()), "kl_eligible_in_edges": e_elig},
             "cpu_baseline": cpu,
             "device_error_flags": flags,
         }

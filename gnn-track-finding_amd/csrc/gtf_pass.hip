@@ -784,8 +784,9 @@ int gtf_pass_ev(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* u
     // occupancy, then clustering (register-heavy) with its LDS state staging
     rc = launch_seq<EXTRAP_OPS, UPDATE_OPS>(g, n, tse, uts, e, p, w, 0.0, 0.0, st);
     if (rc) return rc;
-    rc = launch_seq<CLUSTER_UTS_OPS>(g, n, tse, uts, e, p, w, p->cluster_chi2, p->cluster_kl, st);
     if (events) (void)hipEventRecord((hipEvent_t)events[3], st);
+    rc = launch_seq<CLUSTER_UTS_OPS>(g, n, tse, uts, e, p, w, p->cluster_chi2, p->cluster_kl, st);
+    if (events) (void)hipEventRecord((hipEvent_t)events[4], st);
     return rc;
 }
 

@@ -183,14 +183,14 @@ class DeviceGraph:
                                        self.ptr("ws"), self.stream))
 
     def full_pass(self, p: Params, events=None):
-        """events: optional 4 raw hipEvent_t handles (per-kernel timing)"""
+        """events: optional 5 raw hipEvent_t handles (per-kernel timing)"""
         cp = self.cparams(p)
         if events is None:
             nat.check(self.lib.gtf_pass(ctypes.byref(self.cg), ctypes.byref(self.cn), ctypes.byref(self.ctse),
                                         ctypes.byref(self.cuts), ctypes.byref(self.ce), ctypes.byref(cp),
                                         self.ptr("ws"), self.stream))
         else:
-            arr = (ctypes.c_void_p * 4)(*events)
+            arr = (ctypes.c_void_p * 5)(*events)
             nat.check(self.lib.gtf_pass_ev(ctypes.byref(self.cg), ctypes.byref(self.cn), ctypes.byref(self.ctse),
                                            ctypes.byref(self.cuts), ctypes.byref(self.ce), ctypes.byref(cp),
                                            self.ptr("ws"), self.stream, arr))

@@ -13,7 +13,20 @@ Per pass the survey prices B_alg = 183 B per directed edge + 290 B per node:
 Sums: 183 E + 290 N. DESIGN.md "Roofline" states these figures.
 """
 
+Per kernel of gtf_pass (DESIGN.md "Roofline"):
+  * k_sender + k_extrapolate: the extrapolation side above (94 E + 104 N);
+  * k_node_multi<reweight/update> (priors, side norm, reweight x2, degree, prune,
+    priors, reweight): 100 B per slot -- read rank 4, activation 1, weight 8,
+    likelihood 8, prior 8, sender layer 8, stored x 8, TSE rank 4 and prior 8 (= 57,
+    +1 reverse-edge flag = 58); write weight 8, prior 8, lr 8, side 1, edge weight 8,
+    activation 1, TSE prior 8 (= 42) -- plus 6 B per node (flags, degree);
+  * k_node_multi<cluster> = the KL-distance kernel: SURVEY §8d's B_KL = 89 B per
+    in-edge of an eligible node (3 <= |states| <= 15) + 176 B per eligible node.
+"""
+
 EXTRAP_PER_EDGE, EXTRAP_PER_NODE = 94, 104
+REWEIGHT_PER_SLOT, REWEIGHT_PER_NODE = 100, 6
+KL_PER_EDGE, KL_PER_NODE = 89, 176
 NODE_PER_EDGE, NODE_PER_NODE = 89, 186
 PASS_PER_EDGE, PASS_PER_NODE = 183, 290
 
@@ -26,6 +39,14 @@ def extrap_bytes(n_edges, n_nodes):
 
 def node_bytes(n_edges, n_nodes):
     return NODE_PER_EDGE * n_edges + NODE_PER_NODE * n_nodes
+
+
+def reweight_bytes(n_slots, n_nodes):
+    return REWEIGHT_PER_SLOT * n_slots + REWEIGHT_PER_NODE * n_nodes
+
+
+def kl_bytes(e_elig, n_elig):
+    return KL_PER_EDGE * e_elig + KL_PER_NODE * n_elig
 
 
 def pass_bytes(n_edges, n_nodes):

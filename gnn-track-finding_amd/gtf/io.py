@@ -1,0 +1,60 @@
+"""Event CSV -> packed TrackGraph, directly (no networkx, no pandas row loops).
+
+The reference builds its graph with O(N*H) pandas lookups
+(helper.load_nodes_edges + construct_graph, helper.py:465-545; 34 s of a 35 s
+stage for one volume). Here the CSVs are read with numpy and the CSR
+is assembled vectorised. Semantics kept:
+
+* nodes: ``layer_id`` in [min_volume*1000, (max_volume+1)*1000] (helper.py:526-531,
+  pandas ``between`` is inclusive), r = sqrt(x^2 + y^2), in_volume_layer_id =
+  layer_id % 100, node order = CSV order;
+* edges: ``edges.csv`` has a "<N> <E>" first line, then node2,node1,weight
+  (helper.py:537-543); both directions are added when both ends are kept
+  (helper.py:512-518).
+
+Truth joins (particle ids, module ids) are not on the hot path and are not built.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .graph import TrackGraph
+
+
+def read_nodes(path: str, min_volume: int, max_volume: int):
+    a = np.genfromtxt(path, delimiter=",", names=True, dtype=None, encoding=None)
+    lo, hi = min_volume * 1000, (max_volume + 1) * 1000
+    keep = (a["layer_id"] >= lo) & (a["layer_id"] <= hi)
+    a = a[keep]
+    x, y, z = a["x"].astype(np.float64), a["y"].astype(np.float64), a["z"].astype(np.float64)
+    return a["node_idx"].astype(np.int64), x, y, z, np.sqrt(x**2 + y**2), a["layer_id"].astype(np.int64)
+
+
+def read_edges(path: str):
+    with open(path) as f:
+        f.readline()                      # "<N> <E>"
+        f.readline()                      # node2,node1,weight
+        e = np.loadtxt(f, delimiter=",", dtype=np.float64, ndmin=2)
+    return e[:, 0].astype(np.int64), e[:, 1].astype(np.int64)
+
+
+def load_event(event_prefix: str, min_volume: int, max_volume: int, params=None) -> TrackGraph:
+    """``event_prefix`` like ``.../event_1_filtered_graph_`` (nodes.csv / edges.csv appended)."""
+    from .synth import _assemble
+    from .params import Params
+    ids, x, y, z, r, layer = read_nodes(event_prefix + "nodes.csv", min_volume, max_volume)
+    n2, n1 = read_edges(event_prefix + "edges.csv")
+    pos = {int(v): i for i, v in enumerate(ids)}
+    idx = np.full(int(max(ids.max(), n1.max(), n2.max())) + 1 if ids.size else 1, -1, np.int64)
+    idx[ids] = np.arange(ids.size)
+    a, b = idx[n1], idx[n2]
+    ok = (a >= 0) & (b >= 0)
+    a, b = a[ok], b[ok]
+    # add_edge(node1, node2) then add_edge(node2, node1); duplicates collapse
+    src = np.concatenate([np.stack([a, b], 1), np.stack([b, a], 1)], 1).reshape(-1, 2)
+    _, first = np.unique(src[:, 0] * ids.size + src[:, 1], return_index=True)
+    src = src[np.sort(first)]
+    g = _assemble(ids.size, src[:, 0], src[:, 1], x, y, z, r, layer, params or Params())
+    g.node["node_id"] = ids.copy()
+    del pos
+    return g

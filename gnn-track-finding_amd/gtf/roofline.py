@@ -11,7 +11,6 @@ Per pass the survey prices B_alg = 183 B per directed edge + 290 B per node:
     32, deactivation 1) + 186 B per node (xyzr 32, flags/layer 2, merged outputs
     2 x (3 + 6) x 8 = 144, degree 8).
 Sums: 183 E + 290 N. DESIGN.md "Roofline" states these figures.
-"""
 
 Per kernel of gtf_pass (DESIGN.md "Roofline"):
   * k_sender + k_extrapolate: the extrapolation side above (94 E + 104 N);

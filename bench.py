@@ -45,6 +45,53 @@ def cpu_baseline(n_tracks, params):
                       "%d directed edges (pileup-200 density), %.1f s" % (g.n_nodes, g.n_edges, dt)}
 
 
+def bench_c5(dev, steps, warmup, n_events=256):
+    """Config 5: parabolic-model states + pairwise KL (gtf_parabolic_kl) over a batch of
+    256 copies of the committed volume-7 134 event (tests/golden/kat134, coordinates
+    jittered per copy), fp64 and fp32, with the fp32-vs-fp64 tolerance sweep."""
+    import torch
+    from gtf import io, parabolic, roofline as rf
+    kat = os.path.join(ROOT, "tests", "golden", "kat134")
+    g = io.load_event(os.path.join(kat, "event_1_filtered_graph_"), 7, 7)
+    truth = io.read_truth(os.path.join(kat, "truth_vol7.csv"), g.node["node_id"])
+    ptr, src = parabolic.in_edge_csr(g)
+    ptr, src, gnn, tr = parabolic.batch(ptr, src, g.node["gnn"], truth, n_events)
+    k = parabolic.ParabolicKL(ptr, src, gnn, tr, dev)
+    res = {"workload": "%d x committed vol-7 134 event (jittered copies)" % n_events, "nodes": k.n_nodes,
+           "in_edges": k.n_slots, "pairs": k.n_pairs, "listed_nodes": k.n_listed}
+    outs = {}
+    for dt in ("f64", "f32"):
+        out = k.alloc(dt, emp="var")
+        for _ in range(warmup):
+            k.run(out, dt)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for a, b in ev:
+            a.record()
+            k.run(out, dt)
+            b.record()
+        torch.cuda.synchronize()
+        wall = (time.perf_counter() - t0) / steps
+        ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+        nbytes = rf.parabolic_kl_bytes(k.n_nodes, res["listed_nodes"], k.n_slots, k.n_pairs, dt)
+        res[dt] = {"pairs_per_s": k.n_pairs / wall, "kernel_ms": ms, "wall_ms_per_step": wall * 1e3,
+                   "roofline": {"bound": "hbm", "achieved": nbytes / (ms * 1e-3) / 1e9, "peak": rf.HBM_PEAK_GBS,
+                                "unit": "GB/s", "frac": nbytes / (ms * 1e-3) / 1e9 / rf.HBM_PEAK_GBS,
+                                "algorithmic_bytes_per_launch": nbytes}}
+        outs[dt] = out
+    a = outs["f64"]["kl"].double().cpu().numpy()
+    b = outs["f32"]["kl"].double().cpu().numpy()
+    rel = np.abs(b - a) / np.maximum(np.abs(a), 1e-300)
+    res["fp32_vs_fp64"] = {
+        "rel_err_p50": float(np.percentile(rel, 50)), "rel_err_p99": float(np.percentile(rel, 99)),
+        "rel_err_p999": float(np.percentile(rel, 99.9)), "rel_err_max": float(rel.max()),
+        "decision_flips": {str(t): int(((a < t) != (b < t)).sum()) for t in (1.0, 2.0, 10.0, 100.0)},
+        "truth_identical": bool(torch.equal(outs["f64"]["truth"], outs["f32"]["truth"]))}
+    res["device_error_flags"] = k.errors()
+    return res
+
+
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc", "pmc_c4.json")
 
 
@@ -71,6 +118,7 @@ def main():
     ap.add_argument("--workload", default="c4", choices=["c2", "c3", "c4"])
     ap.add_argument("--cpu-tracks", type=int, default=4000, help="CPU-baseline sample size (tracks)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-c5", action="store_true", help="skip the config-5 parabolic-KL section")
     args = ap.parse_args()
 
     import torch
@@ -153,6 +201,10 @@ def main():
     achieved = nbytes / (ms * 1e-3) / 1e9
     traffic = committed_traffic(args.workload, name)
 
+    c5 = None
+    if rank == 0 and world == 1 and not args.no_c5:
+        c5 = bench_c5(dev, K, W)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(args.cpu_tracks, p)
@@ -184,6 +236,7 @@ def main():
                          "kl_eligible_nodes": int(elig.sum()), "kl_eligible_in_edges": e_elig},
             "cpu_baseline": cpu,
             "device_error_flags": flags,
+            "c5_parabolic_kl": c5,
         }
         if cpu:
             out["speedup_vs_cpu"] = out["value"] / cpu["value"]

@@ -1,0 +1,343 @@
+// gtf_kl.hip -- parabolic-model edge states and pairwise KL distances (SURVEY §8
+// a17) for gfx950: the training-data generator of learn_KL_parabolic_model
+// (utils.py:221-289 states, extract_metadata_trackml_parabolic_model.py:15-99 pairs).
+//
+// One group of G lanes per node, G by in-degree bucket (one thread for d <= 2 with
+// both states in registers; 4 and 8 lanes for d <= 4, <= 8; one 64-lane wavefront
+// beyond), one in-edge per lane, all buckets in one launch. Each lane forms its neighbour's parabolic
+// state in closed form and stages it in LDS; the group then deals the node's
+// d(d-1)/2 pairs round-robin over its lanes and writes them to the node's
+// contiguous pair range (coalesced: a group's lanes write consecutive pairs).
+//
+// Closed form. The reference inverts H = [[x0^2, x0, 1], [0, 0, 1], [xB^2, xB, 1]]
+// with np.linalg.inv. H maps parabola coefficients (a, b, c) to the parabola's
+// values at x0, 0 and xB, so the columns of H^-1 are the Lagrange basis
+// polynomials on {x0, 0, xB}:
+//   L0 = (1, -xB, 0) / (x0 (x0 - xB))   L1 = (1, -(x0 + xB), x0 xB) / (x0 xB)
+//   L2 = (1, -x0, 0) / (xB (xB - x0))
+// so sv = m_B L2, cov = H^-1 S H^-T = sum_k s_k L_k L_k^T and
+// cov^-1 = H^T S^-1 H = sum_k h_k h_k^T / s_k (h_k = rows of H) -- no 3x3 inverse at
+// all, and no loss of accuracy where H is ill-conditioned. Against the reference's
+// committed training CSV this matches to 8e-11 relative (tests/test_kat_parabolic.py).
+// sv[2] = 0 and cov[2][2] = s1 for every state, so the KL terms of component 2
+// vanish and a state is 7 numbers in LDS: sv0, sv1, c00, c11, i00, i01, i11.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "../../include/gtf.h"
+
+namespace gtf {
+void set_error(const char* msg);
+}
+
+namespace {
+
+constexpr int BLOCK = 256;
+
+// node frame: rotation by 2 pi - atan2(y, x) (rotate_track, utils.py:197-218, with
+// cos/sin of the angle as x/h, -y/h), then translation to the node (:262-270)
+struct Frame {
+    double ca, sa, xt, yt, x0, x, y;
+};
+
+__device__ __forceinline__ Frame node_frame(const double* gnn, int v) {
+    Frame f;
+    f.x = gnn[4 * (int64_t)v];
+    f.y = gnn[4 * (int64_t)v + 1];
+    const double h = sqrt(f.x * f.x + f.y * f.y);
+    f.ca = h > 0.0 ? f.x / h : 1.0;
+    f.sa = h > 0.0 ? -f.y / h : 0.0;
+    f.xt = f.x * f.ca - f.y * f.sa;
+    f.yt = f.x * f.sa + f.y * f.ca;
+    f.x0 = 0.0 - f.xt;  // the old origin (0, 0) rotates to (0, 0)
+    return f;
+}
+
+template <typename T>
+struct PState {
+    T s0, s1, c00, c11, i00, i01, i11;
+};
+
+// parabolic state of the edge from neighbour (xb, yb) in the node's frame
+// (utils.py:273-283); optional full fp64 outputs
+template <typename T>
+__device__ __forceinline__ PState<T> pstate(const Frame& f, double xb, double yb, bool& singular, double* sv_out,
+                                            double* cov_out) {
+    const double xB = (xb * f.ca - yb * f.sa) - f.xt;
+    const double mB = (xb * f.sa + yb * f.ca) - f.yt;
+    const double x0 = f.x0;
+    singular = (xB == 0.0) || (xB == x0) || (x0 == 0.0);
+    const double s0d = 4.0 * 4.0, s1d = 0.1 * 0.1;   // sigma0**2, sigmaA**2 = sigmaB**2 (:223-229)
+    if (sv_out || cov_out) {
+        const double r0 = 1.0 / (x0 * (x0 - xB)), r1 = 1.0 / (x0 * xB), r2 = 1.0 / (xB * (xB - x0));
+        const double L0[3] = {r0, -xB * r0, 0.0};
+        const double L1[3] = {r1, -(x0 + xB) * r1, 1.0};
+        const double L2[3] = {r2, -x0 * r2, 0.0};
+        if (sv_out) { sv_out[0] = mB * L2[0]; sv_out[1] = mB * L2[1]; sv_out[2] = 0.0; }
+        if (cov_out)
+            for (int i = 0; i < 3; i++)
+                for (int j = 0; j < 3; j++)
+                    cov_out[3 * i + j] = s0d * L0[i] * L0[j] + s1d * L1[i] * L1[j] + s1d * L2[i] * L2[j];
+    }
+    const T X0 = (T)x0, XB = (T)xB, MB = (T)mB;
+    const T s0 = (T)s0d, s1 = (T)s1d;
+    const T r0 = T(1) / (X0 * (X0 - XB)), r1 = T(1) / (X0 * XB), r2 = T(1) / (XB * (XB - X0));
+    const T a0 = r0, b0 = -XB * r0;
+    const T a1 = r1, b1 = -(X0 + XB) * r1;
+    const T a2 = r2, b2 = -X0 * r2;
+    PState<T> p;
+    p.s0 = MB * a2;
+    p.s1 = MB * b2;
+    p.c00 = s0 * a0 * a0 + s1 * a1 * a1 + s1 * a2 * a2;
+    p.c11 = s0 * b0 * b0 + s1 * b1 * b1 + s1 * b2 * b2;
+    const T w0 = T(1) / s0, w2 = T(1) / s1;  // h1 = (0, 0, 1) adds nothing to the [a, b] block
+    const T X02 = X0 * X0, XB2 = XB * XB;
+    p.i00 = w0 * X02 * X02 + w2 * XB2 * XB2;
+    p.i01 = w0 * X02 * X0 + w2 * XB2 * XB;
+    p.i11 = w0 * X02 + w2 * XB2;
+    return p;
+}
+
+// KLDistance(mean_i, cov_i, inv_i, mean_j, cov_j, inv_j) (:15-17): the trace of the
+// element-wise product is the sum of the diagonal products
+template <typename T>
+__device__ __forceinline__ T pkl(const PState<T>& a, const PState<T>& b) {
+    const T tr = (a.c00 - b.c00) * (b.i00 - a.i00) + (a.c11 - b.c11) * (b.i11 - a.i11);
+    const T d0 = a.s0 - b.s0, d1 = a.s1 - b.s1;
+    const T S00 = a.i00 + b.i00, S01 = a.i01 + b.i01, S11 = a.i11 + b.i11;
+    return tr + (d0 * (d0 * S00 + d1 * S01) + d1 * (d0 * S01 + d1 * S11));
+}
+
+template <typename T, int CAP>
+struct KlStage {
+    T s0[CAP], s1[CAP], c00[CAP], c11[CAP], i00[CAP], i01[CAP], i11[CAP];
+    long long tr[CAP];  // neighbour truth ids (pair truth flags without re-gathering)
+};
+
+template <typename T, typename St>
+__device__ __forceinline__ void put(volatile St* s, int i, const PState<T>& p) {
+    s->s0[i] = p.s0; s->s1[i] = p.s1; s->c00[i] = p.c00; s->c11[i] = p.c11;
+    s->i00[i] = p.i00; s->i01[i] = p.i01; s->i11[i] = p.i11;
+}
+template <typename T, typename St>
+__device__ __forceinline__ PState<T> get(const volatile St* s, int i) {
+    return PState<T>{s->s0[i], s->s1[i], s->c00[i], s->c11[i], s->i00[i], s->i01[i], s->i11[i]};
+}
+
+template <int G>
+__device__ __forceinline__ double grp_sum(double x) {
+#pragma unroll
+    for (int o = G / 2; o > 0; o >>= 1) x += __shfl_xor(x, o, G);
+    return x;
+}
+
+// row i, column j of the row-major lower-triangle pair index t = i (i - 1) / 2 + j
+__device__ __forceinline__ void pair_ij(int t, int& i, int& j) {
+    int r = (int)((1.0f + sqrtf(1.0f + 8.0f * (float)t)) * 0.5f);
+    while (r * (r - 1) / 2 > t) r--;
+    while ((r + 1) * r / 2 <= t) r++;
+    i = r;
+    j = t - r * (r - 1) / 2;
+}
+
+// group sizes of the four degree buckets of gtf_kl_graph.list (d <= 2, <= 4, <= 8, > 8)
+constexpr int BG[4] = {1, 4, 8, 64};
+constexpr size_t stage_bytes(int G, size_t t) { return (size_t)(BLOCK / G) * G * (7 * t + 8); }
+
+// one node per group of G lanes; states staged in LDS when d <= G (always, except in
+// the wavefront bucket beyond 64 in-edges, where pair lanes recompute both states)
+template <typename T, int G, bool STATES>
+__device__ __forceinline__ void pkl_node(const gtf_kl_graph& g, const gtf_kl_out& o, const int32_t* list, int count,
+                                         int bid, char* smem) {
+    using Stage = KlStage<T, G>;
+    const int gi = (bid * BLOCK + (int)threadIdx.x) / G;
+    const int gl = threadIdx.x & (G - 1);
+    if (gi >= count) return;  // group-uniform
+    const int v = list[gi];
+    const int lo = g.slot_ptr[v], d = g.slot_ptr[v + 1] - lo;
+    if (d < 1) return;
+    volatile Stage* stg = (volatile Stage*)smem + (int)threadIdx.x / G;
+    const Frame f = node_frame(g.gnn, v);
+
+    // states of the node's in-edges and the gradients dy/dx (utils.py:249-254, 273-283)
+    double gsum = 0.0, gr0 = 0.0;
+    bool sing = false;
+    for (int q = gl; q < d; q += G) {
+        const int k = lo + q;
+        const int u = g.slot_src[k];
+        const double xb = g.gnn[4 * (int64_t)u], yb = g.gnn[4 * (int64_t)u + 1];
+        bool s;
+        const PState<T> p = pstate<T>(f, xb, yb, s, STATES ? o.sv + 3 * (int64_t)k : nullptr,
+                                      STATES ? o.cov + 9 * (int64_t)k : nullptr);
+        sing |= s;
+        if (d <= G) {
+            put<T>(stg, q, p);
+            if (g.truth) stg->tr[q] = g.truth[u];
+        }
+        const double gr = (f.y - yb) / (f.x - xb);
+        if (q == gl) gr0 = gr;
+        gsum += gr;
+    }
+    if (sing && o.err) atomicOr(o.err, (uint32_t)GTF_ERR_SINGULAR_H);
+    if (o.emp_var || o.emp_mean) {  // np.mean / np.var over the neighbours (:286)
+        const double mean = grp_sum<G>(gsum) / (double)d;
+        double vs = 0.0;
+        for (int q = gl; q < d; q += G) {
+            double gr = gr0;
+            if (q != gl) {
+                const int u = g.slot_src[lo + q];
+                gr = (f.y - g.gnn[4 * (int64_t)u + 1]) / (f.x - g.gnn[4 * (int64_t)u]);
+            }
+            vs += (gr - mean) * (gr - mean);
+        }
+        vs = grp_sum<G>(vs);
+        if (gl == 0) {
+            if (o.emp_var) o.emp_var[v] = vs / (double)d;
+            if (o.emp_mean) o.emp_mean[v] = mean;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+
+    // pairs i > j, row-major, round-robin over the lanes: consecutive lanes write
+    // consecutive distances (calc_pairwise_distances, :19-25)
+    const int np = d * (d - 1) / 2;
+    const int64_t base = g.pair_ptr[v];
+    const long long tv = g.truth ? g.truth[v] : 0;
+    T* kl = (T*)o.kl;
+    for (int t = gl; t < np; t += G) {
+        int i, j;
+        pair_ij(t, i, j);
+        PState<T> a, b;
+        long long ti = 0, tj = 0;
+        if (d <= G) {
+            a = get<T>(stg, i);
+            b = get<T>(stg, j);
+            if (o.truth) { ti = stg->tr[i]; tj = stg->tr[j]; }
+        } else {  // beyond the LDS stage (wavefront bucket, d > 64): recompute both states
+            bool s;
+            const int ui = g.slot_src[lo + i], uj = g.slot_src[lo + j];
+            a = pstate<T>(f, g.gnn[4 * (int64_t)ui], g.gnn[4 * (int64_t)ui + 1], s, nullptr, nullptr);
+            b = pstate<T>(f, g.gnn[4 * (int64_t)uj], g.gnn[4 * (int64_t)uj + 1], s, nullptr, nullptr);
+            if (o.truth) { ti = g.truth[ui]; tj = g.truth[uj]; }
+        }
+        kl[base + t] = pkl<T>(a, b);
+        if (o.truth) o.truth[base + t] = (int8_t)(tv == ti && ti == tj && tv == tj);  // (:84-95)
+    }
+}
+
+// d <= 2: one thread per node, both states in registers (the bulk of a TrackML
+// volume: 88 % of the listed nodes of the vol-7 134 event)
+template <typename T, bool STATES>
+__device__ __forceinline__ void pkl_node1(const gtf_kl_graph& g, const gtf_kl_out& o, const int32_t* list, int count,
+                                          int bid) {
+    const int gi = bid * BLOCK + (int)threadIdx.x;
+    if (gi >= count) return;
+    const int v = list[gi];
+    const int lo = g.slot_ptr[v], d = g.slot_ptr[v + 1] - lo;
+    if (d < 1 || d > 2) return;
+    const Frame f = node_frame(g.gnn, v);
+    const int u0 = g.slot_src[lo];
+    const int u1 = d == 2 ? g.slot_src[lo + 1] : u0;
+    const double x0 = g.gnn[4 * (int64_t)u0], y0 = g.gnn[4 * (int64_t)u0 + 1];
+    const double x1 = g.gnn[4 * (int64_t)u1], y1 = g.gnn[4 * (int64_t)u1 + 1];
+    bool s0, s1 = false;
+    const PState<T> a = pstate<T>(f, x0, y0, s0, STATES ? o.sv + 3 * (int64_t)lo : nullptr,
+                                  STATES ? o.cov + 9 * (int64_t)lo : nullptr);
+    PState<T> b = a;
+    if (d == 2)
+        b = pstate<T>(f, x1, y1, s1, STATES ? o.sv + 3 * (int64_t)(lo + 1) : nullptr,
+                      STATES ? o.cov + 9 * (int64_t)(lo + 1) : nullptr);
+    if ((s0 || s1) && o.err) atomicOr(o.err, (uint32_t)GTF_ERR_SINGULAR_H);
+    const double g0 = (f.y - y0) / (f.x - x0);
+    const double g1 = d == 2 ? (f.y - y1) / (f.x - x1) : g0;
+    const double mean = (d == 2 ? g0 + g1 : g0) / (double)d;
+    if (o.emp_var) o.emp_var[v] = (d == 2 ? (g0 - mean) * (g0 - mean) + (g1 - mean) * (g1 - mean) : 0.0 * (g0 - mean))
+                                  / (double)d;
+    if (o.emp_mean) o.emp_mean[v] = mean;
+    if (d == 2) {
+        const int64_t p = g.pair_ptr[v];
+        ((T*)o.kl)[p] = pkl<T>(b, a);   // pair (i, j) = (1, 0)
+        if (o.truth) {
+            const long long tv = g.truth[v], ti = g.truth[u1], tj = g.truth[u0];
+            o.truth[p] = (int8_t)(tv == ti && ti == tj && tv == tj);
+        }
+    }
+}
+
+struct KlBuckets {
+    int32_t blocks[4];
+};
+
+// one launch over the four buckets; wavefront-bucket blocks first (longest-running)
+// 6 waves per SIMD: fewer VGPRs than the compiler's default pick (measured 10 % faster
+// on config 5 without spills); 8 spills
+#ifndef GTF_KL_WAVES
+#define GTF_KL_WAVES 6
+#endif
+#define KL_ATTR __attribute__((amdgpu_waves_per_eu(GTF_KL_WAVES)))
+template <typename T, bool STATES>
+__global__ void __launch_bounds__(BLOCK) KL_ATTR k_parabolic_kl(gtf_kl_graph g, gtf_kl_out o, KlBuckets bk) {
+    __shared__ __attribute__((aligned(16))) char smem[stage_bytes(4, sizeof(T)) > stage_bytes(64, sizeof(T))
+                                                          ? stage_bytes(4, sizeof(T))
+                                                          : stage_bytes(64, sizeof(T))];
+    int b = blockIdx.x;
+    if (b < bk.blocks[3]) { pkl_node<T, 64, STATES>(g, o, g.list[3], g.count[3], b, smem); return; }
+    b -= bk.blocks[3];
+    if (b < bk.blocks[2]) { pkl_node<T, 8, STATES>(g, o, g.list[2], g.count[2], b, smem); return; }
+    b -= bk.blocks[2];
+    if (b < bk.blocks[1]) { pkl_node<T, 4, STATES>(g, o, g.list[1], g.count[1], b, smem); return; }
+    b -= bk.blocks[1];
+    pkl_node1<T, STATES>(g, o, g.list[0], g.count[0], b);
+}
+
+template <typename T>
+int launch(const gtf_kl_graph* g, const gtf_kl_out* o, hipStream_t st) {
+    KlBuckets bk;
+    int total = 0;
+    for (int i = 0; i < 4; i++) {
+        bk.blocks[i] = (g->count[i] + BLOCK / BG[i] - 1) / (BLOCK / BG[i]);
+        total += bk.blocks[i];
+    }
+    if (total > 0) {
+        if (o->sv || o->cov)
+            hipLaunchKernelGGL((k_parabolic_kl<T, true>), dim3(total), dim3(BLOCK), 0, st, *g, *o, bk);
+        else
+            hipLaunchKernelGGL((k_parabolic_kl<T, false>), dim3(total), dim3(BLOCK), 0, st, *g, *o, bk);
+    }
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) {
+        gtf::set_error(hipGetErrorString(e));
+        return -1;
+    }
+    return 0;
+}
+
+}  // namespace
+
+extern "C" int gtf_parabolic_kl(const gtf_kl_graph* g, int32_t dtype, const gtf_kl_out* out, gtf_stream_t stream) {
+    if (!g || !out) { gtf::set_error("gtf_parabolic_kl: null argument"); return -2; }
+    if (g->n_nodes < 0 || g->n_slots < 0) { gtf::set_error("gtf_parabolic_kl: negative sizes"); return -2; }
+    int listed = 0;
+    for (int i = 0; i < 4; i++) {
+        if (g->count[i] < 0 || (g->count[i] > 0 && !g->list[i])) {
+            gtf::set_error("gtf_parabolic_kl: bad node list");
+            return -2;
+        }
+        listed += g->count[i];
+    }
+    if (listed && (!g->slot_ptr || !g->slot_src || !g->gnn || !g->pair_ptr || !out->kl)) {
+        gtf::set_error("gtf_parabolic_kl: missing arrays");
+        return -2;
+    }
+    if ((out->sv == nullptr) != (out->cov == nullptr)) {
+        gtf::set_error("gtf_parabolic_kl: sv and cov outputs go together");
+        return -2;
+    }
+    if (out->truth && !g->truth) { gtf::set_error("gtf_parabolic_kl: truth output needs graph truth"); return -2; }
+    hipStream_t st = (hipStream_t)stream;
+    if (dtype == GTF_F64) return launch<double>(g, out, st);
+    if (dtype == GTF_F32) return launch<float>(g, out, st);
+    gtf::set_error("gtf_parabolic_kl: dtype must be GTF_F64 or GTF_F32");
+    return -2;
+}

@@ -690,6 +690,11 @@ int launch_seq(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* ut
 
 }  // namespace
 
+namespace gtf {
+// error text for gtf_last_error from the other translation units (gtf_kl.hip)
+void set_error(const char* msg) { snprintf(g_err, sizeof(g_err), "%s", msg); }
+}  // namespace gtf
+
 extern "C" {
 
 size_t gtf_workspace_bytes(int32_t n_nodes, int32_t n_slots) {

@@ -8,7 +8,7 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libgtf.so")
+LIB_PATH = os.environ.get("GTF_LIB") or os.path.join(HERE, "libgtf.so")   # GTF_LIB: an alternative build
 
 P = ctypes.c_void_p
 I32 = ctypes.c_int32
@@ -42,6 +42,17 @@ class GtfParams(ctypes.Structure):
                 ("chi2_cut", F64), ("reweight_threshold", F64), ("cluster_chi2", F64), ("cluster_kl", F64)]
 
 
+class GtfKlGraph(ctypes.Structure):
+    _fields_ = [("n_nodes", I32), ("n_slots", I32), ("slot_ptr", P), ("slot_src", P), ("gnn", P), ("truth", P),
+                ("pair_ptr", P), ("list", P * 4), ("count", I32 * 4)]
+
+
+class GtfKlOut(ctypes.Structure):
+    _fields_ = [("kl", P), ("truth", P), ("emp_var", P), ("emp_mean", P), ("sv", P), ("cov", P), ("err", P)]
+
+
+GTF_F64, GTF_F32 = 0, 1
+
 ERR_FLAGS = {
     1: "KeyError: sender has no track_state_estimates entry for the receiver (extrapolate_merged_states.py:384)",
     2: "KeyError: last state key has no edge (helper.py:131/138)",
@@ -50,12 +61,14 @@ ERR_FLAGS = {
     16: "ZeroDivisionError: empty state dict (helper.py:90)",
     32: "ValueError: NaN KL distance (clustering.py:117)",
     64: "KeyError: node has no state dict (remove_state_metadata.py:39)",
+    128: "LinAlgError: singular parabola matrix H (learn_KL_parabolic_model utils.py:277)",
 }
 
 # exported symbols (must match include/gtf.h; tests check the .so exports all of them)
 SYMBOLS = ["gtf_workspace_bytes", "gtf_clear_errors", "gtf_read_errors", "gtf_extrapolate", "gtf_update",
            "gtf_message_passing", "gtf_node_ops",
-           "gtf_cluster", "gtf_pass", "gtf_pass_ev", "gtf_tag_prepare", "gtf_tag_sweep", "gtf_last_error", "gtf_version"]
+           "gtf_cluster", "gtf_pass", "gtf_pass_ev", "gtf_tag_prepare", "gtf_tag_sweep", "gtf_parabolic_kl", "gtf_last_error",
+           "gtf_version"]
 
 OPS = {"ranks": 1, "priors_tse": 2, "priors_uts": 3, "reweight_uts": 4, "degree": 5, "prune": 6, "mw_tse": 7,
        "mw_uts": 8, "cluster_tse": 9, "cluster_uts": 10}
@@ -87,11 +100,12 @@ def lib():
     L.gtf_pass_ev.argtypes = [G, N, S, S, E, PR, P, P, ctypes.POINTER(P)]
     L.gtf_tag_prepare.argtypes = [G, P, P, P, P, P]
     L.gtf_tag_sweep.argtypes = [G, P, P, P, P, P, P]
+    L.gtf_parabolic_kl.argtypes = [ctypes.POINTER(GtfKlGraph), I32, ctypes.POINTER(GtfKlOut), P]
     L.gtf_last_error.restype = ctypes.c_char_p
     L.gtf_version.restype = ctypes.c_char_p
     for fn in ("gtf_clear_errors", "gtf_read_errors", "gtf_extrapolate", "gtf_update", "gtf_cluster", "gtf_pass",
                "gtf_pass_ev", "gtf_message_passing", "gtf_node_ops",
-               "gtf_tag_prepare", "gtf_tag_sweep"):
+               "gtf_tag_prepare", "gtf_tag_sweep", "gtf_parabolic_kl"):
         getattr(L, fn).restype = ctypes.c_int
     _lib = L
     return L

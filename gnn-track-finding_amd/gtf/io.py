@@ -58,3 +58,21 @@ def load_event(event_prefix: str, min_volume: int, max_volume: int, params=None)
     g.node["node_id"] = ids.copy()
     del pos
     return g
+
+
+def read_truth(path: str, node_ids: np.ndarray) -> np.ndarray:
+    """truth_particle per node, aligned with ``node_ids`` (-1 where absent).
+
+    ``path`` is a hit->particle mapping CSV with ``node_idx`` and ``particle_id``
+    columns (the reference's event_truth/*-full-mapping-*.csv, or a two-column
+    extract of it). A node's truth is the particle of its first row -- the first of
+    ``unique()`` in helper.construct_graph (helper.py:468-471, 493)."""
+    a = np.genfromtxt(path, delimiter=",", names=True, dtype=None, encoding=None)
+    nid = a["node_idx"].astype(np.int64)
+    pid = a["particle_id"].astype(np.int64)
+    u, first = np.unique(nid, return_index=True)
+    out = np.full(node_ids.shape[0], -1, np.int64)
+    pos = np.searchsorted(u, node_ids)
+    ok = (pos < u.size) & (u[np.minimum(pos, u.size - 1)] == node_ids)
+    out[ok] = pid[first[pos[ok]]]
+    return out

@@ -1,0 +1,168 @@
+"""Parabolic-model edge states and pairwise KL distances on the GPU.
+
+Host side of ``gtf_parabolic_kl`` (include/gtf.h). It mirrors the reference's
+training-data generator in learn_KL_parabolic_model/src/generate_training_data:
+
+* ``compute_track_state_estimates`` (utils.py:221-289): per in-edge parabolic
+  state ``edge_state_vector`` (3,) / ``edge_covariance`` (3, 3) and the node's
+  ``xy_edge_gradient_mean_var``;
+* ``calc_pairwise_distances`` + the row loop of
+  extract_metadata_trackml_parabolic_model.py:15-99: one ``(kl_dist, emp_var,
+  truth)`` row per pair i > j of the in-edges of every node with >= 2 in-edges.
+
+Pairs are laid out node by node (node order), row-major lower triangle over the
+node's in-slots (slot order = sender index order); ``ParabolicKL.pair_index``
+gives each row's node and slot positions. The reference orders its rows by glob()
+file order and dict order, which carry no meaning; the row
+multiset is what parity is checked on.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _native as nat
+from .graph import TrackGraph
+
+BUCKETS = ((1, 2), (3, 4), (5, 8), (9, 1 << 30))   # in-degree ranges of the 1/4/8/64-lane groups
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def in_edge_csr(g: TrackGraph):
+    """(slot_ptr, slot_src) of the graph's in-edges (slots that are edges)."""
+    ise = g.slot["is_edge"].astype(bool)
+    if ise.all():
+        return g.slot_ptr.astype(np.int32), g.slot["slot_src"].astype(np.int32)
+    dst = g.slot_dst()
+    cnt = np.bincount(dst[ise], minlength=g.n_nodes)
+    ptr = np.zeros(g.n_nodes + 1, np.int32)
+    np.cumsum(cnt, out=ptr[1:])
+    return ptr, g.slot["slot_src"][ise].astype(np.int32)
+
+
+class ParabolicKL:
+    """Device-resident KL graph of one or many events (events concatenated into one CSR)."""
+
+    def __init__(self, slot_ptr, slot_src, gnn, truth=None, device="cuda", with_single=False):
+        slot_ptr = np.ascontiguousarray(slot_ptr, np.int32)
+        self.n_nodes = int(slot_ptr.shape[0] - 1)
+        self.n_slots = int(slot_ptr[-1])
+        d = np.diff(slot_ptr).astype(np.int64)
+        npair = np.where(d >= 2, d * (d - 1) // 2, 0)
+        pair_ptr = np.zeros(self.n_nodes + 1, np.int64)
+        np.cumsum(npair, out=pair_ptr[1:])
+        self.n_pairs = int(pair_ptr[-1])
+        lo = 1 if with_single else 2
+        lists = [np.nonzero((d >= max(a, lo)) & (d <= b))[0].astype(np.int32) for a, b in BUCKETS]
+        self.n_listed = int(sum(x.size for x in lists))
+        self.degree = d
+        self.pair_ptr_host = pair_ptr
+        dev = torch.device(device)
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+        self.slot_ptr = t(slot_ptr)
+        self.slot_src = t(np.asarray(slot_src, np.int32))
+        self.gnn = t(np.asarray(gnn, np.float64).reshape(-1, 4))
+        self.truth = t(np.asarray(truth, np.int64)) if truth is not None else None
+        self.pair_ptr = t(pair_ptr)
+        self.lists = [t(x) for x in lists]
+        self.device = dev
+        self.err = torch.zeros(1, dtype=torch.int32, device=dev)
+        self._g = nat.GtfKlGraph(self.n_nodes, self.n_slots, _ptr(self.slot_ptr), _ptr(self.slot_src),
+                                 _ptr(self.gnn), _ptr(self.truth), _ptr(self.pair_ptr),
+                                 (ctypes.c_void_p * 4)(*[x.data_ptr() if x.numel() else None for x in self.lists]),
+                                 (ctypes.c_int32 * 4)(*[x.numel() for x in self.lists]))
+
+    @classmethod
+    def from_graph(cls, g: TrackGraph, truth=None, device="cuda", with_single=False):
+        ptr, src = in_edge_csr(g)
+        return cls(ptr, src, g.node["gnn"], truth, device, with_single)
+
+    def alloc(self, dtype="f64", truth=True, emp=True, states=False):
+        f = torch.float64 if dtype == "f64" else torch.float32
+        # never a null pointer, even with no pairs (the C-ABI rejects null outputs)
+        z = lambda n, dt: torch.empty(max(n, 1), dtype=dt, device=self.device)[:n]  # noqa: E731
+        out = {"kl": z(self.n_pairs, f)}
+        if truth and self.truth is not None:
+            out["truth"] = z(self.n_pairs, torch.int8)
+        if emp:     # True: gradient mean and variance; "var": variance only (the training rows)
+            out["emp_var"] = torch.full((self.n_nodes,), float("nan"), dtype=torch.float64, device=self.device)
+            if emp is True:
+                out["emp_mean"] = torch.full((self.n_nodes,), float("nan"), dtype=torch.float64,
+                                             device=self.device)
+        if states:
+            out["sv"] = torch.full((self.n_slots, 3), float("nan"), dtype=torch.float64, device=self.device)
+            out["cov"] = torch.full((self.n_slots, 3, 3), float("nan"), dtype=torch.float64, device=self.device)
+        return out
+
+    def run(self, out, dtype="f64", stream=None):
+        """launch gtf_parabolic_kl into the buffers of ``alloc`` (stream-ordered)."""
+        o = nat.GtfKlOut(_ptr(out["kl"]), _ptr(out.get("truth")), _ptr(out.get("emp_var")),
+                         _ptr(out.get("emp_mean")), _ptr(out.get("sv")), _ptr(out.get("cov")), _ptr(self.err))
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        nat.check(nat.lib().gtf_parabolic_kl(ctypes.byref(self._g), nat.GTF_F64 if dtype == "f64" else nat.GTF_F32,
+                                             ctypes.byref(o), ctypes.c_void_p(s.cuda_stream)))
+        return out
+
+    def errors(self):
+        return int(self.err.item())
+
+    def pair_index(self):
+        """(node, i, j) of every pair row (host)."""
+        d = self.degree
+        nodes = np.nonzero(d >= 2)[0]
+        node = np.repeat(nodes, (d[nodes] * (d[nodes] - 1) // 2))
+        t = np.arange(self.n_pairs, dtype=np.int64) - self.pair_ptr_host[node]
+        i = np.floor((1 + np.sqrt(1 + 8 * t.astype(np.float64))) / 2).astype(np.int64)
+        i -= (i * (i - 1) // 2 > t)
+        i += ((i + 1) * i // 2 <= t)
+        return node, i, t - i * (i - 1) // 2
+
+
+def training_rows(g: TrackGraph, truth=None, dtype="f64", device="cuda"):
+    """(node, i, j, kl_dist, emp_var, truth) rows of extract_metadata_trackml_parabolic_model.py
+    for one event graph, computed on the GPU."""
+    ptr, src = in_edge_csr(g)
+    return training_rows_csr(ptr, src, g.node["gnn"], truth, dtype, device)
+
+
+def training_rows_csr(slot_ptr, slot_src, gnn, truth=None, dtype="f64", device="cuda"):
+    k = ParabolicKL(slot_ptr, slot_src, gnn, truth, device)
+    out = k.run(k.alloc(dtype, truth=truth is not None, emp="var"), dtype)
+    node, i, j = k.pair_index()
+    ev = out["emp_var"].cpu().numpy()[node]
+    tr = out["truth"].cpu().numpy() if "truth" in out else np.zeros(k.n_pairs, np.int8)
+    flags = k.errors()
+    if flags:
+        raise np.linalg.LinAlgError(nat.ERR_FLAGS[128])
+    return node, i, j, out["kl"].cpu().numpy(), ev, tr
+
+
+def compute_track_state_estimates(g: TrackGraph, device="cuda"):
+    """Per in-edge parabolic states and per-node gradient (mean, var) of one graph
+    (utils.py:221-289): returns (sv [S,3], cov [S,3,3], grad_mean [N], grad_var [N]),
+    slots in the graph's in-edge order."""
+    k = ParabolicKL.from_graph(g, None, device, with_single=True)
+    out = k.run(k.alloc("f64", truth=False, emp=True, states=True), "f64")
+    if k.errors():
+        raise np.linalg.LinAlgError(nat.ERR_FLAGS[128])
+    return (out["sv"].cpu().numpy(), out["cov"].cpu().numpy(), out["emp_mean"].cpu().numpy(),
+            out["emp_var"].cpu().numpy())
+
+
+def batch(slot_ptr, slot_src, gnn, truth, n_events, jitter=1e-3, seed=0):
+    """n_events copies of one event concatenated into one CSR (the config-5 batch):
+    copy e > 0 has every hit moved by a seeded N(0, jitter) mm in x and y, so the
+    events differ. Truth ids repeat per copy (pairs never span copies)."""
+    rng = np.random.default_rng(seed)
+    n, s = gnn.shape[0], slot_src.shape[0]
+    ptrs = [np.asarray(slot_ptr[:-1], np.int64) + e * s for e in range(n_events)] + [np.array([n_events * s])]
+    src = np.concatenate([np.asarray(slot_src, np.int64) + e * n for e in range(n_events)])
+    g = np.tile(np.asarray(gnn, np.float64), (n_events, 1))
+    g[n:, :2] += rng.normal(0.0, jitter, (g.shape[0] - n, 2))
+    tr = np.tile(np.asarray(truth, np.int64), n_events) if truth is not None else None
+    return np.concatenate(ptrs).astype(np.int32), src.astype(np.int32), g, tr

@@ -21,7 +21,18 @@ Per kernel of gtf_pass (DESIGN.md "Roofline"):
     activation 1, TSE prior 8 (= 42) -- plus 6 B per node (flags, degree);
   * k_node_multi<cluster> = the KL-distance kernel: SURVEY §8d's B_KL = 89 B per
     in-edge of an eligible node (3 <= |states| <= 15) + 176 B per eligible node.
+
+Parabolic-model KL kernel (gtf_parabolic_kl, §8 a17), minimal unique traffic:
+  * 24 B per node of the batch (GNN x, y and truth id, read once: neighbours
+    re-read them from cache);
+  * 28 B per listed node (d >= 2): list entry 4, slot_ptr 4, pair_ptr 8, emp_var 8
+    written, plus its own coordinates counted above;
+  * 4 B per in-edge (slot_src);
+  * 9 B per pair in fp64 (distance 8 + truth flag 1), 5 B in fp32.
 """
+
+PKL_PER_NODE, PKL_PER_LISTED, PKL_PER_SLOT = 24, 28, 4
+PKL_PER_PAIR = {"f64": 9, "f32": 5}
 
 EXTRAP_PER_EDGE, EXTRAP_PER_NODE = 94, 104
 REWEIGHT_PER_SLOT, REWEIGHT_PER_NODE = 100, 6
@@ -50,3 +61,8 @@ def kl_bytes(e_elig, n_elig):
 
 def pass_bytes(n_edges, n_nodes):
     return PASS_PER_EDGE * n_edges + PASS_PER_NODE * n_nodes
+
+
+def parabolic_kl_bytes(n_nodes, n_listed, n_slots, n_pairs, dtype="f64"):
+    return (PKL_PER_NODE * n_nodes + PKL_PER_LISTED * n_listed + PKL_PER_SLOT * n_slots
+            + PKL_PER_PAIR[dtype] * n_pairs)

@@ -116,7 +116,8 @@ enum {
     GTF_ERR_TIE_EMPTIED = 8,       /* ValueError clustering.py:116 (tie removed every state) */
     GTF_ERR_EMPTY_DICT_MW = 16,    /* ZeroDivisionError helper.py:90 */
     GTF_ERR_NAN_KL = 32,           /* ValueError clustering.py:117 (list.index of NaN) */
-    GTF_ERR_NO_STATE_DICT = 64     /* KeyError remove_state_metadata.py:39 */
+    GTF_ERR_NO_STATE_DICT = 64,    /* KeyError remove_state_metadata.py:39 */
+    GTF_ERR_SINGULAR_H = 128       /* LinAlgError learn_KL_parabolic_model/.../utils.py:277 (x_B = 0 or x_B = x_0) */
 };
 
 /* Workspace: caller allocates gtf_workspace_bytes() bytes of device memory. */
@@ -162,9 +163,10 @@ int gtf_cluster(const gtf_graph* g, gtf_nodes* n, gtf_states* states, gtf_edges*
 /* extrapolate -> update -> cluster(updated_track_states, p->cluster_chi2, p->cluster_kl) */
 int gtf_pass(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts, gtf_edges* e,
              const gtf_params* p, void* workspace, gtf_stream_t stream);
-/* gtf_pass with hipEvent_t events[4] recorded on the stream before the sender scan,
- * after it, after the edge extrapolation kernel and after the fused node kernel
- * (per-kernel timing for the roofline report; events may be NULL). */
+/* gtf_pass with hipEvent_t events[5] recorded on the stream before the sender scan,
+ * after it, after the edge extrapolation kernel, after the reweight/update node kernel
+ * and after the clustering node kernel (per-kernel timing for the roofline report;
+ * events may be NULL). */
 int gtf_pass_ev(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts, gtf_edges* e,
                 const gtf_params* p, void* workspace, gtf_stream_t stream, void* const* events);
 
@@ -176,6 +178,51 @@ int gtf_tag_prepare(const gtf_graph* g, const double* radius, uint8_t* keep, uin
 /* one Jacobi sweep: tags_out[u] = max(tags_in[u], tags_in[kept neighbours]); flips += changes */
 int gtf_tag_sweep(const gtf_graph* g, const uint8_t* keep, const uint8_t* processed,
                   const int64_t* tags_in, int64_t* tags_out, int32_t* flips, gtf_stream_t stream);
+
+/* ---- Parabolic-model KL training data -------------------------
+ * learn_KL_parabolic_model/src/generate_training_data: the per-edge parabolic
+ * state of compute_track_state_estimates (utils.py:221-289; S = diag(16, 0.01,
+ * 0.01), H rows [x^2, x, 1]) for every in-edge of a node, and the pairwise KL
+ * distance KLDistance / calc_pairwise_distances (extract_metadata_trackml_parabolic_
+ * model.py:15-25) of every pair i > j of a node with >= 2 in-edges (:61-62), with the
+ * node's gradient variance (utils.py:240-254, :286) and the pair truth flag (:82-95).
+ *
+ * Pairs of node v are written at out->kl[pair_ptr[v] + t], t = i (i - 1) / 2 + j
+ * (row-major lower triangle over the node's in-slots, slot order); pair_ptr[v + 1] -
+ * pair_ptr[v] must be d (d - 1) / 2 for d = slot_ptr[v + 1] - slot_ptr[v] >= 2, else 0.
+ * emp_var is the variance over in-neighbours, which is the reference's variance
+ * over nx.all_neighbors when the edge set is symmetric (helper.py:512-518 adds both
+ * directions). */
+typedef struct gtf_kl_graph {
+    int32_t n_nodes, n_slots;
+    const int32_t* slot_ptr;  /* [N+1] in-edge CSR (every slot an edge) */
+    const int32_t* slot_src;  /* [S] neighbour of each in-edge */
+    const double* gnn;        /* [N*4] GNN_Measurement x, y, z, r */
+    const int64_t* truth;     /* [N] truth_particle, or NULL */
+    const int64_t* pair_ptr;  /* [N+1] */
+    const int32_t* list[4];   /* nodes to process by in-degree bucket, any order within a bucket:
+                                 d in [1, 2] (one thread each), [3, 4], [5, 8] (4-, 8-lane groups) and d > 8
+                                 (one 64-lane wavefront each); d = 1 nodes yield states and
+                                 gradient moments but no pairs */
+    int32_t count[4];
+} gtf_kl_graph;
+
+enum { GTF_F64 = 0, GTF_F32 = 1 };
+
+typedef struct gtf_kl_out {
+    void* kl;          /* [P] double (GTF_F64) or float (GTF_F32) */
+    int8_t* truth;     /* [P] or NULL (needs graph truth) */
+    double* emp_var;   /* [N] or NULL; np.var of the gradients, written for the listed nodes */
+    double* emp_mean;  /* [N] or NULL; np.mean of the gradients (xy_edge_gradient_mean_var[0]) */
+    double* sv;        /* [S*3] edge_state_vector or NULL */
+    double* cov;       /* [S*9] edge_covariance (row-major) or NULL */
+    uint32_t* err;     /* device error word (GTF_ERR_SINGULAR_H) or NULL */
+} gtf_kl_out;
+
+/* dtype: GTF_F64 computes states and distances in fp64 (the reference's precision);
+ * GTF_F32 rotates/translates in fp64 and forms states and distances in fp32 (the
+ * config-5 tolerance sweep). sv/cov outputs are fp64 in both modes. */
+int gtf_parabolic_kl(const gtf_kl_graph* g, int32_t dtype, const gtf_kl_out* out, gtf_stream_t stream);
 
 const char* gtf_last_error(void);
 const char* gtf_version(void);

@@ -611,3 +611,44 @@ def parabolic_kl_pairs(svs, covs):
             trace = np.trace((covs[i] - covs[j]) * (inv[j] - inv[i]))
             out.append(trace + (svs[i] - svs[j]).T.dot(inv[i] + inv[j]).dot(svs[i] - svs[j]))
     return out
+
+
+def parabolic_training_rows(g: TrackGraph, truth=None):
+    """(kl_dist, emp_var, truth) rows of extract_metadata_trackml_parabolic_model.py:56-99
+    for every node with >= 2 in-edges (:61-62), pairs i > j in slot order per node.
+
+    States: utils.py:221-289 (parabolic_states above). emp_var: np.var of the
+    gradients dy/dx over nx.all_neighbors = predecessors then successors
+    (utils.py:240-254, :286), here the in-slot list then the out-list.
+    truth: 1 iff node, neighbour i and neighbour j share truth_particle (:82-95).
+    Returns (node, i, j, kl, emp_var, truth) arrays."""
+    gnn = g.node["gnn"]
+    src = g.slot["slot_src"]
+    dst = g.slot_dst()
+    rows = []
+    for v in range(g.n_nodes):
+        lo, hi = int(g.slot_ptr[v]), int(g.slot_ptr[v + 1])
+        d = hi - lo
+        if d <= 1:
+            continue
+        nb = list(src[lo:hi]) + list(dst[g.out_slot[g.out_ptr[v]:g.out_ptr[v + 1]]])
+        grads = [(gnn[v][1] - gnn[u][1]) / (gnn[v][0] - gnn[u][0]) for u in nb]
+        with np.errstate(all="ignore"):
+            emp_var = float(np.var(grads))
+        st = parabolic_states(gnn[v], gnn[src[lo:hi]])
+        kl = parabolic_kl_pairs([s for s, _ in st], [c for _, c in st])
+        t = 0
+        for i in range(d):
+            for j in range(i):
+                tr = 0
+                if truth is not None:
+                    tn, ti, tj = truth[v], truth[src[lo + i]], truth[src[lo + j]]
+                    tr = int(tn == ti and ti == tj and tn == tj)
+                rows.append((v, i, j, kl[t], emp_var, tr))
+                t += 1
+    if not rows:
+        z = np.zeros(0)
+        return z.astype(np.int64), z.astype(np.int64), z.astype(np.int64), z, z, z.astype(np.int8)
+    a = list(zip(*rows))
+    return (np.asarray(a[0], np.int64), np.asarray(a[1], np.int64), np.asarray(a[2], np.int64),
+            np.asarray(a[3], np.float64), np.asarray(a[4], np.float64), np.asarray(a[5], np.int8))

@@ -38,19 +38,18 @@ def test_library_loads_and_binds():
 
 
 def test_struct_layout_matches_header():
-    """compile a tiny C probe of offsetof() against the header and compare with ctypes"""
+    """compile a tiny C probe of offsetof()/sizeof() of every field of every struct
+    against the header and compare with the ctypes mirrors"""
     from gtf import _native as nat
-    probe = r'''
-#include <stdio.h>
-#include <stddef.h>
-#include "gtf.h"
-#define P(T, f) printf(#T "." #f " %zu\n", offsetof(T, f));
-int main(void) {
-  P(gtf_graph, slot_ptr) P(gtf_graph, slot_outpos) P(gtf_graph, layer) P(gtf_graph, sched) P(gtf_graph, n_g64)
-  P(gtf_nodes, degree) P(gtf_states, fresh) P(gtf_edges, send_mw) P(gtf_params, cluster_kl)
-  printf("sizeof.gtf_graph %zu\n", sizeof(gtf_graph));
-  return 0;
-}'''
+    py = {"gtf_graph": nat.GtfGraph, "gtf_nodes": nat.GtfNodes, "gtf_states": nat.GtfStates,
+          "gtf_edges": nat.GtfEdges, "gtf_params": nat.GtfParams, "gtf_kl_graph": nat.GtfKlGraph,
+          "gtf_kl_out": nat.GtfKlOut}
+    lines = []
+    for t, cls in py.items():
+        lines += ['  printf("%s.%s %%zu\\n", offsetof(%s, %s));' % (t, f, t, f) for f, _ in cls._fields_]
+        lines.append('  printf("sizeof.%s %%zu\\n", sizeof(%s));' % (t, t))
+    probe = "#include <stdio.h>\n#include <stddef.h>\n#include \"gtf.h\"\nint main(void) {\n%s\n  return 0;\n}\n" % \
+        "\n".join(lines)
     import tempfile
     with tempfile.TemporaryDirectory() as d:
         c = os.path.join(d, "p.c")
@@ -58,8 +57,7 @@ int main(void) {
         exe = os.path.join(d, "p")
         subprocess.check_call(["gcc", "-I", os.path.dirname(HDR), c, "-o", exe])
         got = dict(l.rsplit(" ", 1) for l in subprocess.check_output([exe], text=True).split("\n") if l)
-    py = {"gtf_graph": nat.GtfGraph, "gtf_nodes": nat.GtfNodes, "gtf_states": nat.GtfStates,
-          "gtf_edges": nat.GtfEdges, "gtf_params": nat.GtfParams}
+    assert len(got) == sum(len(c._fields_) + 1 for c in py.values())
     for k, v in got.items():
         t, f = k.split(".")
         if t == "sizeof":

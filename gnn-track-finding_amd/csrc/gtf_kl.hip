@@ -26,6 +26,7 @@
 #include <stdint.h>
 
 #include "../../include/gtf.h"
+#include "gtf_math.h"
 
 namespace gtf {
 void set_error(const char* msg);
@@ -116,12 +117,12 @@ struct KlStage {
 };
 
 template <typename T, typename St>
-__device__ __forceinline__ void put(volatile St* s, int i, const PState<T>& p) {
+__device__ __forceinline__ void put(St* s, int i, const PState<T>& p) {
     s->s0[i] = p.s0; s->s1[i] = p.s1; s->c00[i] = p.c00; s->c11[i] = p.c11;
     s->i00[i] = p.i00; s->i01[i] = p.i01; s->i11[i] = p.i11;
 }
 template <typename T, typename St>
-__device__ __forceinline__ PState<T> get(const volatile St* s, int i) {
+__device__ __forceinline__ PState<T> get(const St* s, int i) {
     return PState<T>{s->s0[i], s->s1[i], s->c00[i], s->c11[i], s->i00[i], s->i01[i], s->i11[i]};
 }
 
@@ -130,15 +131,6 @@ __device__ __forceinline__ double grp_sum(double x) {
 #pragma unroll
     for (int o = G / 2; o > 0; o >>= 1) x += __shfl_xor(x, o, G);
     return x;
-}
-
-// row i, column j of the row-major lower-triangle pair index t = i (i - 1) / 2 + j
-__device__ __forceinline__ void pair_ij(int t, int& i, int& j) {
-    int r = (int)((1.0f + sqrtf(1.0f + 8.0f * (float)t)) * 0.5f);
-    while (r * (r - 1) / 2 > t) r--;
-    while ((r + 1) * r / 2 <= t) r++;
-    i = r;
-    j = t - r * (r - 1) / 2;
 }
 
 // group sizes of the four degree buckets of gtf_kl_graph.list (d <= 2, <= 4, <= 8, > 8)
@@ -157,7 +149,7 @@ __device__ __forceinline__ void pkl_node(const gtf_kl_graph& g, const gtf_kl_out
     const int v = list[gi];
     const int lo = g.slot_ptr[v], d = g.slot_ptr[v + 1] - lo;
     if (d < 1) return;
-    volatile Stage* stg = (volatile Stage*)smem + (int)threadIdx.x / G;
+    Stage* stg = (Stage*)smem + (int)threadIdx.x / G;
     const Frame f = node_frame(g.gnn, v);
 
     // states of the node's in-edges and the gradients dy/dx (utils.py:249-254, 273-283)
@@ -197,7 +189,7 @@ __device__ __forceinline__ void pkl_node(const gtf_kl_graph& g, const gtf_kl_out
             if (o.emp_mean) o.emp_mean[v] = mean;
         }
     }
-    __builtin_amdgcn_wave_barrier();
+    gtf::wave_lds_sync();
 
     // pairs i > j, row-major, round-robin over the lanes: consecutive lanes write
     // consecutive distances (calc_pairwise_distances, :19-25)
@@ -207,7 +199,7 @@ __device__ __forceinline__ void pkl_node(const gtf_kl_graph& g, const gtf_kl_out
     T* kl = (T*)o.kl;
     for (int t = gl; t < np; t += G) {
         int i, j;
-        pair_ij(t, i, j);
+        gtf::pair_ij(t, i, j);
         PState<T> a, b;
         long long ti = 0, tj = 0;
         if (d <= G) {
@@ -281,14 +273,25 @@ __global__ void __launch_bounds__(BLOCK) KL_ATTR k_parabolic_kl(gtf_kl_graph g, 
     __shared__ __attribute__((aligned(16))) char smem[stage_bytes(4, sizeof(T)) > stage_bytes(64, sizeof(T))
                                                           ? stage_bytes(4, sizeof(T))
                                                           : stage_bytes(64, sizeof(T))];
+    // bucket block ranges are multiples of 8, each remapped XCD-contiguous on its own:
+    // neighbouring nodes (one event's hits) share an L2
     int b = blockIdx.x;
-    if (b < bk.blocks[3]) { pkl_node<T, 64, STATES>(g, o, g.list[3], g.count[3], b, smem); return; }
+    if (b < bk.blocks[3]) {
+        pkl_node<T, 64, STATES>(g, o, g.list[3], g.count[3], gtf::xcd_local(b, bk.blocks[3]), smem);
+        return;
+    }
     b -= bk.blocks[3];
-    if (b < bk.blocks[2]) { pkl_node<T, 8, STATES>(g, o, g.list[2], g.count[2], b, smem); return; }
+    if (b < bk.blocks[2]) {
+        pkl_node<T, 8, STATES>(g, o, g.list[2], g.count[2], gtf::xcd_local(b, bk.blocks[2]), smem);
+        return;
+    }
     b -= bk.blocks[2];
-    if (b < bk.blocks[1]) { pkl_node<T, 4, STATES>(g, o, g.list[1], g.count[1], b, smem); return; }
+    if (b < bk.blocks[1]) {
+        pkl_node<T, 4, STATES>(g, o, g.list[1], g.count[1], gtf::xcd_local(b, bk.blocks[1]), smem);
+        return;
+    }
     b -= bk.blocks[1];
-    pkl_node1<T, STATES>(g, o, g.list[0], g.count[0], b);
+    pkl_node1<T, STATES>(g, o, g.list[0], g.count[0], gtf::xcd_local(b, bk.blocks[0]));
 }
 
 template <typename T>
@@ -296,7 +299,7 @@ int launch(const gtf_kl_graph* g, const gtf_kl_out* o, hipStream_t st) {
     KlBuckets bk;
     int total = 0;
     for (int i = 0; i < 4; i++) {
-        bk.blocks[i] = (g->count[i] + BLOCK / BG[i] - 1) / (BLOCK / BG[i]);
+        bk.blocks[i] = gtf::pad8((g->count[i] + BLOCK / BG[i] - 1) / (BLOCK / BG[i]));
         total += bk.blocks[i];
     }
     if (total > 0) {

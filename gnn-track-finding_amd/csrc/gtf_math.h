@@ -13,6 +13,40 @@
 
 namespace gtf {
 
+// XCD-aware block index. MI355X deals workgroups round-robin over its 8 XCDs, each with
+// its own 4 MiB L2 (MI355X_MICROARCH.md, workgroup dispatch), so consecutive blocks --
+// which gather the same nodes' data -- would fill eight L2s with the same lines. This
+// bijective remap (cdna_hip_programming.md T1) gives the blocks that share an XCD one
+// contiguous range of work instead. `b` indexes a range of n blocks that starts at a
+// multiple of 8 in the grid; speed only, never correctness.
+__device__ __forceinline__ int xcd_local(int b, int n) {
+    const int q = n / 8, r = n % 8, x = b % 8;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+__host__ __device__ __forceinline__ int pad8(int n) { return (n + 7) & ~7; }
+
+// Lanes of ONE wavefront hand values to each other through LDS. A wave's LDS
+// instructions execute in issue order, so only the compiler has to be kept from
+// moving loads above the other lanes' stores: wavefront-scope fences around a
+// wave barrier. (Plain, not volatile, LDS pointers: a volatile access makes the
+// compiler wait for each LDS load on its own instead of batching them.)
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// row i and column j of lower-triangle pair t in row-major order
+// ((1,0) (2,0) (2,1) (3,0) ...): t = i (i - 1) / 2 + j. Arithmetic, not a table: a
+// lane-varying index into a __constant__ table is a vector memory load per pair.
+__device__ __forceinline__ void pair_ij(int t, int& i, int& j) {
+    int r = (int)((1.0f + sqrtf(1.0f + 8.0f * (float)t)) * 0.5f);
+    while (r * (r - 1) / 2 > t) r--;
+    while ((r + 1) * r / 2 <= t) r++;
+    i = r;
+    j = t - r * (r - 1) / 2;
+}
+
 struct Cov5 {
     double c00, c01, c10, c11, c22;
 };

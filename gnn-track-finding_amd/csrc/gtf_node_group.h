@@ -16,6 +16,10 @@
 // active at each shuffle.
 #pragma once
 
+#ifndef GTF_ABLATE
+#define GTF_ABLATE 0  // diagnostics builds only (tools/ablate_build.sh)
+#endif
+
 template <int G>
 struct Grp {
     int gl;     // lane within the group
@@ -117,15 +121,15 @@ __device__ __forceinline__ int dict_pos(const NodeCtx<G>& c, LaneDict& st) {
 // every lane adds the line in order; skipped entries add +0.0, which leaves the
 // running sum unchanged (it starts from the integer 0 of helper.py:165).
 template <int G>
-__device__ __forceinline__ double ordered_sum(NodeCtx<G>& c, volatile double* sval, LaneDict& st, bool take,
+__device__ __forceinline__ double ordered_sum(NodeCtx<G>& c, double* sval, LaneDict& st, bool take,
                                              double term) {
     const int pos = dict_pos(c, st);
     const int npres = c.grp.count(c.valid && st.rank >= 0);
     if (pos >= 0) sval[c.grp.gbase + pos] = take ? term : 0.0;
-    __builtin_amdgcn_wave_barrier();
+    wave_lds_sync();
     double s = 0.0;
     for (int i = 0; i < npres; i++) s = s + sval[c.grp.gbase + i];
-    __builtin_amdgcn_wave_barrier();
+    wave_lds_sync();
     return s;
 }
 
@@ -163,7 +167,7 @@ __device__ __forceinline__ void g_priors(NodeCtx<G>& c, LaneDict& st) {
 
 // calculate_side_norm_factor + reweight (helper.py:99-200), UTS only
 template <int G>
-__device__ __forceinline__ void g_reweight(NodeCtx<G>& c, volatile double* sval, const double* gnn, double thr,
+__device__ __forceinline__ void g_reweight(NodeCtx<G>& c, double* sval, const double* gnn, double thr,
                                            uint32_t* err) {
     LaneDict& st = c.uts;
     const bool act = lane_active(c, st.rank);
@@ -260,18 +264,6 @@ __device__ __forceinline__ void g_ranks(NodeCtx<G>& c) {
     st.pos_ok = false;
 }
 
-// lower-triangle pair t (row-major: (1,0) (2,0) (2,1) (3,0) ...) for d <= 15
-__constant__ uint8_t c_pair_i[105] = {
-    1, 2, 2, 3, 3, 3, 4, 4, 4, 4, 5, 5, 5, 5, 5, 6, 6, 6, 6, 6, 6, 7, 7, 7, 7, 7, 7, 7,
-    8, 8, 8, 8, 8, 8, 8, 8, 9, 9, 9, 9, 9, 9, 9, 9, 9, 10, 10, 10, 10, 10, 10, 10, 10, 10, 10,
-    11, 11, 11, 11, 11, 11, 11, 11, 11, 11, 11, 12, 12, 12, 12, 12, 12, 12, 12, 12, 12, 12, 12,
-    13, 13, 13, 13, 13, 13, 13, 13, 13, 13, 13, 13, 13, 14, 14, 14, 14, 14, 14, 14, 14, 14, 14, 14, 14, 14, 14};
-__constant__ uint8_t c_pair_j[105] = {
-    0, 0, 1, 0, 1, 2, 0, 1, 2, 3, 0, 1, 2, 3, 4, 0, 1, 2, 3, 4, 5, 0, 1, 2, 3, 4, 5, 6,
-    0, 1, 2, 3, 4, 5, 6, 7, 0, 1, 2, 3, 4, 5, 6, 7, 8, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9,
-    0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11,
-    0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13};
-
 // per-group LDS staging of up to 15 states (structure of arrays): the state, its
 // covariance and inverse (computed once per state: np.linalg.inv of a state's
 // covariance is the same value every time the reference recomputes it), and the
@@ -285,15 +277,15 @@ struct StageT {
 };
 
 template <typename Stage>
-__device__ __forceinline__ Cov5 stage_cov(const volatile Stage* s, int i) {
+__device__ __forceinline__ Cov5 stage_cov(const Stage* s, int i) {
     return Cov5{s->c00[i], s->c01[i], s->c10[i], s->c11[i], s->c22[i]};
 }
 template <typename Stage>
-__device__ __forceinline__ Cov5 stage_inv(const volatile Stage* s, int i) {
+__device__ __forceinline__ Cov5 stage_inv(const Stage* s, int i) {
     return Cov5{s->i00[i], s->i01[i], s->i10[i], s->i11[i], s->i22[i]};
 }
 template <typename Stage>
-__device__ __forceinline__ TauGeo stage_geo(const volatile Stage* s, int i) {
+__device__ __forceinline__ TauGeo stage_geo(const Stage* s, int i) {
     TauGeo t;
     t.q = s->q[i]; t.w = s->w[i]; t.tau = s->tg[i]; t.sz2 = s->sz2[i]; t.sr2 = s->sr2[i];
     return t;
@@ -306,8 +298,11 @@ __device__ __forceinline__ TauGeo stage_geo(const volatile Stage* s, int i) {
 // (I1 + I2)^-1 serves both means.
 template <int G, typename Stage>
 __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf_states& S, LaneDict& st,
-                                          volatile Stage* stg, const double* xyzr_node, double chi2_thr,
+                                          Stage* stg, const double* xyzr_node, double chi2_thr,
                                           double kl_thr, const gtf_params& p, uint32_t* err) {
+#if GTF_ABLATE == 1
+    return;  // diagnostics build (tools/ablate_build.sh): no clustering work
+#endif
     const bool pres = c.valid && st.rank >= 0;
     const int d = c.grp.count(pres);
     if (d <= 2 || d >= 16) return;                                                 // :207
@@ -331,7 +326,7 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
         stg->q[pos] = t.q; stg->w[pos] = t.w; stg->tg[pos] = t.tau; stg->sz2[pos] = t.sz2; stg->sr2[pos] = t.sr2;
         stg->prior[pos] = st.prior;
     }
-    __builtin_amdgcn_wave_barrier();
+    wave_lds_sync();
     const bool ec = fabs(xa) >= p.endcap_boundary;
     const double sza = ec ? p.sigma0rz : p.sigma0rz2, sra = ec ? p.sigma0rz2 : p.sigma0rz;
     const double sza2 = sza * sza, sra2 = sra * sra;
@@ -341,7 +336,8 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
     unsigned lmask = 0;
     bool lnan = false, lnz = false;
     for (int t = c.grp.gl; t < npairs; t += G) {
-        const int i = c_pair_i[t], j = c_pair_j[t];
+        int i, j;
+        pair_ij(t, i, j);
         const double D = mahalanobis_geo(stg->a[i], stg->b[i], stage_cov(stg, i), stg->a[j], stg->b[j],
                                          stage_cov(stg, j), sza2, sra2, stage_geo(stg, i), stage_geo(stg, j));
         if (D == 0.0) continue;  // zeros are excluded (np.nonzero)
@@ -359,15 +355,20 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
         return;
     }
     if (c.grp.any(lnan)) return;                       // np.min over a NaN -> no merge (:228)
+#if GTF_ABLATE == 2
+    if (c.grp.min_d(lmin) > -1.0) return;  // diagnostics build: staging + pair distances only
+#endif
     const double best = c.grp.min_d(lmin);
     if (!(best < chi2_thr)) return;
     const bool tl = lmin == best;
     const int t0 = c.grp.min_i(tl ? lt0 : (1 << 20));
     const int t1 = c.grp.min_i(tl ? (lt0 == t0 ? lt1 : lt0) : (1 << 20));
     const unsigned tiemask = c.grp.or_u(tl ? lmask : 0u);
-    const int ti0 = c_pair_i[t0], tj0 = c_pair_j[t0];
+    int ti0, tj0, ti1 = 0, tj1;
+    pair_ij(t0, ti0, tj0);
+    if (t1 < (1 << 20)) pair_ij(t1, ti1, tj1);
     // merged pair = (idx[0], idx[1]) of concatenate((rows, cols)) (:231-233)
-    const int p0 = ti0, p1 = (t1 < (1 << 20)) ? (int)c_pair_i[t1] : tj0;
+    const int p0 = ti0, p1 = (t1 < (1 << 20)) ? ti1 : tj0;
     double pm[3], jm[3];
     Cov5 mc;
     {
@@ -385,7 +386,7 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
     if (alive == 0) {
         if (c.grp.gl == 0) atomicOr(err, (uint32_t)GTF_ERR_TIE_EMPTIED);
     } else {
-        while (true) {                                                             // :251-287
+        while (GTF_ABLATE != 3) {                                                  // :251-287
             const Cov5 im = inv_cov5(mc);   // the merged state's inverse, shared by KL and the next merge
             const bool me = pres && (alive >> pos & 1u);
             double D = INFINITY;
@@ -417,7 +418,7 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
             if (alive == 0) break;
         }
     }
-    __builtin_amdgcn_wave_barrier();
+    wave_lds_sync();
     if (c.grp.gl == 0) {                                                           // :291-293
         n.has_merged[c.v] = 1;
         n.merged_state[3 * (int64_t)c.v + 0] = pm[0];
@@ -489,8 +490,8 @@ __device__ __forceinline__ void node_store(NodeCtx<G>& c, gtf_nodes& n, gtf_stat
 
 template <int G, int OP, typename Stage>
 __device__ __forceinline__ void node_op(NodeCtx<G>& c, const gtf_graph& g, gtf_nodes& n, gtf_states& tse,
-                                        gtf_states& uts, const gtf_params& p, const Ws& w, volatile double* sval,
-                                        volatile Stage* stg, double chi2_thr, double kl_thr, bool has_tse,
+                                        gtf_states& uts, const gtf_params& p, const Ws& w, double* sval,
+                                        Stage* stg, double chi2_thr, double kl_thr, bool has_tse,
                                         bool has_uts) {
     if constexpr (OP == OP_RANKS) g_ranks(c);
     if constexpr (OP == OP_PRIORS_TSE) { if (has_tse) g_priors(c, c.tse); }
@@ -529,8 +530,8 @@ __device__ __forceinline__ void node_seq_body(const gtf_graph& g, gtf_nodes& n, 
     NodeCtx<G> c;
     const int gi = (bid * BLOCK + (int)threadIdx.x) / G;
     if (!node_load(c, g, n, tse, uts, e, list, count, gi, Q::uses_tse, Q::uses_uts)) return;
-    volatile double* sval = (volatile double*)smem + (threadIdx.x & ~63);
-    volatile Stage* stg = (volatile Stage*)(smem + BLOCK * sizeof(double)) + (Q::cluster ? (int)threadIdx.x / G : 0);
+    double* sval = (double*)smem + (threadIdx.x & ~63);
+    Stage* stg = (Stage*)(smem + BLOCK * sizeof(double)) + (Q::cluster ? (int)threadIdx.x / G : 0);
     const bool has_tse = n.has_tse[c.v], has_uts = n.has_uts[c.v];
     (node_op<G, OPS, Stage>(c, g, n, tse, uts, p, w, sval, stg, chi2_thr, kl_thr, has_tse, has_uts), ...);
     node_store(c, n, tse, uts, e);
@@ -559,19 +560,26 @@ __global__ void __launch_bounds__(BLOCK) k_node_multi(gtf_graph g, gtf_nodes n, 
                                                       double kl_thr, Buckets bk) {
     using Q = OpSeq<OPS...>;
     __shared__ __attribute__((aligned(16))) char smem[Q::cluster ? node_smem_bytes() : BLOCK * sizeof(double)];
+    // Blocks stay in dispatch order (round-robin over the XCDs): per-node cost varies
+    // with the node's state count and clustering work, and an XCD-contiguous remap
+    // (gtf::xcd_local) made this kernel 35 % slower on config 4, presumably by putting
+    // the costly nodes of a node range on one XCD.
     int b = blockIdx.x;
     if (b < bk.blocks[0]) {
-        node_seq_body<64, OPS...>(g, n, tse, uts, e, p, w, chi2_thr, kl_thr, bk.list[0], bk.count[0], b, smem);
+        node_seq_body<64, OPS...>(g, n, tse, uts, e, p, w, chi2_thr, kl_thr, bk.list[0], bk.count[0], b,
+                                  smem);
         return;
     }
     b -= bk.blocks[0];
     if (b < bk.blocks[1]) {
-        node_seq_body<32, OPS...>(g, n, tse, uts, e, p, w, chi2_thr, kl_thr, bk.list[1], bk.count[1], b, smem);
+        node_seq_body<32, OPS...>(g, n, tse, uts, e, p, w, chi2_thr, kl_thr, bk.list[1], bk.count[1], b,
+                                  smem);
         return;
     }
     b -= bk.blocks[1];
     if (b < bk.blocks[2]) {
-        node_seq_body<16, OPS...>(g, n, tse, uts, e, p, w, chi2_thr, kl_thr, bk.list[2], bk.count[2], b, smem);
+        node_seq_body<16, OPS...>(g, n, tse, uts, e, p, w, chi2_thr, kl_thr, bk.list[2], bk.count[2], b,
+                                  smem);
         return;
     }
     b -= bk.blocks[2];
@@ -585,13 +593,13 @@ __global__ void __launch_bounds__(BLOCK) k_node_group(gtf_graph g, gtf_nodes n, 
                                                       double chi2_thr, double kl_thr, const int32_t* list,
                                                       int count) {
     using Stage = StageT<(G < 16 ? G : 16)>;
-    __shared__ volatile double s_val[BLOCK];
-    __shared__ volatile Stage s_stage[BLOCK / G];
+    __shared__ double s_val[BLOCK];
+    __shared__ Stage s_stage[BLOCK / G];
     NodeCtx<G> c;
     const int gi = (blockIdx.x * BLOCK + (int)threadIdx.x) / G;
     if (!node_load(c, g, n, tse, uts, e, list, count, gi, ops.uses_tse, ops.uses_uts)) return;
-    volatile double* sval = s_val + (threadIdx.x & ~63);
-    volatile Stage* stg = s_stage + (int)threadIdx.x / G;
+    double* sval = s_val + (threadIdx.x & ~63);
+    Stage* stg = s_stage + (int)threadIdx.x / G;
     const bool has_tse = n.has_tse[c.v], has_uts = n.has_uts[c.v];
     for (int i = 0; i < ops.n; i++) {
         switch (ops.op[i]) {

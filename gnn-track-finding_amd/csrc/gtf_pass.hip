@@ -92,7 +92,7 @@ __device__ __forceinline__ double highland_var_ms(double a, double b, const doub
 // ---------------------------------------------------------------------------
 constexpr int SG = 8;
 __global__ void __launch_bounds__(BLOCK) k_sender(gtf_graph g, gtf_nodes n, gtf_edges e, gtf_params p, Ws w) {
-    const int u = (blockIdx.x * BLOCK + (int)threadIdx.x) / SG;
+    const int u = (xcd_local(blockIdx.x, gridDim.x) * BLOCK + (int)threadIdx.x) / SG;
     const int gl = threadIdx.x & (SG - 1);
     if (u >= g.n_nodes || !n.has_merged[u]) return;  // group-uniform
     const int ob = g.out_ptr[u], oe = g.out_ptr[u + 1];
@@ -125,7 +125,7 @@ __global__ void __launch_bounds__(BLOCK) k_sender(gtf_graph g, gtf_nodes n, gtf_
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(BLOCK) k_extrapolate(gtf_graph g, gtf_nodes n, gtf_states uts, gtf_edges e,
                                                        gtf_params p, Ws w) {
-    const int k = blockIdx.x * BLOCK + threadIdx.x;
+    const int k = xcd_local(blockIdx.x, gridDim.x) * BLOCK + threadIdx.x;
     if (k >= g.n_slots) return;
     uts.fresh[k] = 0;
     if (!g.is_edge[k]) return;

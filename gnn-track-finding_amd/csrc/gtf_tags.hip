@@ -8,6 +8,7 @@
 #include <stdint.h>
 
 #include "../../include/gtf.h"
+#include "gtf_math.h"
 
 namespace {
 constexpr int BLOCK = 256;
@@ -15,7 +16,7 @@ constexpr int BLOCK = 256;
 // keep[e] = neighbour radius <= node radius (:99-110); processed[u] = any kept (:109-110)
 __global__ void __launch_bounds__(BLOCK) k_tag_prepare(gtf_graph g, const double* radius, uint8_t* keep,
                                                        uint8_t* processed, int32_t* n_processed) {
-    const int u = blockIdx.x * BLOCK + threadIdx.x;
+    const int u = gtf::xcd_local(blockIdx.x, gridDim.x) * BLOCK + threadIdx.x;
     int mine = 0;
     if (u < g.n_nodes) {
         const double ru = radius[u];
@@ -36,7 +37,7 @@ __global__ void __launch_bounds__(BLOCK) k_tag_prepare(gtf_graph g, const double
 // tags_out[u] = max(tags_in[u], tags_in[kept successors]) (:141-150 -- max, not min)
 __global__ void __launch_bounds__(BLOCK) k_tag_sweep(gtf_graph g, const uint8_t* keep, const uint8_t* processed,
                                                      const int64_t* tin, int64_t* tout, int32_t* flips) {
-    const int u = blockIdx.x * BLOCK + threadIdx.x;
+    const int u = gtf::xcd_local(blockIdx.x, gridDim.x) * BLOCK + threadIdx.x;
     int flipped = 0;
     if (u < g.n_nodes) {
         const int64_t t0 = tin[u];

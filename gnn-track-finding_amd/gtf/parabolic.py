@@ -84,11 +84,14 @@ class ParabolicKL:
 
     def alloc(self, dtype="f64", truth=True, emp=True, states=False):
         f = torch.float64 if dtype == "f64" else torch.float32
-        # never a null pointer, even with no pairs (the C-ABI rejects null outputs)
-        z = lambda n, dt: torch.empty(max(n, 1), dtype=dt, device=self.device)[:n]  # noqa: E731
-        out = {"kl": z(self.n_pairs, f)}
+        # pair buffers hold >= 1 element so their pointers are never null, even with no
+        # pairs (the C-ABI rejects null outputs); "kl"/"truth" are views of the pair count
+        z = lambda n, dt: torch.empty(max(n, 1), dtype=dt, device=self.device)  # noqa: E731
+        out = {"_kl": z(self.n_pairs, f)}
+        out["kl"] = out["_kl"][:self.n_pairs]
         if truth and self.truth is not None:
-            out["truth"] = z(self.n_pairs, torch.int8)
+            out["_truth"] = z(self.n_pairs, torch.int8)
+            out["truth"] = out["_truth"][:self.n_pairs]
         if emp:     # True: gradient mean and variance; "var": variance only (the training rows)
             out["emp_var"] = torch.full((self.n_nodes,), float("nan"), dtype=torch.float64, device=self.device)
             if emp is True:
@@ -101,7 +104,7 @@ class ParabolicKL:
 
     def run(self, out, dtype="f64", stream=None):
         """launch gtf_parabolic_kl into the buffers of ``alloc`` (stream-ordered)."""
-        o = nat.GtfKlOut(_ptr(out["kl"]), _ptr(out.get("truth")), _ptr(out.get("emp_var")),
+        o = nat.GtfKlOut(_ptr(out["_kl"]), _ptr(out.get("_truth")), _ptr(out.get("emp_var")),
                          _ptr(out.get("emp_mean")), _ptr(out.get("sv")), _ptr(out.get("cov")), _ptr(self.err))
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
         nat.check(nat.lib().gtf_parabolic_kl(ctypes.byref(self._g), nat.GTF_F64 if dtype == "f64" else nat.GTF_F32,

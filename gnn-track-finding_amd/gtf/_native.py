@@ -42,6 +42,11 @@ class GtfParams(ctypes.Structure):
                 ("chi2_cut", F64), ("reweight_threshold", F64), ("cluster_chi2", F64), ("cluster_kl", F64)]
 
 
+class GtfTseExtra(ctypes.Structure):
+    _fields_ = [("theta", P), ("var_ms", P), ("xy_mean_var", P), ("zr_mean_var", P), ("angle", P),
+                ("translation", P)]
+
+
 class GtfKlGraph(ctypes.Structure):
     _fields_ = [("n_nodes", I32), ("n_slots", I32), ("slot_ptr", P), ("slot_src", P), ("gnn", P), ("truth", P),
                 ("pair_ptr", P), ("list", P * 4), ("count", I32 * 4)]
@@ -67,7 +72,7 @@ ERR_FLAGS = {
 # exported symbols (must match include/gtf.h; tests check the .so exports all of them)
 SYMBOLS = ["gtf_workspace_bytes", "gtf_clear_errors", "gtf_read_errors", "gtf_extrapolate", "gtf_update",
            "gtf_message_passing", "gtf_node_ops",
-           "gtf_cluster", "gtf_pass", "gtf_pass_ev", "gtf_tag_prepare", "gtf_tag_sweep", "gtf_parabolic_kl", "gtf_last_error",
+           "gtf_cluster", "gtf_pass", "gtf_pass_ev", "gtf_tag_prepare", "gtf_tag_sweep", "gtf_parabolic_kl", "gtf_track_state_estimates", "gtf_last_error",
            "gtf_version"]
 
 OPS = {"ranks": 1, "priors_tse": 2, "priors_uts": 3, "reweight_uts": 4, "degree": 5, "prune": 6, "mw_tse": 7,
@@ -100,12 +105,13 @@ def lib():
     L.gtf_pass_ev.argtypes = [G, N, S, S, E, PR, P, P, ctypes.POINTER(P)]
     L.gtf_tag_prepare.argtypes = [G, P, P, P, P, P]
     L.gtf_tag_sweep.argtypes = [G, P, P, P, P, P, P]
+    L.gtf_track_state_estimates.argtypes = [G, S, ctypes.POINTER(GtfTseExtra), PR, P]
     L.gtf_parabolic_kl.argtypes = [ctypes.POINTER(GtfKlGraph), I32, ctypes.POINTER(GtfKlOut), P]
     L.gtf_last_error.restype = ctypes.c_char_p
     L.gtf_version.restype = ctypes.c_char_p
     for fn in ("gtf_clear_errors", "gtf_read_errors", "gtf_extrapolate", "gtf_update", "gtf_cluster", "gtf_pass",
                "gtf_pass_ev", "gtf_message_passing", "gtf_node_ops",
-               "gtf_tag_prepare", "gtf_tag_sweep", "gtf_parabolic_kl"):
+               "gtf_tag_prepare", "gtf_tag_sweep", "gtf_parabolic_kl", "gtf_track_state_estimates"):
         getattr(L, fn).restype = ctypes.c_int
     _lib = L
     return L

@@ -67,7 +67,8 @@ class DeviceGraph:
         buckets = [idx[(deg >= lo) & (deg <= hi)] for lo, hi in edges]
         rest = idx[deg > 64]
         up("sched", np.concatenate(buckets + [rest]).astype(np.int32))
-        self.n_g = [int(b.size) for b in buckets] if schedule else [0, 0, 0, 0]
+        self.n_g_all = [int(b.size) for b in buckets]
+        self.n_g = self.n_g_all if schedule else [0, 0, 0, 0]
         self.use_sched = schedule
         for f in ("gnn", "xyzr", "layer") + MUTABLE_NODE:
             up(f, g.node[f])
@@ -115,6 +116,10 @@ class DeviceGraph:
                                p("slot_dst"), p("out_ptr"), p("out_slot"), p("slot_outpos"), p("is_edge"), p("rev_edge"), p("solo"),
                                p("gnn"), p("xyzr"), p("layer"),
                                p("sched") if self.use_sched else ctypes.c_void_p(0), *self.n_g)
+        self.cg_sched = nat.GtfGraph(self.n_nodes, self.n_slots, self.n_edges, 0, p("slot_ptr"), p("slot_src"),
+                                     p("slot_dst"), p("out_ptr"), p("out_slot"), p("slot_outpos"), p("is_edge"),
+                                     p("rev_edge"), p("solo"), p("gnn"), p("xyzr"), p("layer"), p("sched"),
+                                     *self.n_g_all)
         self.cn = nat.GtfNodes(*[p(f) for f in MUTABLE_NODE])
         self.cuts = nat.GtfStates(p("uts_rank"), p("uts_sv"), p("uts_tau"), p("uts_cov"), p("uts_xyzr"),
                                   p("uts_lik"), p("uts_mw"), p("uts_prior"), p("uts_lr"), p("uts_side"),
@@ -194,6 +199,27 @@ class DeviceGraph:
             nat.check(self.lib.gtf_pass_ev(ctypes.byref(self.cg), ctypes.byref(self.cn), ctypes.byref(self.ctse),
                                            ctypes.byref(self.cuts), ctypes.byref(self.ce), ctypes.byref(cp),
                                            self.ptr("ws"), self.stream, arr))
+
+    def track_state_estimates(self, p: Params):
+        """helper.compute_track_state_estimates (helper.py:238-452) for every key of the
+        nodes' track_state_estimates dicts (tse_rank >= 0, dict order as given): writes
+        tse_sv / tse_cov / tse_tau / tse_xyzr / tse_theta / tse_var_ms on the device and
+        returns the per-node attributes (xy/zr_edge_gradient_mean_var,
+        angle_of_rotation, translation) as device tensors."""
+        torch = self.torch
+        N = self.n_nodes
+        nan = float("nan")
+        x = {"xy_mean_var": torch.full((N, 2), nan, dtype=torch.float64, device=self.device),
+             "zr_mean_var": torch.full((N, 2), nan, dtype=torch.float64, device=self.device),
+             "angle_of_rotation": torch.full((N,), nan, dtype=torch.float64, device=self.device),
+             "translation": torch.full((N, 2), nan, dtype=torch.float64, device=self.device)}
+        vp = lambda t: ctypes.c_void_p(t.data_ptr() if t.numel() else 0)  # noqa: E731
+        ex = nat.GtfTseExtra(self.ptr("tse_theta"), self.ptr("tse_var_ms"), vp(x["xy_mean_var"]),
+                             vp(x["zr_mean_var"]), vp(x["angle_of_rotation"]), vp(x["translation"]))
+        cp = self.cparams(p)
+        nat.check(self.lib.gtf_track_state_estimates(ctypes.byref(self.cg_sched), ctypes.byref(self.ctse),
+                                                     ctypes.byref(ex), ctypes.byref(cp), self.stream))
+        return x
 
     # ------------------------------------------------------- tag propagation
     def tag_propagation(self, tags, radius, threshold=0.1, max_sweeps=100000):

@@ -179,6 +179,27 @@ int gtf_tag_prepare(const gtf_graph* g, const double* radius, uint8_t* keep, uin
 int gtf_tag_sweep(const gtf_graph* g, const uint8_t* keep, const uint8_t* processed,
                   const int64_t* tags_in, int64_t* tags_out, int32_t* flips, gtf_stream_t stream);
 
+/* ---- Initial track-state estimates -----------------------------
+ * helper.compute_track_state_estimates (helper.py:238-452): for every key of every
+ * node's track_state_estimates dict (slots with tse->rank >= 0; the dict order is an
+ * input, the reference's reversed(set(nx.all_neighbors)) order) writes tse->sv
+ * (edge_state_vector), tse->cov (the aliased edge/joint covariance, :417-425),
+ * tse->tau (joint_vector[2]) and tse->xyzr (neighbour coordinates), plus the optional
+ * per-slot / per-node extras below. Needs g->sched (the slot-count node schedule).
+ * The reference reads its set-ordered tau / del_tau / theta lists with dict positions
+ * (:384, :419-431); that pairing is reproduced. */
+typedef struct gtf_tse_extra {
+    double* theta;        /* [S*3] theta, theta2, variance_theta, or NULL */
+    double* var_ms;       /* [S]   var_ms_node, or NULL */
+    double* xy_mean_var;  /* [N*2] xy_edge_gradient_mean_var, or NULL */
+    double* zr_mean_var;  /* [N*2] zr_edge_gradient_mean_var, or NULL */
+    double* angle;        /* [N]   angle_of_rotation, or NULL */
+    double* translation;  /* [N*2] translation, or NULL */
+} gtf_tse_extra;
+
+int gtf_track_state_estimates(const gtf_graph* g, gtf_states* tse, const gtf_tse_extra* extra,
+                              const gtf_params* p, gtf_stream_t stream);
+
 /* ---- Parabolic-model KL training data -------------------------
  * learn_KL_parabolic_model/src/generate_training_data: the per-edge parabolic
  * state of compute_track_state_estimates (utils.py:221-289; S = diag(16, 0.01,

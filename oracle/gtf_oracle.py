@@ -652,3 +652,84 @@ def parabolic_training_rows(g: TrackGraph, truth=None):
     a = list(zip(*rows))
     return (np.asarray(a[0], np.int64), np.asarray(a[1], np.int64), np.asarray(a[2], np.int64),
             np.asarray(a[3], np.float64), np.asarray(a[4], np.float64), np.asarray(a[5], np.int8))
+
+
+def compute_track_state_estimates(g: TrackGraph, p):
+    """helper.compute_track_state_estimates (helper.py:238-452) on the packed layout.
+
+    The dict order of each node's track_state_estimates is the INPUT ``tse_rank``
+    (the reference's reversed(set(nx.all_neighbors)) order); the
+    set order is its reverse. Writes tse_sv, tse_cov (aliased, :417-425), tse_tau,
+    tse_xyzr, tse_theta (theta, theta2, variance_theta), tse_var_ms per slot and
+    returns the node arrays (xy_mean_var, zr_mean_var, angle_of_rotation,
+    translation). The per-neighbour lists gradients_zr / del_tau / theta are
+    filled in set order but read with the dict-order index (:384, :419-431) --
+    reproduced as is."""
+    S = np.array([[4.0**2, 0, 0], [0, p.sigma0xy**2, 0], [0, 0, p.sigma0xy**2]])
+    gnn = g.node["gnn"]
+    N = g.n_nodes
+    xy_mv = np.full((N, 2), np.nan)
+    zr_mv = np.full((N, 2), np.nan)
+    ang = np.full(N, np.nan)
+    trans = np.full((N, 2), np.nan)
+    sl = g.slot
+    for v in range(N):
+        dict_order = _dict_order(g, "tse", v)
+        set_order = dict_order[::-1]
+        xA, yA, zA, rA = gnn[v]
+        sigma_r, sigma_z = p.sigma0rz, p.sigma0rz2                                    # :269-274
+        if np.abs(zA) >= p.endcap_boundary:
+            sigma_z, sigma_r = p.sigma0rz, p.sigma0rz2
+        gxy, gzr, del_tau, th, th2, del_th = [], [], [], [], [], []
+        for k in set_order:                                                          # :277-338
+            u = sl["slot_src"][k]
+            x2, y2, z2, r2 = gnn[u]
+            gxy.append((y2 - yA) / (x2 - xA))
+            r1, z1 = rA, zA
+            gzr.append((z2 - z1) / (r2 - r1))
+            szn, srn = p.sigma0rz2, p.sigma0rz
+            if np.abs(z2) >= p.endcap_boundary:
+                szn, srn = p.sigma0rz, p.sigma0rz2
+            J = np.array([1 / (r1 - r2), -1 / (r1 - r2), -(z1 - z2) / (r1 - r2)**2, (z1 - z2) / (r1 - r2)**2])
+            S2 = np.diag([sigma_z**2, szn**2, sigma_r**2, srn**2])
+            del_tau.append(J.dot(S2).dot(J.T))
+            tau = gzr[-1]
+            th.append(np.arctan(1 / tau))
+            th2.append(np.arctan2(r2 - r1, z2 - z1))
+            pre = -1 / (1 + tau**2)
+            J = np.array([pre / (r1 - r2), -pre / (r1 - r2), (-pre * (z1 - z2)) / (r1 - r2)**2,
+                          (pre * (z1 - z2)) / (r1 - r2)**2])
+            del_th.append(J.dot(S2).dot(J.T))
+        azimuth = atan2(yA, xA)                                                      # :352-365
+        ca, sa = np.cos(azimuth), np.sin(azimuth)
+        x_0 = (0.0 - xA) * ca + (0.0 - yA) * sa
+        for i, k in enumerate(dict_order):                                           # :371-437
+            u = sl["slot_src"][k]
+            xk, yk, zk, rk = gnn[u]
+            x_B = (xk - xA) * ca + (yk - yA) * sa
+            m_B = -(xk - xA) * sa + (yk - yA) * ca
+            H = np.array([[0.5 * x_0**2, x_0, 1], [0.0, 0.0, 1], [0.5 * x_B**2, x_B, 1]])
+            H_inv = np.linalg.inv(H)
+            sv = H_inv.dot([0.0, 0.0, m_B])
+            a, b = sv[0], sv[1]
+            dr, dz = rA - rk, zA - zk
+            hyp = np.sqrt(dr**2 + dz**2)
+            sin_t = np.abs(dr) / hyp
+            kappa = (2 * a) / (1 + ((2 * a * xk) + b)**2)**1.5
+            var_ms = sin_t * ((13.6 * 1e-3 * np.sqrt(0.02) * kappa) / 0.3)**2
+            if np.abs(zA) >= p.endcap_boundary:
+                var_ms = var_ms * np.abs(dr / dz)
+            cov = H_inv.dot(S).dot(H_inv.T)
+            cov[1, 1] += var_ms
+            sl["tse_sv"][k] = sv
+            sl["tse_tau"][k] = gzr[i]
+            sl["tse_cov"][k] = (cov[0, 0], cov[0, 1], cov[1, 0], cov[1, 1], del_tau[i]**2 + var_ms)
+            sl["tse_xyzr"][k] = (xk, yk, zk, rk)
+            sl["tse_theta"][k] = (th[i], th2[i], del_th[i]**2 + var_ms)
+            sl["tse_var_ms"][k] = var_ms
+        with np.errstate(all="ignore"):
+            xy_mv[v] = (np.mean(gxy), np.var(gxy))
+            zr_mv[v] = (np.mean(gzr), np.var(gzr))
+        ang[v] = azimuth
+        trans[v] = (xA, yA)
+    return {"xy_mean_var": xy_mv, "zr_mean_var": zr_mv, "angle_of_rotation": ang, "translation": trans}

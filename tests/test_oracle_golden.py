@@ -73,3 +73,22 @@ def test_tag_propagation():
     assert kept.sum() > 0.7 * len(kept)
     assert np.array_equal(tags[kept], extra["tags"][kept])
     assert np.array_equal(tags[~kept], g.node["tag"][~kept])
+
+
+TSE_FIELDS = ("tse_sv", "tse_tau", "tse_cov", "tse_xyzr", "tse_theta", "tse_var_ms")
+
+
+def test_track_state_estimates_full_vol7():
+    """helper.compute_track_state_estimates (§8 a2) on the whole volume-7 network"""
+    g, _, extra, meta = load("tse_full")
+    exp = {f: g.slot[f].copy() for f in TSE_FIELDS}
+    for f in TSE_FIELDS:
+        g.slot[f][:] = np.nan
+    node = O.compute_track_state_estimates(g, _params(meta))
+    has = g.slot["tse_rank"] >= 0
+    assert has.sum() == 14766
+    for f in TSE_FIELDS:
+        a, b = g.slot[f][has], exp[f][has]
+        assert np.allclose(a, b, rtol=RTOL, atol=0, equal_nan=True), f
+    for k in ("xy_mean_var", "zr_mean_var", "angle_of_rotation", "translation"):
+        assert np.allclose(node[k], extra[k], rtol=RTOL, atol=0, equal_nan=True), k

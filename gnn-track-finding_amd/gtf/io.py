@@ -76,3 +76,31 @@ def read_truth(path: str, node_ids: np.ndarray) -> np.ndarray:
     ok = (pos < u.size) & (u[np.minimum(pos, u.size - 1)] == node_ids)
     out[ok] = pid[first[pos[ok]]]
     return out
+
+
+def build_networkx(event_prefix: str, min_volume: int, max_volume: int, truth_csv: str = None):
+    """The reference's event_conversion graph (event_conversion.py:53-88): construct_graph
+    (helper.py:465-521) -- nodes in CSV order with GNN_Measurement, xy, zr, xyzr,
+    volume/layer ids, truth_particle and tags; both directions of every CSV edge in row
+    order -- then nx.DiGraph and the weakly connected subgraphs, copied. Returns the
+    list of subgraphs (no state estimates yet). module_id / hit_dissociation (truth-file
+    joins used only by extraction diagnostics) are not built."""
+    import networkx as nx
+    from GNN_Measurement.GNN_Measurement import GNN_Measurement
+    ids, x, y, z, r, layer = read_nodes(event_prefix + "nodes.csv", min_volume, max_volume)
+    truth = read_truth(truth_csv, ids) if truth_csv else np.full(ids.size, -1, np.int64)
+    G = nx.DiGraph()
+    for i in range(ids.size):
+        n = int(ids[i])
+        xi, yi, zi, ri = float(x[i]), float(y[i]), float(z[i]), float(r[i])
+        vol, lay = int(layer[i] / 1000), int(layer[i] % 100)
+        G.add_node(n, GNN_Measurement=GNN_Measurement(xi, yi, zi, ri, truth_particle=int(truth[i]), n=n),
+                   xy=(xi, yi), zr=(zi, ri), xyzr=(xi, yi, zi, ri), volume_id=vol, in_volume_layer_id=lay,
+                   vivl_id=(vol, lay), truth_particle=int(truth[i]), tags=[n])
+    n2, n1 = read_edges(event_prefix + "edges.csv")
+    for a, b in zip(n1.tolist(), n2.tolist()):
+        if a in G and b in G:
+            G.add_edge(a, b)
+            G.add_edge(b, a)
+    G = nx.DiGraph(G)
+    return [G.subgraph(c).copy() for c in nx.weakly_connected_components(G)]

@@ -56,6 +56,60 @@ def _key(k: str) -> str:
 
 
 # ------------------------------------------------------------------ helpers
+def compute_track_state_estimates(GraphList, sigma0xy, sigma0rz, sigma0rz2, endcap_boundary):
+    """helper.compute_track_state_estimates (helper.py:238-452) on the GPU.
+
+    The dict order is the reference's: reversed(set(nx.all_neighbors(G, node)))
+    (:277, :350-351), taken from this interpreter's own set() on the same neighbour
+    sequence; the states themselves come from gtf_track_state_estimates. Writes the
+    same node attributes and dict entries as the reference (``edge_covariance is
+    joint_vector_covariance``, :417-425)."""
+    import networkx as nx
+    import numpy as np
+    from .device import DeviceGraph
+    from .graph import mat_from_cov5
+    for G in GraphList:
+        for node in G.nodes():
+            keys = list(set(nx.all_neighbors(G, node)))
+            keys.reverse()
+            G.nodes[node]["track_state_estimates"] = {k: {} for k in keys}
+    g = pack(GraphList)
+    if g.n_nodes == 0:
+        return GraphList
+    p = Params(sigma0xy=sigma0xy, sigma0rz=sigma0rz, sigma0rz2=sigma0rz2, endcap_boundary=endcap_boundary)
+    d = DeviceGraph(g)
+    x = {k: v.cpu().numpy() for k, v in d.track_state_estimates(p).items()}
+    d.download(g)
+    S = g.slot
+    vi = 0
+    for G in GraphList:
+        for node in G.nodes():
+            attr = G.nodes[node]
+            lo, hi = int(g.slot_ptr[vi]), int(g.slot_ptr[vi + 1])
+            ranked = sorted((int(S["tse_rank"][k]), k) for k in range(lo, hi) if S["tse_rank"][k] >= 0)
+            keys = list(attr["track_state_estimates"].keys())
+            tse = {}
+            for (_, k), key in zip(ranked, keys):
+                sv = S["tse_sv"][k].copy()
+                cov = mat_from_cov5(S["tse_cov"][k])
+                th = S["tse_theta"][k]
+                xyzr = S["tse_xyzr"][k]
+                tse[key] = {"xyzr": (xyzr[0], xyzr[1], xyzr[2], xyzr[3]),
+                            "edge_state_vector": sv,
+                            "edge_covariance": cov,
+                            "joint_vector": [sv[0], sv[1], S["tse_tau"][k]],
+                            "joint_vector_covariance": cov,
+                            "theta": th[0], "theta2": th[1], "variance_theta": th[2],
+                            "var_ms_node": S["tse_var_ms"][k]}
+            attr["track_state_estimates"] = tse
+            attr["xy_edge_gradient_mean_var"] = tuple(np.float64(v) for v in x["xy_mean_var"][vi])
+            attr["zr_edge_gradient_mean_var"] = tuple(np.float64(v) for v in x["zr_mean_var"][vi])
+            attr["angle_of_rotation"] = float(x["angle_of_rotation"][vi])
+            attr["translation"] = (x["translation"][vi][0], x["translation"][vi][1])
+            vi += 1
+    return GraphList
+
+
 def compute_prior_probabilities(GraphList, track_state_key):
     """helper.compute_prior_probabilities (helper.py:30-63)"""
     k = _key(track_state_key)

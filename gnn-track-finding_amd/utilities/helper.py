@@ -22,6 +22,10 @@ def initialize_edge_activation(GraphList):         # helper.py:24-25
         nx.set_edge_attributes(subGraph, 1, "activated")
 
 
+def compute_track_state_estimates(GraphList, sigma0xy, sigma0rz, sigma0rz2, endcap_boundary):  # helper.py:238-452
+    return _st.compute_track_state_estimates(GraphList, sigma0xy, sigma0rz, sigma0rz2, endcap_boundary)
+
+
 def compute_prior_probabilities(GraphList, track_state_key):       # helper.py:30-63
     _st.compute_prior_probabilities(GraphList, track_state_key)
 

@@ -170,3 +170,75 @@ def test_dropin_update_cli(tmp_path):
     _run_cli("update/remove_state_metadata.py", ["-r", str(tmp_path / "rem") + "/"], str(tmp_path))
     errs = graphs_equal(_read(str(tmp_path / "rem")), d["out"])
     assert errs == [], "\n".join(errs[:20])
+
+
+@pytest.mark.gpu
+def test_dropin_track_state_estimates_vol7():
+    """helper.compute_track_state_estimates drop-in on the vol-7 network built from the
+    committed CSVs (gtf.io.build_networkx): every dict in the reference's order, every
+    value within 1e-6 of the reference's own run (tests/golden/tse_full.npz)"""
+    sys.path.insert(0, PKG)
+    from fixtures import load
+    from gtf import io
+    from utilities import helper as dh
+    g, _, extra, meta = load("tse_full")
+    kat = os.path.join(GOLDEN, "kat134", "event_1_filtered_graph_")
+    subs = io.build_networkx(kat, 7, 7)
+    dh.compute_track_state_estimates(subs, meta["sigma0xy"], meta["sigma0rz"], meta["sigma0rz2"],
+                                     meta["endcap_boundary"])
+    row = {int(n): i for i, n in enumerate(g.node["node_id"])}
+    S = g.slot
+    errs, n_keys = [], 0
+    for G in subs:
+        for n, attr in G.nodes(data=True):
+            vi = row[int(n)]
+            lo, hi = g.slot_ptr[vi], g.slot_ptr[vi + 1]
+            ks = sorted((S["tse_rank"][k], k) for k in range(lo, hi) if S["tse_rank"][k] >= 0)
+            exp_keys = [int(S["slot_key"][k]) for _, k in ks]
+            tse = attr["track_state_estimates"]
+            if [int(k) for k in tse] != exp_keys:
+                errs.append("node %d: dict order" % n)
+                continue
+            for (_, k), key in zip(ks, tse):
+                st = tse[key]
+                n_keys += 1
+                assert st["edge_covariance"] is st["joint_vector_covariance"]
+                c = st["edge_covariance"]
+                checks = [(st["edge_state_vector"], S["tse_sv"][k]), (st["joint_vector"][2], S["tse_tau"][k]),
+                          ([c[0, 0], c[0, 1], c[1, 0], c[1, 1], c[2, 2]], S["tse_cov"][k]),
+                          (st["xyzr"], S["tse_xyzr"][k]),
+                          ([st["theta"], st["theta2"], st["variance_theta"]], S["tse_theta"][k]),
+                          (st["var_ms_node"], S["tse_var_ms"][k])]
+                for a, b in checks:
+                    if not _close(a, b, 1e-6):
+                        errs.append("node %d key %d: %r != %r" % (n, key, a, b))
+            for name, ek in (("xy_edge_gradient_mean_var", "xy_mean_var"), ("zr_edge_gradient_mean_var",
+                                                                              "zr_mean_var")):
+                if not _close(attr[name], extra[ek][vi], 1e-6):
+                    errs.append("node %d %s" % (n, name))
+            if not _close(attr["angle_of_rotation"], extra["angle_of_rotation"][vi], 1e-12):
+                errs.append("node %d angle" % n)
+    assert n_keys == 14766
+    assert errs == [], errs[:10]
+
+
+def test_networkx_builder_reproduces_reference_dict_order():
+    """gtf.io.build_networkx + reversed(set(nx.all_neighbors)) gives the reference's
+    track_state_estimates key order on every node of the vol-7 network (CPU)"""
+    import networkx as nx
+    sys.path.insert(0, PKG)
+    from fixtures import load
+    from gtf import io
+    g, _, _, _ = load("tse_full")
+    subs = io.build_networkx(os.path.join(GOLDEN, "kat134", "event_1_filtered_graph_"), 7, 7)
+    row = {int(n): i for i, n in enumerate(g.node["node_id"])}
+    S = g.slot
+    for G in subs:
+        for n in G.nodes():
+            keys = list(set(nx.all_neighbors(G, n)))
+            keys.reverse()
+            vi = row[int(n)]
+            lo, hi = g.slot_ptr[vi], g.slot_ptr[vi + 1]
+            exp = [int(S["slot_key"][k]) for _, k in sorted((S["tse_rank"][k], k) for k in range(lo, hi)
+                                                            if S["tse_rank"][k] >= 0)]
+            assert [int(k) for k in keys] == exp, n

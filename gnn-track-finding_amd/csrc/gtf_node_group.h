@@ -1,5 +1,5 @@
 // gtf_node_group.h -- the node-local op sequence with G lanes per receiver node
-// (G = 16 for nodes with <= 16 slots, G = 64 for <= 64), one slot per lane.
+// (G = 8, 16, 32, 64 for nodes with <= 8, 16, 32, 64 slots), one slot per lane.
 //
 // Why: every stage after message passing reduces over one node's in-edge slot
 // segment. One thread per node serialises O(d^2) loops over

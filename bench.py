@@ -14,7 +14,9 @@ the config the north-star 1-GPU target is quoted on; it fits one GPU.
 Multi-GPU (torchrun, one process per GPU): every rank processes its own event
 (seed differs per rank) -- events are independent, so there is no data-path
 collective ("scaling": "weak"); the barrier and max-over-ranks timing bracket
-the timed steps. value = edges of all ranks x steps / max elapsed.
+the timed steps. value = edges of all ranks x steps / max elapsed. At N > 1 the
+line also carries "sharded_single_event": one C4 event edge-sharded across the N
+ranks with the per-pass RCCL exchange (gtf/shard.py), total work fixed ("strong").
 
 The CPU baseline (rank 0, N = 1 only) times the repository's NumPy restatement
 of the same pass (oracle/gtf_oracle.py, kind "port", 1 core) on a bounded
@@ -92,6 +94,40 @@ def bench_c5(dev, steps, warmup, n_events=256):
     return res
 
 
+def bench_sharded(workload, rank, world, dev, steps, warmup, params):
+    """Config 4 as the north star states it: ONE pileup-200 event edge-sharded across
+    the ranks (receiver ranges balanced by slot count), one exchange of the owned merged
+    states and activations per pass (all-gather over RCCL; gtf/shard.py). Total work is
+    fixed as N grows ("strong"). Every rank runs the same event (seed 0)."""
+    import torch
+    import torch.distributed as dist
+    from gtf import synth
+    from gtf.device import DeviceGraph
+    from gtf.shard import ShardedDeviceGraph
+    g = synth.workload(workload, seed=0)
+    sd = ShardedDeviceGraph(g, rank, world, dev, backend="nccl")
+    snap = sd.d.snapshot(DeviceGraph.PASS_INPUTS)
+    for _ in range(warmup):
+        sd.d.restore(snap)
+        sd.step(params)
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        sd.d.restore(snap)
+        sd.step(params)
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+    return {"scaling": "strong", "n_gpus": world, "edges": g.n_edges, "ms_per_step": el / steps * 1e3,
+            "edges_per_s": g.n_edges * steps / el, "exchange_chunk_bytes_per_rank": sd.chunk_bytes,
+            "owned_slots_max": sd.plan.cap_slots, "collective": "all_gather_into_tensor (RCCL)"}
+
+
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc", "pmc_c4.json")
 
 
@@ -119,6 +155,7 @@ def main():
     ap.add_argument("--cpu-tracks", type=int, default=4000, help="CPU-baseline sample size (tracks)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-c5", action="store_true", help="skip the config-5 parabolic-KL section")
+    ap.add_argument("--no-sharded", action="store_true", help="skip the single-event sharded section (N > 1)")
     args = ap.parse_args()
 
     import torch
@@ -201,6 +238,13 @@ def main():
     achieved = nbytes / (ms * 1e-3) / 1e9
     traffic = committed_traffic(args.workload, name)
 
+    sharded = None
+    if world > 1 and not args.no_sharded:
+        try:
+            sharded = bench_sharded(args.workload, rank, world, dev, K, W, p)
+        except Exception as ex:   # reported, never fatal: the headline line above stands
+            sharded = {"error": repr(ex)[:300]}
+
     c5 = None
     if rank == 0 and world == 1 and not args.no_c5:
         c5 = bench_c5(dev, K, W)
@@ -237,6 +281,7 @@ def main():
             "cpu_baseline": cpu,
             "device_error_flags": flags,
             "c5_parabolic_kl": c5,
+            "sharded_single_event": sharded,
         }
         if cpu:
             out["speedup_vs_cpu"] = out["value"] / cpu["value"]

@@ -91,10 +91,13 @@ __device__ __forceinline__ double highland_var_ms(double a, double b, const doub
 // not take part (:431). Out-list arrays are contiguous per sender: coalesced.
 // ---------------------------------------------------------------------------
 constexpr int SG = 8;
-__global__ void __launch_bounds__(BLOCK) k_sender(gtf_graph g, gtf_nodes n, gtf_edges e, gtf_params p, Ws w) {
-    const int u = (xcd_local(blockIdx.x, gridDim.x) * BLOCK + (int)threadIdx.x) / SG;
+__global__ void __launch_bounds__(BLOCK) k_sender(gtf_graph g, gtf_nodes n, gtf_edges e, gtf_params p, Ws w,
+                                                  const int32_t* list, int count) {
+    const int gi = (xcd_local(blockIdx.x, gridDim.x) * BLOCK + (int)threadIdx.x) / SG;
     const int gl = threadIdx.x & (SG - 1);
-    if (u >= g.n_nodes || !n.has_merged[u]) return;  // group-uniform
+    if (gi >= count) return;  // group-uniform
+    const int u = list ? list[gi] : gi;
+    if (!n.has_merged[u]) return;
     const int ob = g.out_ptr[u], oe = g.out_ptr[u + 1];
     if (ob == oe) return;
     const double a = n.merged_state[3 * (int64_t)u + 0];
@@ -124,9 +127,9 @@ __global__ void __launch_bounds__(BLOCK) k_sender(gtf_graph g, gtf_nodes n, gtf_
 // k_extrapolate: one slot (edge u -> v) per thread
 // ---------------------------------------------------------------------------
 __global__ void __launch_bounds__(BLOCK) k_extrapolate(gtf_graph g, gtf_nodes n, gtf_states uts, gtf_edges e,
-                                                       gtf_params p, Ws w) {
-    const int k = xcd_local(blockIdx.x, gridDim.x) * BLOCK + threadIdx.x;
-    if (k >= g.n_slots) return;
+                                                       gtf_params p, Ws w, int slot_lo, int slot_hi) {
+    const int k = slot_lo + xcd_local(blockIdx.x, gridDim.x) * BLOCK + threadIdx.x;
+    if (k >= slot_hi) return;
     uts.fresh[k] = 0;
     if (!g.is_edge[k]) return;
     const int u = g.slot_src[k];
@@ -250,6 +253,11 @@ __global__ void __launch_bounds__(BLOCK) k_extrapolate(gtf_graph g, gtf_nodes n,
 // ---------------------------------------------------------------------------
 // node-local stages (1 thread per receiver node)
 // ---------------------------------------------------------------------------
+#define EXTRAP_OPS OP_RANKS, OP_PRIORS_UTS, OP_REWEIGHT_UTS, OP_PRIORS_UTS, OP_REWEIGHT_UTS, OP_DEGREE
+#define UPDATE_OPS OP_PRUNE, OP_PRIORS_TSE, OP_PRIORS_UTS, OP_REWEIGHT_UTS
+#define CLUSTER_UTS_OPS OP_CLUSTER_UTS, OP_DEGREE, OP_MW_UTS, OP_PRIORS_UTS
+#define CLUSTER_TSE_OPS OP_CLUSTER_TSE, OP_DEGREE, OP_MW_TSE, OP_PRIORS_TSE
+
 struct Seg {
     int lo, hi;
 };
@@ -564,16 +572,26 @@ int check_graph(const gtf_graph* g) {
 
 inline int grid(int n) { return (n + BLOCK - 1) / BLOCK; }
 
+// sender scan over `senders` (NULL = every node) and extrapolation of slots [slot_lo,
+// slot_hi); events (may be NULL) are recorded before, between and after the two
 int launch_extrap_edges(const gtf_graph* g, gtf_nodes* n, gtf_states* uts, gtf_edges* e, const gtf_params* p,
-                        Ws w, hipStream_t st) {
-    if (g->n_slots > 0) {
-        hipLaunchKernelGGL(k_sender, dim3((g->n_nodes + BLOCK / SG - 1) / (BLOCK / SG)), dim3(BLOCK), 0, st, *g, *n,
-                           *e, *p, w);
-        hipLaunchKernelGGL(k_extrapolate, dim3(grid(g->n_slots)), dim3(BLOCK), 0, st, *g, *n, *uts, *e, *p, w);
-    }
+                        Ws w, hipStream_t st, const gtf_shard* sh = nullptr, void* const* events = nullptr) {
+    const int32_t* list = sh ? sh->senders : nullptr;
+    const int count = sh ? sh->n_senders : g->n_nodes;
+    const int slot_lo = sh ? sh->slot_lo : 0, slot_hi = sh ? sh->slot_hi : g->n_slots;
+    if (events) (void)hipEventRecord((hipEvent_t)events[0], st);
+    if (g->n_slots > 0 && count > 0)
+        hipLaunchKernelGGL(k_sender, dim3((count + BLOCK / SG - 1) / (BLOCK / SG)), dim3(BLOCK), 0, st, *g, *n, *e,
+                           *p, w, list, count);
+    if (events) (void)hipEventRecord((hipEvent_t)events[1], st);
+    if (slot_hi > slot_lo)
+        hipLaunchKernelGGL(k_extrapolate, dim3(grid(slot_hi - slot_lo)), dim3(BLOCK), 0, st, *g, *n, *uts, *e, *p,
+                           w, slot_lo, slot_hi);
+    if (events) (void)hipEventRecord((hipEvent_t)events[2], st);
     hipError_t err = hipGetLastError();
     return err == hipSuccess ? 0 : fail("extrapolate launch", err);
 }
+
 
 void finish_ops(NodeOps& ops, const gtf_states* tse, const gtf_states* uts) {
     for (int i = 0; i < ops.n; i++) {
@@ -592,7 +610,7 @@ void launch_serial_rest(const gtf_graph* g, gtf_nodes* n, const gtf_states& T, c
                         const gtf_params* p, Ws w, const NodeOps& ops, double chi2, double kl, hipStream_t st) {
     if (g->sched) {
         const int ng = g->n_g8 + g->n_g16 + g->n_g32 + g->n_g64;
-        const int nbig = g->n_nodes - ng;
+        const int nbig = g->n_big;
         if (nbig > 0)
             hipLaunchKernelGGL(k_node, dim3(grid(nbig)), dim3(BLOCK), 0, st, *g, *n, T, U, *e, *p, w, ops, chi2, kl,
                                g->sched + ng, nbig);
@@ -681,12 +699,23 @@ int launch_seq(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* ut
     return err == hipSuccess ? 0 : fail("node kernel launch", err);
 }
 
-#define EXTRAP_OPS OP_RANKS, OP_PRIORS_UTS, OP_REWEIGHT_UTS, OP_PRIORS_UTS, OP_REWEIGHT_UTS, OP_DEGREE
-#define UPDATE_OPS OP_PRUNE, OP_PRIORS_TSE, OP_PRIORS_UTS, OP_REWEIGHT_UTS
-#define CLUSTER_UTS_OPS OP_CLUSTER_UTS, OP_DEGREE, OP_MW_UTS, OP_PRIORS_UTS
-#define CLUSTER_TSE_OPS OP_CLUSTER_TSE, OP_DEGREE, OP_MW_TSE, OP_PRIORS_TSE
 
 #define SEQ(x) x, (int)sizeof(x)
+
+// the fused pass: message passing, then the node-local work in two launches (the light
+// reweight/update sequence at high occupancy, then clustering with its LDS staging)
+int run_pass(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts, gtf_edges* e,
+             const gtf_params* p, const gtf_shard* sh, void* ws, hipStream_t st, void* const* events) {
+    Ws w = carve(ws, g->n_nodes, g->n_slots);
+    int rc = launch_extrap_edges(g, n, uts, e, p, w, st, sh, events);
+    if (rc) return rc;
+    rc = launch_seq<EXTRAP_OPS, UPDATE_OPS>(g, n, tse, uts, e, p, w, 0.0, 0.0, st);
+    if (rc) return rc;
+    if (events) (void)hipEventRecord((hipEvent_t)events[3], st);
+    rc = launch_seq<CLUSTER_UTS_OPS>(g, n, tse, uts, e, p, w, p->cluster_chi2, p->cluster_kl, st);
+    if (events) (void)hipEventRecord((hipEvent_t)events[4], st);
+    return rc;
+}
 
 }  // namespace
 
@@ -773,26 +802,24 @@ int gtf_pass_ev(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* u
                 const gtf_params* p, void* ws, gtf_stream_t stream, void* const* events) {
     int rc = check_graph(g);
     if (rc) return rc;
-    hipStream_t st = (hipStream_t)stream;
-    Ws w = carve(ws, g->n_nodes, g->n_slots);
-    if (events) (void)hipEventRecord((hipEvent_t)events[0], st);
-    if (g->n_slots > 0)
-        hipLaunchKernelGGL(k_sender, dim3((g->n_nodes + BLOCK / SG - 1) / (BLOCK / SG)), dim3(BLOCK), 0, st, *g, *n,
-                           *e, *p, w);
-    if (events) (void)hipEventRecord((hipEvent_t)events[1], st);
-    if (g->n_slots > 0)
-        hipLaunchKernelGGL(k_extrapolate, dim3(grid(g->n_slots)), dim3(BLOCK), 0, st, *g, *n, *uts, *e, *p, w);
-    if (events) (void)hipEventRecord((hipEvent_t)events[2], st);
-    hipError_t err = hipGetLastError();
-    if (err != hipSuccess) return fail("extrapolate launch", err);
-    // node-local work in two launches: the light reweight/update sequence at high
-    // occupancy, then clustering (register-heavy) with its LDS state staging
-    rc = launch_seq<EXTRAP_OPS, UPDATE_OPS>(g, n, tse, uts, e, p, w, 0.0, 0.0, st);
+    return run_pass(g, n, tse, uts, e, p, nullptr, ws, (hipStream_t)stream, events);
+}
+
+int gtf_pass_shard(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts, gtf_edges* e,
+                   const gtf_params* p, const gtf_shard* sh, void* ws, gtf_stream_t stream, void* const* events) {
+    int rc = check_graph(g);
     if (rc) return rc;
-    if (events) (void)hipEventRecord((hipEvent_t)events[3], st);
-    rc = launch_seq<CLUSTER_UTS_OPS>(g, n, tse, uts, e, p, w, p->cluster_chi2, p->cluster_kl, st);
-    if (events) (void)hipEventRecord((hipEvent_t)events[4], st);
-    return rc;
+    if (!sh || sh->n_senders < 0 || (sh->n_senders > 0 && !sh->senders) || sh->slot_lo < 0 ||
+        sh->slot_hi < sh->slot_lo || sh->slot_hi > g->n_slots || sh->node_lo < 0 || sh->node_hi < sh->node_lo ||
+        sh->node_hi > g->n_nodes) {
+        snprintf(g_err, sizeof(g_err), "gtf_pass_shard: bad shard");
+        return -2;
+    }
+    if (!g->sched) {
+        snprintf(g_err, sizeof(g_err), "gtf_pass_shard: needs the owned receivers' schedule in g->sched");
+        return -2;
+    }
+    return run_pass(g, n, tse, uts, e, p, sh, ws, (hipStream_t)stream, events);
 }
 
 int gtf_pass(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts, gtf_edges* e,

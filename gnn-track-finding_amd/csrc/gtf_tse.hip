@@ -294,8 +294,11 @@ extern "C" int gtf_track_state_estimates(const gtf_graph* g, gtf_states* tse, co
         return -2;
     }
     const int n8 = g->n_g8, n16 = g->n_g16, n32 = g->n_g32, n64 = g->n_g64;
-    const int rest = g->n_nodes - n8 - n16 - n32 - n64;
-    if (rest < 0) { gtf::set_error("gtf_track_state_estimates: bad schedule counts"); return -2; }
+    const int rest = g->n_big;
+    if (rest < 0 || n8 < 0 || n16 < 0 || n32 < 0 || n64 < 0) {
+        gtf::set_error("gtf_track_state_estimates: bad schedule counts");
+        return -2;
+    }
     TseBuckets bk;
     bk.list[0] = g->sched + n8 + n16 + n32 + n64; bk.count[0] = rest;
     bk.list[1] = g->sched + n8 + n16 + n32;       bk.count[1] = n64;

@@ -16,7 +16,7 @@ F64 = ctypes.c_double
 
 
 class GtfGraph(ctypes.Structure):
-    _fields_ = [("n_nodes", I32), ("n_slots", I32), ("n_edges", I32), ("pad_", I32),
+    _fields_ = [("n_nodes", I32), ("n_slots", I32), ("n_edges", I32), ("n_big", I32),
                 ("slot_ptr", P), ("slot_src", P), ("slot_dst", P), ("out_ptr", P), ("out_slot", P),
                 ("slot_outpos", P),
                 ("is_edge", P), ("rev_edge", P), ("solo", P), ("gnn", P), ("xyzr", P), ("layer", P),
@@ -40,6 +40,11 @@ class GtfEdges(ctypes.Structure):
 class GtfParams(ctypes.Structure):
     _fields_ = [("sigma0xy", F64), ("sigma0rz", F64), ("sigma0rz2", F64), ("endcap_boundary", F64),
                 ("chi2_cut", F64), ("reweight_threshold", F64), ("cluster_chi2", F64), ("cluster_kl", F64)]
+
+
+class GtfShard(ctypes.Structure):
+    _fields_ = [("senders", P), ("n_senders", I32), ("node_lo", I32), ("node_hi", I32), ("slot_lo", I32),
+                ("slot_hi", I32)]
 
 
 class GtfTseExtra(ctypes.Structure):
@@ -72,7 +77,8 @@ ERR_FLAGS = {
 # exported symbols (must match include/gtf.h; tests check the .so exports all of them)
 SYMBOLS = ["gtf_workspace_bytes", "gtf_clear_errors", "gtf_read_errors", "gtf_extrapolate", "gtf_update",
            "gtf_message_passing", "gtf_node_ops",
-           "gtf_cluster", "gtf_pass", "gtf_pass_ev", "gtf_tag_prepare", "gtf_tag_sweep", "gtf_parabolic_kl", "gtf_track_state_estimates", "gtf_last_error",
+           "gtf_cluster", "gtf_pass", "gtf_pass_ev", "gtf_tag_prepare", "gtf_tag_sweep", "gtf_parabolic_kl", "gtf_track_state_estimates", "gtf_pass_shard",
+           "gtf_shard_chunk_bytes", "gtf_shard_pack", "gtf_shard_unpack", "gtf_last_error",
            "gtf_version"]
 
 OPS = {"ranks": 1, "priors_tse": 2, "priors_uts": 3, "reweight_uts": 4, "degree": 5, "prune": 6, "mw_tse": 7,
@@ -105,13 +111,20 @@ def lib():
     L.gtf_pass_ev.argtypes = [G, N, S, S, E, PR, P, P, ctypes.POINTER(P)]
     L.gtf_tag_prepare.argtypes = [G, P, P, P, P, P]
     L.gtf_tag_sweep.argtypes = [G, P, P, P, P, P, P]
+    SH = ctypes.POINTER(GtfShard)
+    L.gtf_pass_shard.argtypes = [G, N, S, S, E, PR, SH, P, P, ctypes.POINTER(P)]
+    L.gtf_shard_chunk_bytes.restype = ctypes.c_size_t
+    L.gtf_shard_chunk_bytes.argtypes = [I32, I32]
+    L.gtf_shard_pack.argtypes = [N, E, SH, I32, I32, P, P]
+    L.gtf_shard_unpack.argtypes = [N, E, P, I32, I32, P, I32, I32, P]
     L.gtf_track_state_estimates.argtypes = [G, S, ctypes.POINTER(GtfTseExtra), PR, P]
     L.gtf_parabolic_kl.argtypes = [ctypes.POINTER(GtfKlGraph), I32, ctypes.POINTER(GtfKlOut), P]
     L.gtf_last_error.restype = ctypes.c_char_p
     L.gtf_version.restype = ctypes.c_char_p
     for fn in ("gtf_clear_errors", "gtf_read_errors", "gtf_extrapolate", "gtf_update", "gtf_cluster", "gtf_pass",
                "gtf_pass_ev", "gtf_message_passing", "gtf_node_ops",
-               "gtf_tag_prepare", "gtf_tag_sweep", "gtf_parabolic_kl", "gtf_track_state_estimates"):
+               "gtf_tag_prepare", "gtf_tag_sweep", "gtf_parabolic_kl", "gtf_track_state_estimates", "gtf_pass_shard", "gtf_shard_pack",
+               "gtf_shard_unpack"):
         getattr(L, fn).restype = ctypes.c_int
     _lib = L
     return L

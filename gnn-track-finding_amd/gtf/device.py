@@ -68,6 +68,7 @@ class DeviceGraph:
         rest = idx[deg > 64]
         up("sched", np.concatenate(buckets + [rest]).astype(np.int32))
         self.n_g_all = [int(b.size) for b in buckets]
+        self.n_big = int(rest.size)
         self.n_g = self.n_g_all if schedule else [0, 0, 0, 0]
         self.use_sched = schedule
         for f in ("gnn", "xyzr", "layer") + MUTABLE_NODE:
@@ -112,11 +113,13 @@ class DeviceGraph:
 
     def _build_structs(self):
         p = self.ptr
-        self.cg = nat.GtfGraph(self.n_nodes, self.n_slots, self.n_edges, 0, p("slot_ptr"), p("slot_src"),
+        self.cg = nat.GtfGraph(self.n_nodes, self.n_slots, self.n_edges, self.n_big if self.use_sched else 0,
+                               p("slot_ptr"), p("slot_src"),
                                p("slot_dst"), p("out_ptr"), p("out_slot"), p("slot_outpos"), p("is_edge"), p("rev_edge"), p("solo"),
                                p("gnn"), p("xyzr"), p("layer"),
                                p("sched") if self.use_sched else ctypes.c_void_p(0), *self.n_g)
-        self.cg_sched = nat.GtfGraph(self.n_nodes, self.n_slots, self.n_edges, 0, p("slot_ptr"), p("slot_src"),
+        self.cg_sched = nat.GtfGraph(self.n_nodes, self.n_slots, self.n_edges, self.n_big, p("slot_ptr"),
+                                     p("slot_src"),
                                      p("slot_dst"), p("out_ptr"), p("out_slot"), p("slot_outpos"), p("is_edge"),
                                      p("rev_edge"), p("solo"), p("gnn"), p("xyzr"), p("layer"), p("sched"),
                                      *self.n_g_all)

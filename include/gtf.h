@@ -40,7 +40,7 @@ typedef struct gtf_graph {
     int32_t n_nodes;
     int32_t n_slots;          /* slots = (receiver, sender) pairs, receiver-major */
     int32_t n_edges;          /* directed edges = slots with is_edge == 1 */
-    int32_t pad_;
+    int32_t n_big;            /* schedule entries after the four lane-group buckets (> 64 slots) */
     const int32_t* slot_ptr;  /* [N+1] slot segment of each receiver */
     const int32_t* slot_src;  /* [S]   sender node index, -1 = orphan state key */
     const int32_t* slot_dst;  /* [S]   receiver node index */
@@ -56,7 +56,8 @@ typedef struct gtf_graph {
     /* optional node schedule for the node-local stages (NULL = one thread per node):
      * node indices bucketed by slot count -- n_g8 nodes with <= 8 slots, then n_g16 with
      * 9..16, n_g32 with 17..32, n_g64 with 33..64 (a group of that many lanes per node),
-     * then the rest (one thread per node). Built once per graph (gtf/device.py). */
+     * then n_big nodes with more slots (one thread per node). Built once per graph
+     * (gtf/device.py); a shard's graph view holds the schedule of its own receivers. */
     const int32_t* sched;     /* [N] */
     int32_t n_g8;
     int32_t n_g16;
@@ -169,6 +170,37 @@ int gtf_pass(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts,
  * events may be NULL). */
 int gtf_pass_ev(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts, gtf_edges* e,
                 const gtf_params* p, void* workspace, gtf_stream_t stream, void* const* events);
+
+/* ---- One event sharded across GPUs --------------------------------
+ * Rank r owns a contiguous receiver range [node_lo, node_hi) and so the contiguous slot
+ * range [slot_lo, slot_hi) (slots are receiver-major); every rank holds the whole graph.
+ * gtf_pass_shard runs the pass for the owned receivers: the sender scan over `senders`
+ * (every sender with an out-edge into an owned receiver, plus the owned senders whose
+ * merged_cov write-back the rank publishes), extrapolation of the owned slots, and the
+ * node kernels over the owned receivers (pass `g` with sched, n_g8..n_g64 and n_big describing the
+ * owned receivers only). Between passes each rank publishes its owned merged states and
+ * slot activations (gtf_shard_pack -> an all-gather of equal-size chunks over RCCL ->
+ * gtf_shard_unpack), the only cross-rank data the next pass reads. */
+typedef struct gtf_shard {
+    const int32_t* senders;   /* [n_senders] device */
+    int32_t n_senders;
+    int32_t node_lo, node_hi;
+    int32_t slot_lo, slot_hi;
+} gtf_shard;
+
+int gtf_pass_shard(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts, gtf_edges* e,
+                   const gtf_params* p, const gtf_shard* shard, void* workspace, gtf_stream_t stream,
+                   void* const* events);
+/* bytes of one rank's chunk holding up to cap_nodes node states and cap_slots activations */
+size_t gtf_shard_chunk_bytes(int32_t cap_nodes, int32_t cap_slots);
+/* write the owned nodes' has_merged / merged_state / merged_cov / merged_prior and the
+ * owned slots' activation into chunk (device) */
+int gtf_shard_pack(const gtf_nodes* n, const gtf_edges* e, const gtf_shard* shard, int32_t cap_nodes,
+                   int32_t cap_slots, void* chunk, gtf_stream_t stream);
+/* scatter the chunks of all ranks except `self` (gathered: nranks chunks back to back);
+ * ranges: device int32 [4 * nranks] = node_lo, node_hi, slot_lo, slot_hi per rank */
+int gtf_shard_unpack(gtf_nodes* n, gtf_edges* e, const void* gathered, int32_t nranks, int32_t self,
+                     const int32_t* ranges, int32_t cap_nodes, int32_t cap_slots, gtf_stream_t stream);
 
 /* Tag propagation. radius: [N] node radius (attr 'zr'[1]); keep: [E] output mask of
  * kept inward neighbours per out-edge (u8, indexed by out-edge position);

@@ -35,6 +35,9 @@ void set_error(const char* msg);
 namespace {
 
 constexpr int BLOCK = 256;
+#ifndef GTF_KL_NPT
+#define GTF_KL_NPT 1
+#endif
 
 // node frame: rotation by 2 pi - atan2(y, x) (rotate_track, utils.py:197-218, with
 // cos/sin of the angle as x/h, -y/h), then translation to the node (:262-270)
@@ -42,10 +45,10 @@ struct Frame {
     double ca, sa, xt, yt, x0, x, y;
 };
 
-__device__ __forceinline__ Frame node_frame(const double* gnn, int v) {
+__device__ __forceinline__ Frame node_frame_xy(double x, double y) {
     Frame f;
-    f.x = gnn[4 * (int64_t)v];
-    f.y = gnn[4 * (int64_t)v + 1];
+    f.x = x;
+    f.y = y;
     const double h = sqrt(f.x * f.x + f.y * f.y);
     f.ca = h > 0.0 ? f.x / h : 1.0;
     f.sa = h > 0.0 ? -f.y / h : 0.0;
@@ -150,7 +153,7 @@ __device__ __forceinline__ void pkl_node(const gtf_kl_graph& g, const gtf_kl_out
     const int lo = g.slot_ptr[v], d = g.slot_ptr[v + 1] - lo;
     if (d < 1) return;
     Stage* stg = (Stage*)smem + (int)threadIdx.x / G;
-    const Frame f = node_frame(g.gnn, v);
+    const Frame f = node_frame_xy(g.gnn[4 * (int64_t)v], g.gnn[4 * (int64_t)v + 1]);
 
     // states of the node's in-edges and the gradients dy/dx (utils.py:249-254, 273-283)
     double gsum = 0.0, gr0 = 0.0;
@@ -219,40 +222,78 @@ __device__ __forceinline__ void pkl_node(const gtf_kl_graph& g, const gtf_kl_out
 }
 
 // d <= 2: one thread per node, both states in registers (the bulk of a TrackML
-// volume: 88 % of the listed nodes of the vol-7 134 event)
+// volume: 88 % of the listed nodes of the vol-7 134 event). A thread may take NPT
+// nodes and issue their loads phase by phase (node -> its slots -> the neighbours),
+// NPT independent gather chains in flight per lane. Measured on config 5: NPT = 1 48 us, 2 58 us, 4 90 us -- more
+// resident waves beat more chains per wave, so the default is 1.
+constexpr int NPT = GTF_KL_NPT;
+
 template <typename T, bool STATES>
 __device__ __forceinline__ void pkl_node1(const gtf_kl_graph& g, const gtf_kl_out& o, const int32_t* list, int count,
                                           int bid) {
-    const int gi = bid * BLOCK + (int)threadIdx.x;
-    if (gi >= count) return;
-    const int v = list[gi];
-    const int lo = g.slot_ptr[v], d = g.slot_ptr[v + 1] - lo;
-    if (d < 1 || d > 2) return;
-    const Frame f = node_frame(g.gnn, v);
-    const int u0 = g.slot_src[lo];
-    const int u1 = d == 2 ? g.slot_src[lo + 1] : u0;
-    const double x0 = g.gnn[4 * (int64_t)u0], y0 = g.gnn[4 * (int64_t)u0 + 1];
-    const double x1 = g.gnn[4 * (int64_t)u1], y1 = g.gnn[4 * (int64_t)u1 + 1];
-    bool s0, s1 = false;
-    const PState<T> a = pstate<T>(f, x0, y0, s0, STATES ? o.sv + 3 * (int64_t)lo : nullptr,
-                                  STATES ? o.cov + 9 * (int64_t)lo : nullptr);
-    PState<T> b = a;
-    if (d == 2)
-        b = pstate<T>(f, x1, y1, s1, STATES ? o.sv + 3 * (int64_t)(lo + 1) : nullptr,
-                      STATES ? o.cov + 9 * (int64_t)(lo + 1) : nullptr);
-    if ((s0 || s1) && o.err) atomicOr(o.err, (uint32_t)GTF_ERR_SINGULAR_H);
-    const double g0 = (f.y - y0) / (f.x - x0);
-    const double g1 = d == 2 ? (f.y - y1) / (f.x - x1) : g0;
-    const double mean = (d == 2 ? g0 + g1 : g0) / (double)d;
-    if (o.emp_var) o.emp_var[v] = (d == 2 ? (g0 - mean) * (g0 - mean) + (g1 - mean) * (g1 - mean) : 0.0 * (g0 - mean))
-                                  / (double)d;
-    if (o.emp_mean) o.emp_mean[v] = mean;
-    if (d == 2) {
-        const int64_t p = g.pair_ptr[v];
-        ((T*)o.kl)[p] = pkl<T>(b, a);   // pair (i, j) = (1, 0)
-        if (o.truth) {
-            const long long tv = g.truth[v], ti = g.truth[u1], tj = g.truth[u0];
-            o.truth[p] = (int8_t)(tv == ti && ti == tj && tv == tj);
+    int v[NPT], lo[NPT], d[NPT], u0[NPT], u1[NPT];
+    double xv[NPT], yv[NPT], x0[NPT], y0[NPT], x1[NPT], y1[NPT];
+    int64_t pp[NPT];
+    long long tv[NPT], t0[NPT], t1[NPT];
+#pragma unroll
+    for (int j = 0; j < NPT; j++) {
+        const int gi = (bid * NPT + j) * BLOCK + (int)threadIdx.x;
+        v[j] = gi < count ? list[gi] : -1;
+    }
+#pragma unroll
+    for (int j = 0; j < NPT; j++) {
+        d[j] = 0;
+        if (v[j] >= 0) {
+            lo[j] = g.slot_ptr[v[j]];
+            d[j] = g.slot_ptr[v[j] + 1] - lo[j];
+            xv[j] = g.gnn[4 * (int64_t)v[j]];
+            yv[j] = g.gnn[4 * (int64_t)v[j] + 1];
+            pp[j] = g.pair_ptr[v[j]];
+            tv[j] = (o.truth && g.truth) ? g.truth[v[j]] : 0;
+        }
+        if (d[j] < 1 || d[j] > 2) d[j] = 0;
+    }
+#pragma unroll
+    for (int j = 0; j < NPT; j++)
+        if (d[j]) {
+            u0[j] = g.slot_src[lo[j]];
+            u1[j] = d[j] == 2 ? g.slot_src[lo[j] + 1] : u0[j];
+        }
+#pragma unroll
+    for (int j = 0; j < NPT; j++)
+        if (d[j]) {
+            x0[j] = g.gnn[4 * (int64_t)u0[j]];
+            y0[j] = g.gnn[4 * (int64_t)u0[j] + 1];
+            x1[j] = g.gnn[4 * (int64_t)u1[j]];
+            y1[j] = g.gnn[4 * (int64_t)u1[j] + 1];
+            if (o.truth && g.truth) {
+                t0[j] = g.truth[u0[j]];
+                t1[j] = g.truth[u1[j]];
+            }
+        }
+#pragma unroll
+    for (int j = 0; j < NPT; j++) {
+        if (!d[j]) continue;
+        const Frame f = node_frame_xy(xv[j], yv[j]);
+        const int l = lo[j];
+        bool s0, s1 = false;
+        const PState<T> a = pstate<T>(f, x0[j], y0[j], s0, STATES ? o.sv + 3 * (int64_t)l : nullptr,
+                                      STATES ? o.cov + 9 * (int64_t)l : nullptr);
+        PState<T> b = a;
+        if (d[j] == 2)
+            b = pstate<T>(f, x1[j], y1[j], s1, STATES ? o.sv + 3 * (int64_t)(l + 1) : nullptr,
+                          STATES ? o.cov + 9 * (int64_t)(l + 1) : nullptr);
+        if ((s0 || s1) && o.err) atomicOr(o.err, (uint32_t)GTF_ERR_SINGULAR_H);
+        const double g0 = (f.y - y0[j]) / (f.x - x0[j]);
+        const double g1 = d[j] == 2 ? (f.y - y1[j]) / (f.x - x1[j]) : g0;
+        const double mean = (d[j] == 2 ? g0 + g1 : g0) / (double)d[j];
+        if (o.emp_var)
+            o.emp_var[v[j]] = (d[j] == 2 ? (g0 - mean) * (g0 - mean) + (g1 - mean) * (g1 - mean)
+                                         : 0.0 * (g0 - mean)) / (double)d[j];
+        if (o.emp_mean) o.emp_mean[v[j]] = mean;
+        if (d[j] == 2) {
+            ((T*)o.kl)[pp[j]] = pkl<T>(b, a);   // pair (i, j) = (1, 0)
+            if (o.truth) o.truth[pp[j]] = (int8_t)(tv[j] == t1[j] && t1[j] == t0[j] && tv[j] == t0[j]);
         }
     }
 }
@@ -299,7 +340,8 @@ int launch(const gtf_kl_graph* g, const gtf_kl_out* o, hipStream_t st) {
     KlBuckets bk;
     int total = 0;
     for (int i = 0; i < 4; i++) {
-        bk.blocks[i] = gtf::pad8((g->count[i] + BLOCK / BG[i] - 1) / (BLOCK / BG[i]));
+        const int per_block = i == 0 ? BLOCK * NPT : BLOCK / BG[i];   // nodes per block
+        bk.blocks[i] = gtf::pad8((g->count[i] + per_block - 1) / per_block);
         total += bk.blocks[i];
     }
     if (total > 0) {

@@ -28,24 +28,19 @@ constexpr int BLOCK = 256;
 constexpr int MAX_CLUSTER = 15;  // clustering.py:207 (2 < d < 16)
 
 struct Ws {
-    uint32_t* err;     // error word
-    double* var_ms;    // [E] var_ms of each out-edge, in out-list order (-1 = edge was inactive)
-    double* c11_base;  // [N] merged_cov[1,1] before message passing
-    double* c11_seen;  // [E] merged_cov[1,1] seen by each out-edge's extrapolation (out-list order)
+    uint32_t* err;    // error word
+    double2* vc;      // [S] per active edge, by SLOT: (var_ms, merged_cov[1,1] its extrapolation sees)
 };
 
 __host__ inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
 __host__ inline Ws carve(void* base, int32_t n_nodes, int32_t n_slots) {
+    (void)n_nodes;
     char* p = (char*)base;
     Ws w;
     w.err = (uint32_t*)p;
     p += 256;
-    w.var_ms = (double*)p;
-    p += align256(sizeof(double) * (size_t)(n_slots > 0 ? n_slots : 1));
-    w.c11_base = (double*)p;
-    p += align256(sizeof(double) * (size_t)(n_nodes > 0 ? n_nodes : 1));
-    w.c11_seen = (double*)p;
+    w.vc = (double2*)p;
     return w;
 }
 
@@ -88,7 +83,9 @@ __device__ __forceinline__ double highland_var_ms(double a, double b, const doub
 // running "merged_cov[1, 1] += var_ms" its extrapolation sees (:127-128) as the
 // sequential sum over the lanes before it (shuffles, the reference's addition
 // order), and the last value is the array the stage saves. Inactive out-edges do
-// not take part (:431). Out-list arrays are contiguous per sender: coalesced.
+// not take part (:431). Out-list reads are contiguous per sender; each active edge's
+// (var_ms, running value) record goes to the edge's slot, where k_extrapolate reads
+// it coalesced instead of gathering it through the sender's out-list.
 // ---------------------------------------------------------------------------
 constexpr int SG = 8;
 __global__ void __launch_bounds__(BLOCK) k_sender(gtf_graph g, gtf_nodes n, gtf_edges e, gtf_params p, Ws w,
@@ -107,17 +104,19 @@ __global__ void __launch_bounds__(BLOCK) k_sender(gtf_graph g, gtf_nodes n, gtf_
     for (int base = ob; base < oe; base += SG) {
         const int i = base + gl;
         double vm = -1.0;
+        int k = -1;
         if (i < oe) {
-            const int k = g.out_slot[i];
+            k = g.out_slot[i];
             if (e.act[k] == 1) vm = highland_var_ms(a, b, ng, g.gnn + 4 * (int64_t)g.slot_dst[k], p.endcap_boundary);
-            w.var_ms[i] = vm;
         }
         double c = carry;
         for (int m = 0; m < SG; m++) {
             const double vmm = __shfl(vm, m, SG);
             if (m <= gl && vmm != -1.0) c = c + vmm;
         }
-        if (i < oe) w.c11_seen[i] = c;
+        // one 16-byte record per active edge, stored at its slot: the extrapolation
+        // thread of that slot reads it coalesced
+        if (vm != -1.0) w.vc[k] = make_double2(vm, c);
         carry = __shfl(c, SG - 1, SG);  // lanes past the end carry the full sum
     }
     if (gl == 0) n.merged_cov[5 * (int64_t)u + 3] = carry;
@@ -135,7 +134,6 @@ __global__ void __launch_bounds__(BLOCK) k_extrapolate(gtf_graph g, gtf_nodes n,
     const int u = g.slot_src[k];
     if (!n.has_merged[u]) return;
     if (e.act[k] != 1) return;
-    const int oi = g.out_ptr[u] + g.slot_outpos[k];
     const int v = g.slot_dst[k];
     const double* ng = g.gnn + 4 * (int64_t)u;  // sender ("node" in the reference)
     const double* nb = g.gnn + 4 * (int64_t)v;  // receiver ("neighbour")
@@ -178,9 +176,10 @@ __global__ void __launch_bounds__(BLOCK) k_extrapolate(gtf_graph g, gtf_nodes n,
     const double dc_dc = (ds_dc * bracket) + cp;
     const Mat3 F = {{{da_da, da_db, da_dc}, {db_da, db_db, db_dc}, {dc_da, dc_db, dc_dc}}};
 
-    const double var_ms = w.var_ms[oi];
+    const double2 vc = w.vc[k];
+    const double var_ms = vc.x;
     const double* mcp = n.merged_cov + 5 * (int64_t)u;
-    const Mat3 C = {{{mcp[0], mcp[1], 0.0}, {mcp[2], w.c11_seen[oi], 0.0}, {0.0, 0.0, mcp[4]}}};  // :128
+    const Mat3 C = {{{mcp[0], mcp[1], 0.0}, {mcp[2], vc.y, 0.0}, {0.0, 0.0, mcp[4]}}};  // :128
     const double m[3] = {a, b, c};
     double xe[3];
     mv3(F, m, xe);                                                                 // :129
@@ -727,8 +726,8 @@ void set_error(const char* msg) { snprintf(g_err, sizeof(g_err), "%s", msg); }
 extern "C" {
 
 size_t gtf_workspace_bytes(int32_t n_nodes, int32_t n_slots) {
-    return 256 + 2 * align256(sizeof(double) * (size_t)(n_slots > 0 ? n_slots : 1)) +
-           align256(sizeof(double) * (size_t)(n_nodes > 0 ? n_nodes : 1));
+    (void)n_nodes;
+    return 256 + align256(2 * sizeof(double) * (size_t)(n_slots > 0 ? n_slots : 1));
 }
 
 int gtf_clear_errors(void* ws, gtf_stream_t stream) {

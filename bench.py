@@ -66,16 +66,19 @@ def bench_c5(dev, steps, warmup, n_events=256):
         out = k.alloc(dt, emp="var")
         for _ in range(warmup):
             k.run(out, dt)
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+        # K launches back to back between two events: the launch time on the stream,
+        # free of the host's per-call enqueue gap (one ctypes call ~8 us, longer than
+        # a small kernel), so kernel_ms is the device time per launch
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for a, b in ev:
-            a.record()
+        a.record()
+        for _ in range(steps):
             k.run(out, dt)
-            b.record()
+        b.record()
         torch.cuda.synchronize()
         wall = (time.perf_counter() - t0) / steps
-        ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+        ms = a.elapsed_time(b) / steps
         nbytes = rf.parabolic_kl_bytes(k.n_nodes, res["listed_nodes"], k.n_slots, k.n_pairs, dt)
         res[dt] = {"pairs_per_s": k.n_pairs / wall, "kernel_ms": ms, "wall_ms_per_step": wall * 1e3,
                    "roofline": {"bound": "hbm", "achieved": nbytes / (ms * 1e-3) / 1e9, "peak": rf.HBM_PEAK_GBS,

@@ -107,7 +107,8 @@ __global__ void __launch_bounds__(BLOCK) k_sender(gtf_graph g, gtf_nodes n, gtf_
         int k = -1;
         if (i < oe) {
             k = g.out_slot[i];
-            if (e.act[k] == 1) vm = highland_var_ms(a, b, ng, g.gnn + 4 * (int64_t)g.slot_dst[k], p.endcap_boundary);
+            const int v = g.out_dst ? g.out_dst[i] : g.slot_dst[k];
+            if (e.act[k] == 1) vm = highland_var_ms(a, b, ng, g.gnn + 4 * (int64_t)v, p.endcap_boundary);
         }
         double c = carry;
         for (int m = 0; m < SG; m++) {

@@ -22,7 +22,7 @@ __global__ void __launch_bounds__(BLOCK) k_tag_prepare(gtf_graph g, const double
         const double ru = radius[u];
         int any = 0;
         for (int i = g.out_ptr[u]; i < g.out_ptr[u + 1]; i++) {
-            const int w = g.slot_dst[g.out_slot[i]];
+            const int w = g.out_dst ? g.out_dst[i] : g.slot_dst[g.out_slot[i]];
             const uint8_t k = !(radius[w] > ru);
             keep[i] = k;
             any |= k;
@@ -45,7 +45,7 @@ __global__ void __launch_bounds__(BLOCK) k_tag_sweep(gtf_graph g, const uint8_t*
         if (processed[u]) {
             for (int i = g.out_ptr[u]; i < g.out_ptr[u + 1]; i++)
                 if (keep[i]) {
-                    const int64_t tw = tin[g.slot_dst[g.out_slot[i]]];
+                    const int64_t tw = tin[g.out_dst ? g.out_dst[i] : g.slot_dst[g.out_slot[i]]];
                     t = tw > t ? tw : t;
                 }
             flipped = (t != t0);

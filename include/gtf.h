@@ -63,6 +63,8 @@ typedef struct gtf_graph {
     int32_t n_g16;
     int32_t n_g32;
     int32_t n_g64;
+    const int32_t* out_dst;   /* [E] receiver of each out-edge = slot_dst[out_slot] (saves the sender
+                                 scan a dependent gather), or NULL */
 } gtf_graph;
 
 /* ---- per-node mutable state ------------------------------------------------ */

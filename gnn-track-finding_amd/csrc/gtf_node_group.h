@@ -449,7 +449,7 @@ __device__ __forceinline__ bool node_load(NodeCtx<G>& c, const gtf_graph& g, con
     c.act = c.valid ? e.act[k] : 0;
     c.act0 = c.act;
     c.src = c.valid ? g.slot_src[k] : -1;
-    c.layer = c.src >= 0 ? g.layer[c.src] : NAN;
+    c.layer = g.slot_layer ? (c.valid ? g.slot_layer[k] : NAN) : (c.src >= 0 ? g.layer[c.src] : NAN);
     c.same_layer = 0;
     c.same_layer_ok = false;
     c.tse = LaneDict{-1, 0.0, 0.0, false, -1, false};

@@ -20,7 +20,8 @@ class GtfGraph(ctypes.Structure):
                 ("slot_ptr", P), ("slot_src", P), ("slot_dst", P), ("out_ptr", P), ("out_slot", P),
                 ("slot_outpos", P),
                 ("is_edge", P), ("rev_edge", P), ("solo", P), ("gnn", P), ("xyzr", P), ("layer", P),
-                ("sched", P), ("n_g8", I32), ("n_g16", I32), ("n_g32", I32), ("n_g64", I32), ("out_dst", P)]
+                ("sched", P), ("n_g8", I32), ("n_g16", I32), ("n_g32", I32), ("n_g64", I32), ("out_dst", P),
+                ("slot_layer", P)]
 
 
 class GtfNodes(ctypes.Structure):

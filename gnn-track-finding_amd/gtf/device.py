@@ -49,6 +49,9 @@ class DeviceGraph:
         up("out_slot", g.out_slot.astype(np.int32))
         up("slot_dst", g.slot_dst().astype(np.int32))
         up("out_dst", g.slot_dst()[g.out_slot].astype(np.int32) if g.n_edges else np.zeros(0, np.int32))
+        src = g.slot["slot_src"].astype(np.int64)
+        up("slot_layer", np.where(src >= 0, g.node["layer"][np.maximum(src, 0)] if g.n_nodes else np.nan,
+                                  np.nan).astype(np.float64))
         outpos = np.full(g.n_slots, -1, np.int32)
         if g.n_edges:
             owner = np.repeat(np.arange(g.n_nodes, dtype=np.int64), np.diff(g.out_ptr.astype(np.int64)))
@@ -118,12 +121,12 @@ class DeviceGraph:
                                p("slot_ptr"), p("slot_src"),
                                p("slot_dst"), p("out_ptr"), p("out_slot"), p("slot_outpos"), p("is_edge"), p("rev_edge"), p("solo"),
                                p("gnn"), p("xyzr"), p("layer"),
-                               p("sched") if self.use_sched else ctypes.c_void_p(0), *self.n_g, p("out_dst"))
+                               p("sched") if self.use_sched else ctypes.c_void_p(0), *self.n_g, p("out_dst"), p("slot_layer"))
         self.cg_sched = nat.GtfGraph(self.n_nodes, self.n_slots, self.n_edges, self.n_big, p("slot_ptr"),
                                      p("slot_src"),
                                      p("slot_dst"), p("out_ptr"), p("out_slot"), p("slot_outpos"), p("is_edge"),
                                      p("rev_edge"), p("solo"), p("gnn"), p("xyzr"), p("layer"), p("sched"),
-                                     *self.n_g_all, p("out_dst"))
+                                     *self.n_g_all, p("out_dst"), p("slot_layer"))
         self.cn = nat.GtfNodes(*[p(f) for f in MUTABLE_NODE])
         self.cuts = nat.GtfStates(p("uts_rank"), p("uts_sv"), p("uts_tau"), p("uts_cov"), p("uts_xyzr"),
                                   p("uts_lik"), p("uts_mw"), p("uts_prior"), p("uts_lr"), p("uts_side"),

@@ -110,7 +110,8 @@ class ShardedDeviceGraph:
         vp = lambda t: ctypes.c_void_p(t.data_ptr() if t.numel() else 0)  # noqa: E731
         self.cg = nat.GtfGraph(d.n_nodes, d.n_slots, d.n_edges, n_big, p("slot_ptr"), p("slot_src"), p("slot_dst"),
                                p("out_ptr"), p("out_slot"), p("slot_outpos"), p("is_edge"), p("rev_edge"),
-                               p("solo"), p("gnn"), p("xyzr"), p("layer"), vp(self.sched), *n_g, p("out_dst"))
+                               p("solo"), p("gnn"), p("xyzr"), p("layer"), vp(self.sched), *n_g, p("out_dst"),
+                               p("slot_layer"))
         pl = self.plan
         self.shard = nat.GtfShard(vp(self.senders), int(self.senders.numel()), int(pl.node_lo[rank]),
                                   int(pl.node_hi[rank]), int(pl.slot_lo[rank]), int(pl.slot_hi[rank]))

@@ -65,6 +65,8 @@ typedef struct gtf_graph {
     int32_t n_g64;
     const int32_t* out_dst;   /* [E] receiver of each out-edge = slot_dst[out_slot] (saves the sender
                                  scan a dependent gather), or NULL */
+    const double* slot_layer; /* [S] layer of each slot's sender (NaN for orphans) = layer[slot_src]:
+                                 a coalesced read in the node kernels instead of a gather, or NULL */
 } gtf_graph;
 
 /* ---- per-node mutable state ------------------------------------------------ */

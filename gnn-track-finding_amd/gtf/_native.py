@@ -53,6 +53,17 @@ class GtfTseExtra(ctypes.Structure):
                 ("translation", P)]
 
 
+class GtfExtractParams(ctypes.Structure):
+    _fields_ = [("p_accept", F64), ("fragment", I32), ("pad_", I32), ("separation_3d", F64),
+                ("merge_distance", F64), ("sigma0xy", F64), ("sigma0rz", F64), ("endcap_boundary", F64)]
+
+
+class GtfExtractIO(ctypes.Structure):
+    _fields_ = [("xyzr", P), ("vivl", P), ("sub_id", P), ("sub_ptr", P), ("n_sub", I32), ("pad_", I32),
+                ("order_key", P), ("gnn", P), ("label", P), ("status", P), ("pval_xy", P), ("pval_zr", P),
+                ("extracted", P), ("n_candidates", P)]
+
+
 class GtfKlGraph(ctypes.Structure):
     _fields_ = [("n_nodes", I32), ("n_slots", I32), ("slot_ptr", P), ("slot_src", P), ("gnn", P), ("truth", P),
                 ("pair_ptr", P), ("list", P * 4), ("count", I32 * 4)]
@@ -79,7 +90,8 @@ ERR_FLAGS = {
 SYMBOLS = ["gtf_workspace_bytes", "gtf_clear_errors", "gtf_read_errors", "gtf_extrapolate", "gtf_update",
            "gtf_message_passing", "gtf_node_ops",
            "gtf_cluster", "gtf_pass", "gtf_pass_ev", "gtf_tag_prepare", "gtf_tag_sweep", "gtf_parabolic_kl", "gtf_track_state_estimates", "gtf_pass_shard",
-           "gtf_shard_chunk_bytes", "gtf_shard_pack", "gtf_shard_unpack", "gtf_last_error",
+           "gtf_shard_chunk_bytes", "gtf_shard_pack", "gtf_shard_unpack", "gtf_extract_workspace_bytes",
+           "gtf_extract_candidates", "gtf_last_error",
            "gtf_version"]
 
 OPS = {"ranks": 1, "priors_tse": 2, "priors_uts": 3, "reweight_uts": 4, "degree": 5, "prune": 6, "mw_tse": 7,
@@ -112,6 +124,9 @@ def lib():
     L.gtf_pass_ev.argtypes = [G, N, S, S, E, PR, P, P, ctypes.POINTER(P)]
     L.gtf_tag_prepare.argtypes = [G, P, P, P, P, P]
     L.gtf_tag_sweep.argtypes = [G, P, P, P, P, P, P]
+    L.gtf_extract_workspace_bytes.restype = ctypes.c_size_t
+    L.gtf_extract_workspace_bytes.argtypes = [I32, I32]
+    L.gtf_extract_candidates.argtypes = [G, E, ctypes.POINTER(GtfExtractIO), ctypes.POINTER(GtfExtractParams), P, P]
     SH = ctypes.POINTER(GtfShard)
     L.gtf_pass_shard.argtypes = [G, N, S, S, E, PR, SH, P, P, ctypes.POINTER(P)]
     L.gtf_shard_chunk_bytes.restype = ctypes.c_size_t
@@ -125,7 +140,7 @@ def lib():
     for fn in ("gtf_clear_errors", "gtf_read_errors", "gtf_extrapolate", "gtf_update", "gtf_cluster", "gtf_pass",
                "gtf_pass_ev", "gtf_message_passing", "gtf_node_ops",
                "gtf_tag_prepare", "gtf_tag_sweep", "gtf_parabolic_kl", "gtf_track_state_estimates", "gtf_pass_shard", "gtf_shard_pack",
-               "gtf_shard_unpack"):
+               "gtf_shard_unpack", "gtf_extract_candidates"):
         getattr(L, fn).restype = ctypes.c_int
     _lib = L
     return L

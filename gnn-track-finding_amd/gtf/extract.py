@@ -1,0 +1,96 @@
+"""Track-candidate extraction on the GPU: host side of ``gtf_extract_candidates``.
+
+Mirrors src/extract/extract_track_candidates.py (:349-467): CCA over the activated
+edges, close-proximity merging, the one-hit-per-layer check and the xy / rz Kalman
+fits with chi-square p-values, per candidate on the device. This module turns the
+per-candidate device results into the stage's outputs (extracted candidates in the
+reference's order with their p-values, the remaining and fragment subgraphs) and, in
+:func:`extract_graphs`, into the reference's networkx objects.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _native as nat
+from .graph import TrackGraph
+
+FRAGMENT, BAD, REJECTED, EXTRACTED = 0, 1, 2, 3
+
+
+class Params:
+    """extract_track_candidates.py flags -p -n -s -t -e -z -b (run_gnn_trackml_mod.sh defaults)."""
+
+    def __init__(self, pval=0.01, numhits=4, separation_3d_threshold=10.0, threshold_distance_node_merging=8.0,
+                 sigma0xy=0.3, sigma0rz=0.4, endcap_boundary=550.0):
+        self.pval, self.numhits = float(pval), int(numhits)
+        self.separation = float(separation_3d_threshold)
+        self.merge = float(threshold_distance_node_merging)
+        self.sigma0xy, self.sigma0rz, self.endcap = float(sigma0xy), float(sigma0rz), float(endcap_boundary)
+
+    def c(self):
+        return nat.GtfExtractParams(self.pval, self.numhits, 0, self.separation, self.merge, self.sigma0xy,
+                                    self.sigma0rz, self.endcap)
+
+
+def run(g: TrackGraph, vivl, params: Params, order_key=None, device="cuda"):
+    """Run the extraction on the device for a packed graph (the pass's output).
+    vivl: [N, 2] (volume_id, in_volume_layer_id); order_key: optional [N] member order
+    inside a candidate (default node order). Returns a dict of host arrays."""
+    from .device import DeviceGraph
+    if params.numhits < 3:
+        raise ValueError("numhits must be >= 3 (rotate_track reads three hits)")
+    d = DeviceGraph(g, device)
+    torch = d.torch
+    dev = d.device
+    N = g.n_nodes
+    sub = g.node["sub_id"].astype(np.int32)
+    if N and (np.any(np.diff(sub) < 0) or sub[0] != 0 or np.any(np.diff(sub) > 1)):
+        raise ValueError("extraction needs nodes grouped by subgraph (sub_id 0, 1, 2, ... non-decreasing), "
+                         "as pack() numbers them")
+    n_sub = int(sub.max()) + 1 if N else 0
+    sub_ptr = np.searchsorted(sub, np.arange(n_sub + 1)).astype(np.int32)
+    up = lambda a, dt=None: torch.from_numpy(np.ascontiguousarray(a if dt is None else a.astype(dt))).to(dev)  # noqa
+    t = {"xyzr": up(g.node["xyzr"], np.float64), "vivl": up(np.asarray(vivl), np.float64), "sub": up(sub),
+         "sub_ptr": up(sub_ptr), "gnn": up(g.node["gnn"], np.float64),
+         "order": up(np.asarray(order_key), np.int32) if order_key is not None else None,
+         "label": torch.empty(max(N, 1), dtype=torch.int32, device=dev),
+         "status": torch.full((max(N, 1),), -1, dtype=torch.int8, device=dev),
+         "pxy": torch.full((max(N, 1),), float("nan"), dtype=torch.float64, device=dev),
+         "pzr": torch.full((max(N, 1),), float("nan"), dtype=torch.float64, device=dev),
+         "ext": torch.zeros(max(N, 1), dtype=torch.uint8, device=dev),
+         "ncand": torch.zeros(1, dtype=torch.int32, device=dev)}
+    ws = torch.zeros(int(d.lib.gtf_extract_workspace_bytes(N, n_sub)), dtype=torch.uint8, device=dev)
+    vp = lambda x: ctypes.c_void_p(x.data_ptr() if x is not None and x.numel() else 0)  # noqa: E731
+    io = nat.GtfExtractIO(vp(t["xyzr"]), vp(t["vivl"]), vp(t["sub"]), vp(t["sub_ptr"]), n_sub, 0, vp(t["order"]),
+                          vp(t["gnn"]), vp(t["label"]), vp(t["status"]), vp(t["pxy"]), vp(t["pzr"]),
+                          vp(t["ext"]), vp(t["ncand"]))
+    cp = params.c()
+    nat.check(d.lib.gtf_extract_candidates(ctypes.byref(d.cg), ctypes.byref(d.ce), ctypes.byref(io),
+                                           ctypes.byref(cp), vp(ws), d.stream))
+    out = {k: t[k][:N].cpu().numpy() for k in ("label", "status", "pxy", "pzr", "ext")}
+    out["gnn"] = t["gnn"].cpu().numpy().reshape(-1, 4)[:N]
+    out["n_candidates"] = int(t["ncand"].item())
+    return out
+
+
+def outputs(g: TrackGraph, res, fragment):
+    """The stage's outputs from the device results: extracted candidates (node index
+    arrays, in the reference's order), their p-values, remaining and fragment node
+    sets per subgraph (:423-430)."""
+    label, status, ext = res["label"], res["status"], res["ext"].astype(bool)
+    roots = np.unique(label)                          # candidate order = first-node order
+    extracted = [np.nonzero(label == r)[0] for r in roots if status[r] == EXTRACTED]
+    pxy = np.array([res["pxy"][r] for r in roots if status[r] == EXTRACTED])
+    pzr = np.array([res["pzr"][r] for r in roots if status[r] == EXTRACTED])
+    sub = g.node["sub_id"]
+    remaining, fragments = [], []
+    for s in range(int(sub.max()) + 1 if g.n_nodes else 0):
+        left = np.nonzero((sub == s) & ~ext)[0]
+        if 0 < len(left) < fragment:
+            fragments.append(left)
+        elif len(left) >= fragment:
+            remaining.append(left)
+    return {"extracted": extracted, "pval_xy": pxy, "pval_zr": pzr, "remaining": remaining,
+            "fragments": fragments}

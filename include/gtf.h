@@ -236,6 +236,45 @@ typedef struct gtf_tse_extra {
 int gtf_track_state_estimates(const gtf_graph* g, gtf_states* tse, const gtf_tse_extra* extra,
                               const gtf_params* p, gtf_stream_t stream);
 
+/* ---- Track-candidate extraction ---------------------------
+ * src/extract/extract_track_candidates.py main (:349-467) on the pass's output: CCA
+ * over the activated edges of each subgraph (a subgraph with no deactivated edge stays
+ * one candidate), then per candidate the fragment check, close-proximity merging (the
+ * reference mutates the merged node's GNN_Measurement in place, :111-114: io->gnn is
+ * updated the same way), the one-hit-per-layer check, rotate_track and the xy / rz
+ * Kalman fits with their chi-square p-values; a candidate is extracted when both
+ * p-values reach p_accept. Candidates are identified by their first node (min index). */
+typedef struct gtf_extract_params {
+    double p_accept;          /* -p */
+    int32_t fragment;         /* -n minimum hits (>= 3) */
+    int32_t pad_;
+    double separation_3d;     /* -s (rotate_track) */
+    double merge_distance;    /* -t (close-proximity merging) */
+    double sigma0xy, sigma0rz, endcap_boundary;   /* -e -z -b */
+} gtf_extract_params;
+
+typedef struct gtf_extract_io {
+    const double* xyzr;       /* [N*4] node attribute xyzr */
+    const double* vivl;       /* [N*2] volume_id, in_volume_layer_id */
+    const int32_t* sub_id;    /* [N]   subgraph of each node (nodes grouped by subgraph) */
+    const int32_t* sub_ptr;   /* [n_sub+1] first node of each subgraph */
+    int32_t n_sub;
+    int32_t pad_;
+    const int32_t* order_key; /* [N] member order inside a candidate (distinct values), or NULL = node order */
+    double* gnn;              /* [N*4] GNN_Measurement x,y,z,r: merged nodes get the midpoint */
+    int32_t* label;           /* [N] out: candidate id of each node */
+    int8_t* status;           /* [N] out per candidate id: 0 fragment, 1 bad layers, 2 rejected, 3 extracted */
+    double* pval_xy;          /* [N] out per candidate id (NaN when not fitted) */
+    double* pval_zr;
+    uint8_t* extracted;       /* [N] out per node */
+    int32_t* n_candidates;    /* device scalar out */
+} gtf_extract_io;
+
+size_t gtf_extract_workspace_bytes(int32_t n_nodes, int32_t n_sub);
+/* synchronises the stream once per connected-components round (a few rounds) */
+int gtf_extract_candidates(const gtf_graph* g, const gtf_edges* e, const gtf_extract_io* io,
+                           const gtf_extract_params* p, void* workspace, gtf_stream_t stream);
+
 /* ---- Parabolic-model KL training data -------------------------
  * learn_KL_parabolic_model/src/generate_training_data: the per-edge parabolic
  * state of compute_track_state_estimates (utils.py:221-289; S = diag(16, 0.01,

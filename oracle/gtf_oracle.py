@@ -733,3 +733,224 @@ def compute_track_state_estimates(g: TrackGraph, p):
         ang[v] = azimuth
         trans[v] = (xA, yA)
     return {"xy_mean_var": xy_mv, "zr_mean_var": zr_mv, "angle_of_rotation": ang, "translation": trans}
+
+
+# ---------------------------------------------------------------------------
+# candidate extraction (src/extract/extract_track_candidates.py, §8f next #1)
+# ---------------------------------------------------------------------------
+def active_components(g: TrackGraph):
+    """CCA (extract_track_candidates.py:332-346) per subgraph: weakly connected
+    components over the activated edges, in nx.weakly_connected_components order
+    (by first node), nodes ascending; a subgraph with no deactivated edge stays one
+    candidate (:342-343), connected or not. Returns a list of (subgraph, nodes)."""
+    N = g.n_nodes
+    sub = g.node["sub_id"]
+    parent = np.arange(N)
+
+    def find(a):
+        while parent[a] != a:
+            parent[a] = parent[parent[a]]
+            a = parent[a]
+        return a
+    dst = g.slot_dst()
+    ise = g.slot["is_edge"].astype(bool)
+    act = g.slot["act"] == 1
+    src = g.slot["slot_src"]
+    inactive_sub = np.zeros(int(sub.max()) + 1 if N else 0, bool)
+    for k in np.nonzero(ise)[0]:
+        u, v = int(src[k]), int(dst[k])
+        if act[k]:
+            ru, rv = find(u), find(v)
+            if ru != rv:
+                parent[max(ru, rv)] = min(ru, rv)
+        else:
+            inactive_sub[sub[v]] = True
+    out = []
+    starts = np.r_[0, np.nonzero(np.diff(sub))[0] + 1, N] if N else np.zeros(1, np.int64)
+    for a, b in zip(starts[:-1], starts[1:]):
+        s = int(sub[a])
+        nodes = np.arange(a, b)
+        if not inactive_sub[s]:
+            out.append((s, nodes))
+            continue
+        roots = np.array([find(v) for v in nodes])
+        seen = {}
+        for v, r in zip(nodes, roots):
+            seen.setdefault(r, []).append(v)
+        for r in sorted(seen, key=lambda r: seen[r][0]):
+            out.append((s, np.asarray(seen[r])))
+    return out
+
+
+def check_close_proximity_nodes(nodes, vivl, xyzr, gnn, threshold):
+    """extract_track_candidates.py:56-152 on one candidate (nodes in candidate order).
+    Mutates gnn (the shared GNN_Measurement objects) like the reference; returns
+    (assess_nodes, assess_xyzr, merged) -- the merged copy's nodes and coordinates, or
+    the candidate's own when no merge copy survives."""
+    ids = [tuple(vivl[v]) for v in nodes]
+    freq = {}
+    for x in ids:
+        freq[x] = freq.get(x, 0) + 1
+    fc = list(freq.values())
+    coords = {int(v): tuple(xyzr[v]) for v in nodes}
+    merged = False
+    copied = None
+    if 2 in fc:
+        rest = [c for c in fc if c != 2]
+        if len(fc) - len(rest) <= 2 and not any(c != 1 for c in rest):
+            dups = list(set([t for t in ids if ids.count(t) > 1]))
+            copied = (list(int(v) for v in nodes), dict(coords))
+            for dup in dups:
+                idx = [i for i, x in enumerate(ids) if x == dup]
+                noi = [int(nodes[i]) for i in idx]
+                if len(noi) == 2:
+                    n1, n2 = noi
+                    c1, c2 = copied[1][n1], copied[1][n2]
+                    dist = np.sqrt((c1[0] - c2[0])**2 + (c1[1] - c2[1])**2 + (c1[2] - c2[2])**2)
+                    if dist <= threshold:
+                        xm, ym, zm = (c1[0] + c2[0]) / 2, (c1[1] + c2[1]) / 2, (c1[2] + c2[2]) / 2
+                        rm = np.sqrt(xm**2 + ym**2)
+                        gnn[n1] = (xm, ym, zm, rm)
+                        copied[1][n1] = (xm, ym, zm, rm)
+                        copied[0].remove(n2)
+                        merged = True
+                    else:
+                        copied = None
+                        break
+                else:
+                    copied = None
+                    break
+    if copied is None:
+        return [int(v) for v in nodes], coords, merged
+    return copied[0], copied[1], merged
+
+
+def rotate_track(coords, separation_3d_threshold):                            # :176-195
+    p1, p2 = coords[-1], coords[-2]
+    d = np.sqrt((p1[0] - p2[0])**2 + (p1[1] - p2[1])**2 + (p1[2] - p2[2])**2)
+    if d < separation_3d_threshold:
+        p2 = coords[-3]
+    axy = atan2(p2[1] - p1[1], p2[0] - p1[0])
+    azr = atan2(p2[2] - p1[2], p2[3] - p1[3])
+    out = []
+    for c in coords:
+        x, y, z, r = c[0], c[1], c[2], c[3]
+        out.append((x * np.cos(axy) + y * np.sin(axy), -x * np.sin(axy) + y * np.cos(axy),
+                    -z * np.sin(azr) + z * np.cos(azr), r * np.cos(azr) + r * np.sin(azr)))
+    return out
+
+
+def _kf_step(x, P, F, Q, H, R, z):
+    """filterpy 1.4.5 predict() then update(z) (Q may be a scalar: broadcast, as filterpy)."""
+    x = F.dot(x)
+    P = F.dot(P).dot(F.T) + Q
+    y = z - H.dot(x)
+    PHT = P.dot(H.T)
+    S = H.dot(PHT) + R
+    K = PHT.dot(np.linalg.inv(S))
+    x = x + K.dot(y)
+    IKH = np.eye(len(x)) - K.dot(H)
+    P = IKH.dot(P).dot(IKH.T) + K.dot(R).dot(K.T)
+    return x, P
+
+
+def kf_track_fit_moliere(sigma0xy, sigma0rz, coords, endcap_boundary):         # :209-327
+    from scipy.stats import distributions
+    f_x = np.array([coords[0][1], 0., 0.])
+    f_P = np.array([[sigma0xy**2, 0., 0.], [0., 1., 0.], [0., 0., 1.]])
+    f_H = np.array([[1., 0., 0.]])
+    f_R = sigma0xy**2
+    g_x = np.array([coords[0][3], 0.])
+    g_P = np.array([[sigma0rz**2, 0.], [0., 1000.]])
+    g_H = np.array([[1., 0.]])
+    g_R = sigma0rz**2
+    c2xy, c2zr = [], []
+    for i in range(len(coords) - 1):
+        x2, y2 = coords[i][0], coords[i][1]
+        x3, y3 = coords[i + 1][0], coords[i + 1][1]
+        x1, y1 = .0, .0
+        denom = (x1 - x2) * (x1 - x3) * (x2 - x3)                              # calc_parabola_params
+        a = ((x3 * (y2 - y1)) + (x2 * (y1 - y3)) + (x1 * (y3 - y2))) / denom
+        b = ((x3**2 * (y1 - y2)) + (x2**2 * (y3 - y1)) + (x1**2 * (y2 - y3))) / denom
+        z2, r2 = coords[i][2], coords[i][3]
+        z3, r3 = coords[i + 1][2], coords[i + 1][3]
+        dr, dz = r3 - r2, z3 - z2
+        hyp = np.sqrt(dr**2 + dz**2)
+        sin_t = np.abs(dr) / hyp
+        kappa = (2 * a) / (1 + ((2 * a * x3) + b)**2)**1.5
+        var_ms = sin_t * ((13.6 * 1e-3 * np.sqrt(0.02) * kappa) / 0.3)**2
+        if np.abs(z3) >= endcap_boundary:
+            var_ms = var_ms * np.abs(dr / dz)
+        dx = x3 - x2
+        alpha = 0.1
+        e1 = np.exp(-np.abs(dx) * alpha)
+        f1 = (1.0 - e1) / alpha
+        g1 = (np.abs(dx) - f1) / alpha
+        sw2 = 0.00001**2
+        st2 = var_ms
+        dx2 = dx**2
+        dxw2 = dx2 * sw2
+        Q02 = 0.5 * dxw2
+        Q01 = dx * (st2 + Q02)
+        Q12 = dx * sw2
+        F = np.array([[1., dx, g1], [0., 1., f1], [0., 0., e1]])
+        Q = np.array([[dx2 * (st2 + 0.25 * dxw2), Q01, Q02], [Q01, st2 + dxw2, Q12], [Q02, Q12, sw2]])
+        f_x, f_P = _kf_step(f_x, f_P, F, Q, f_H, f_R, y3)
+        res = y3 - f_H.dot(f_x)
+        S = f_H.dot(f_P).dot(f_H.T) + f_R
+        c2xy.append(res.T.dot(np.linalg.inv(S)).dot(res))
+        G = np.array([[1., dz], [0., 1.]])
+        g_x, g_P = _kf_step(g_x, g_P, G, var_ms, g_H, g_R, r3)
+        res = r3 - g_H.dot(g_x)
+        S = g_H.dot(g_P).dot(g_H.T) + g_R
+        c2zr.append(res.T.dot(np.linalg.inv(S)).dot(res))
+    dof = len(coords) - 2
+    return (float(distributions.chi2.sf(sum(c2xy), dof)), float(distributions.chi2.sf(sum(c2zr), dof)))
+
+
+def extract_candidates(g: TrackGraph, vivl, p_accept, fragment, separation, merge_threshold, sigma0xy,
+                       sigma0rz, endcap_boundary):
+    """extract_track_candidates.main (:349-467) on the packed graph. vivl: [N,2]
+    (volume_id, in_volume_layer_id). Candidate node order is ascending node index
+    (the reference iterates networkx subgraph views, whose order can follow a Python
+    set for small components). Returns extracted candidates (node
+    index arrays) with p-values in extraction order, remaining and fragment node
+    sets, the mutated GNN coordinates, and per-candidate records."""
+    gnn = g.node["gnn"].copy()
+    xyzr = g.node["xyzr"]
+    comps = active_components(g)
+    extracted, pxy, pzr, records = [], [], [], []
+    removed = np.zeros(g.n_nodes, bool)
+    for s, nodes in comps:
+        rec = {"sub": s, "nodes": nodes, "status": "fragment", "pval_xy": np.nan, "pval_zr": np.nan}
+        records.append(rec)
+        if len(nodes) < fragment:
+            continue
+        an, ac, merged = check_close_proximity_nodes(nodes, vivl, xyzr, gnn, merge_threshold)
+        rec["merged"] = merged
+        ids = [tuple(vivl[v]) for v in an]
+        if not (len(ids) == len(set(ids)) and len(set(ids)) >= fragment):
+            rec["status"] = "bad"
+            continue
+        coords = sorted([ac[v] for v in an], key=lambda c: c[3], reverse=True)
+        coords = rotate_track(coords, separation)
+        pv, pz = kf_track_fit_moliere(sigma0xy, sigma0rz, coords, endcap_boundary)
+        rec["pval_xy"], rec["pval_zr"] = pv, pz
+        if pv >= p_accept and pz >= p_accept:
+            rec["status"] = "extracted"
+            extracted.append(np.asarray(nodes))
+            pxy.append(pv)
+            pzr.append(pz)
+            removed[nodes] = True
+        else:
+            rec["status"] = "rejected"
+    sub = g.node["sub_id"]
+    remaining, fragments = [], []
+    for s in range(int(sub.max()) + 1 if g.n_nodes else 0):
+        left = np.nonzero((sub == s) & ~removed)[0]
+        if 0 < len(left) < fragment:
+            fragments.append(left)
+        elif len(left) >= fragment:
+            remaining.append(left)
+    return {"extracted": extracted, "pval_xy": np.asarray(pxy), "pval_zr": np.asarray(pzr),
+            "remaining": remaining, "fragments": fragments, "gnn_after": gnn, "records": records}

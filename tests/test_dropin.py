@@ -242,3 +242,45 @@ def test_networkx_builder_reproduces_reference_dict_order():
             exp = [int(S["slot_key"][k]) for _, k in sorted((S["tse_rank"][k], k) for k in range(lo, hi)
                                                             if S["tse_rank"][k] >= 0)]
             assert [int(k) for k in keys] == exp, n
+
+
+@pytest.mark.gpu
+def test_dropin_extract_track_candidates_cli(tmp_path):
+    """the drop-in extraction CLI on the reference's stage input (150 subgraphs of the
+    iteration-1 network): same candidates / remaining / fragments in the same files,
+    same edges, same GNN_Measurement coordinates after merging, p-values 1e-7"""
+    d = _load("extract")
+    a = d["args"]
+    dirs = {k: str(tmp_path / k) + "/" for k in ("in", "cand", "rem", "frag")}
+    for v in dirs.values():
+        os.makedirs(v)
+    for i, s in enumerate(d["input"]):
+        with open(dirs["in"] + "%d_subgraph.gpickle" % i, "wb") as f:
+            pickle.dump(s, f, pickle.HIGHEST_PROTOCOL)
+    cmd = [sys.executable, os.path.join(PKG, "extract", "extract_track_candidates.py"), "-i", dirs["in"],
+           "-c", dirs["cand"], "-r", dirs["rem"], "-f", dirs["frag"], "-p", str(a["p"]), "-n", str(a["n"]),
+           "-s", str(a["s"]), "-t", str(a["t"]), "-a", str(a["a"]), "-e", str(d["P"]["sigma0xy"]),
+           "-z", str(d["P"]["sigma0rz"]), "-b", str(d["P"]["endcap_boundary"])]
+    subprocess.check_call(cmd, cwd=ROOT)
+
+    def read(dd):
+        out, i = [], 0
+        while os.path.isfile(dd + "%d_subgraph.gpickle" % i):
+            with open(dd + "%d_subgraph.gpickle" % i, "rb") as f:
+                out.append(pickle.load(f))
+            i += 1
+        return out
+    for key, dd in (("candidates", "cand"), ("remaining", "rem"), ("fragments", "frag")):
+        got, exp = read(dirs[dd]), d[key]
+        assert len(got) == len(exp), key
+        for gs, es in zip(got, exp):
+            assert list(gs.nodes) == list(es.nodes), key
+            assert sorted(gs.edges) == sorted(es.edges), key
+            assert gs.graph == es.graph, key
+            for n in es.nodes:
+                ge, ee = gs.nodes[n]["GNN_Measurement"], es.nodes[n]["GNN_Measurement"]
+                assert (ge.x, ge.y, ge.z, ge.r) == (ee.x, ee.y, ee.z, ee.r), (key, n)
+    import pandas as pd
+    pv = pd.read_csv(dirs["cand"] + "pvals.csv")[["pvals_xy", "pvals_zr"]].to_numpy()
+    assert pv.shape == d["pvals"].shape
+    assert np.all(np.abs(pv - d["pvals"]) <= 1e-7 * np.abs(d["pvals"]) + 1e-300)

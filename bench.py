@@ -238,6 +238,11 @@ def main():
     cands.update({k: v for k, v in kern.items() if v[1] is not None})
     name = max(cands, key=lambda k: cands[k][0])
     ms, nbytes = cands[name]
+    # every kernel of the pass against the HBM roofline (algorithmic bytes / its time)
+    per_kernel = {k: {"ms": round(v[0], 5), "algorithmic_bytes": v[1],
+                      "achieved_GBps": v[1] / (v[0] * 1e-3) / 1e9,
+                      "frac": v[1] / (v[0] * 1e-3) / 1e9 / rf.HBM_PEAK_GBS,
+                      "traffic_bytes": committed_traffic(args.workload, k)} for k, v in cands.items()}
     achieved = nbytes / (ms * 1e-3) / 1e9
     traffic = committed_traffic(args.workload, name)
 
@@ -277,6 +282,7 @@ def main():
                        "parallelism": "event-parallel x%d (no collective)" % world,
                        "pass": "gtf_pass: extrapolate (a6-a8) + update (a3,a9,a10x2,a11) + KL cluster (a12-a14)"},
             "kernel_ms": {k: round(v[0], 5) for k, v in kern.items()},
+            "kernels_roofline": per_kernel,
             "roofline": {"bound": "hbm", "kernel": name, "achieved": achieved, "peak": rf.HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / rf.HBM_PEAK_GBS, "traffic": traffic,
                          "algorithmic_bytes_per_launch": nbytes, "kernel_ms": ms,

@@ -273,7 +273,8 @@ struct StageT {
     double a[CAP], b[CAP], c[CAP], tau[CAP];
     double c00[CAP], c01[CAP], c10[CAP], c11[CAP], c22[CAP];
     double i00[CAP], i01[CAP], i10[CAP], i11[CAP], i22[CAP];
-    double q[CAP], w[CAP], tg[CAP], sz2[CAP], sr2[CAP], prior[CAP];
+    double q[CAP], w[CAP], tg[CAP], prior[CAP];
+    uint8_t ec[CAP];  // neighbour in the endcap (|x| >= boundary): picks its sigma_z / sigma_r pair
 };
 
 template <typename Stage>
@@ -285,9 +286,12 @@ __device__ __forceinline__ Cov5 stage_inv(const Stage* s, int i) {
     return Cov5{s->i00[i], s->i01[i], s->i10[i], s->i11[i], s->i22[i]};
 }
 template <typename Stage>
-__device__ __forceinline__ TauGeo stage_geo(const Stage* s, int i) {
+__device__ __forceinline__ TauGeo stage_geo(const Stage* s, int i, double szb2, double srb2) {
     TauGeo t;
-    t.q = s->q[i]; t.w = s->w[i]; t.tau = s->tg[i]; t.sz2 = s->sz2[i]; t.sr2 = s->sr2[i];
+    t.q = s->q[i]; t.w = s->w[i]; t.tau = s->tg[i];
+    const bool ec = s->ec[i];   // endcap swaps the barrel pair (tau_geo)
+    t.sz2 = ec ? srb2 : szb2;
+    t.sr2 = ec ? szb2 : srb2;
     return t;
 }
 
@@ -323,10 +327,12 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
         stg->i22[pos] = I.c22;
         const TauGeo t = tau_geo(S.xyzr[4 * k], S.xyzr[4 * k + 2], S.xyzr[4 * k + 3], za, ra, p.sigma0rz2, p.sigma0rz,
                                  p.sigma0rz, p.sigma0rz2, p.endcap_boundary);
-        stg->q[pos] = t.q; stg->w[pos] = t.w; stg->tg[pos] = t.tau; stg->sz2[pos] = t.sz2; stg->sr2[pos] = t.sr2;
+        stg->q[pos] = t.q; stg->w[pos] = t.w; stg->tg[pos] = t.tau;
+        stg->ec[pos] = fabs(S.xyzr[4 * k]) >= p.endcap_boundary;
         stg->prior[pos] = st.prior;
     }
     wave_lds_sync();
+    const double szb2 = p.sigma0rz2 * p.sigma0rz2, srb2 = p.sigma0rz * p.sigma0rz;   // barrel sigma_z^2, sigma_r^2
     const bool ec = fabs(xa) >= p.endcap_boundary;
     const double sza = ec ? p.sigma0rz : p.sigma0rz2, sra = ec ? p.sigma0rz2 : p.sigma0rz;
     const double sza2 = sza * sza, sra2 = sra * sra;
@@ -339,7 +345,8 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
         int i, j;
         pair_ij(t, i, j);
         const double D = mahalanobis_geo(stg->a[i], stg->b[i], stage_cov(stg, i), stg->a[j], stg->b[j],
-                                         stage_cov(stg, j), sza2, sra2, stage_geo(stg, i), stage_geo(stg, j));
+                                         stage_cov(stg, j), sza2, sra2, stage_geo(stg, i, szb2, srb2),
+                                         stage_geo(stg, j, szb2, srb2));
         if (D == 0.0) continue;  // zeros are excluded (np.nonzero)
         lnz = true;
         if (D != D) { lnan = true; continue; }
@@ -543,12 +550,13 @@ struct Buckets {
     int32_t blocks[4];
 };
 
-constexpr size_t stage_bytes(int G) { return (size_t)(BLOCK / G) * 20 * (G < 16 ? G : 16) * sizeof(double); }
+template <int G>
+constexpr size_t stage_bytes() { return (size_t)(BLOCK / G) * sizeof(StageT<(G < 16 ? G : 16)>); }
 constexpr size_t node_smem_bytes() {
-    size_t m = stage_bytes(8);
-    m = stage_bytes(16) > m ? stage_bytes(16) : m;
-    m = stage_bytes(32) > m ? stage_bytes(32) : m;
-    m = stage_bytes(64) > m ? stage_bytes(64) : m;
+    size_t m = stage_bytes<8>();
+    m = stage_bytes<16>() > m ? stage_bytes<16>() : m;
+    m = stage_bytes<32>() > m ? stage_bytes<32>() : m;
+    m = stage_bytes<64>() > m ? stage_bytes<64>() : m;
     return BLOCK * sizeof(double) + m;
 }
 

@@ -34,14 +34,19 @@ class Params:
                                     self.sigma0rz, self.endcap)
 
 
-def run(g: TrackGraph, vivl, params: Params, order_key=None, device="cuda"):
+def run(g: TrackGraph, vivl, params: Params, order_key=None, device="cuda", d=None):
     """Run the extraction on the device for a packed graph (the pass's output).
     vivl: [N, 2] (volume_id, in_volume_layer_id); order_key: optional [N] member order
-    inside a candidate (default node order). Returns a dict of host arrays."""
+    inside a candidate (default node order); d: the DeviceGraph of ``g`` already in HBM
+    (a stage just ran on it: its activation mask is read in place), else ``g`` is
+    uploaded. Returns a dict of host arrays."""
     from .device import DeviceGraph
     if params.numhits < 3:
         raise ValueError("numhits must be >= 3 (rotate_track reads three hits)")
-    d = DeviceGraph(g, device)
+    if d is None:
+        d = DeviceGraph(g, device)
+    elif d.n_nodes != g.n_nodes or d.n_slots != g.n_slots:
+        raise ValueError("DeviceGraph does not hold this graph")
     torch = d.torch
     dev = d.device
     N = g.n_nodes

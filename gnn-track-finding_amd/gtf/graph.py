@@ -474,3 +474,98 @@ def concat(graphs: List[TrackGraph]) -> TrackGraph:
                      out_slot.astype(np.int32), node, slot, int(sub_off[-1]))
     check_layout(out)
     return out
+
+
+# --------------------------------------------------------------------------
+# subset: the graph a stage saves after removing nodes (extraction)
+# --------------------------------------------------------------------------
+def subset(g: TrackGraph, keep) -> TrackGraph:
+    """The packed form of the reference's ``subGraph.remove_nodes_from(extracted)``
+    (extract_track_candidates.py:459-467) followed by dropping the fragment
+    subgraphs: nodes with ``keep`` set survive, in order. Equal to ``pack()`` of the
+    reduced networkx graphs, array for array:
+
+    * a kept receiver keeps a slot per remaining dict key: senders still in the
+      graph first (by node index), then the removed senders whose keys stay in its
+      state dicts as orphans (slot_src = -1, no edge), in the key order pack()
+      discovers them -- track_state_estimates order, then updated_track_states;
+    * slots whose key was neither an edge nor a dict entry disappear;
+    * successor order of the out view is kept; ``sub_id`` is renumbered densely
+      (the saved subgraphs are numbered 0..k-1).
+    """
+    keep = np.asarray(keep, dtype=bool)
+    N, S = g.n_nodes, g.n_slots
+    if keep.shape != (N,):
+        raise ValueError("keep must be a bool mask over the %d nodes" % N)
+    new_idx = np.full(N, -1, np.int64)
+    new_idx[keep] = np.arange(int(keep.sum()))
+    dst = g.slot_dst().astype(np.int64)
+    src = g.slot["slot_src"].astype(np.int64)
+    kr = keep[dst] if S else np.zeros(0, bool)
+    inside = kr & (src >= 0) & keep[np.maximum(src, 0)]
+    edge = inside & g.slot["is_edge"].astype(bool)
+    tr, ur = g.slot["tse_rank"].astype(np.int64), g.slot["uts_rank"].astype(np.int64)
+    orphan = kr & ~inside & ((tr >= 0) | (ur >= 0))
+    ks = np.nonzero(edge | (inside & ((tr >= 0) | (ur >= 0))) | orphan)[0]
+    big = np.int64(1) << 40
+    minor = np.where(inside[ks], new_idx[np.maximum(src[ks], 0)],
+                     big + np.where(tr[ks] >= 0, tr[ks], big + ur[ks]))
+    ks = ks[np.lexsort((minor, new_idx[dst[ks]]))]
+    n2 = int(keep.sum())
+    s2 = ks.size
+    slot_ptr = np.zeros(n2 + 1, np.int64)
+    np.add.at(slot_ptr, new_idx[dst[ks]] + 1, 1)
+    slot_ptr = np.cumsum(slot_ptr)
+    slot = {k: v[ks].copy() for k, v in g.slot.items()}
+    orph = ~inside[ks]
+    slot["slot_src"] = np.where(orph, -1, new_idx[np.maximum(src[ks], 0)]).astype(np.int32)
+    for name in ("is_edge", "rev_edge", "act"):
+        slot[name][orph] = 0
+    slot["is_edge"][~orph] = g.slot["is_edge"][ks][~orph]
+    for name in ("edge_mw", "send_mw"):
+        slot[name][orph] = NAN
+    slot["uts_fresh"][:] = 0
+    # out view: successors still in the graph, order kept
+    old2new = np.full(S, -1, np.int64)
+    old2new[ks] = np.arange(s2)
+    osl = g.out_slot.astype(np.int64)
+    owner = np.repeat(np.arange(N, dtype=np.int64), np.diff(g.out_ptr.astype(np.int64)))
+    ok = keep[owner] & (old2new[osl] >= 0) if osl.size else np.zeros(0, bool)
+    ok &= edge[osl] if osl.size else ok
+    out_slot = old2new[osl[ok]].astype(np.int32)
+    out_ptr = np.zeros(n2 + 1, np.int64)
+    np.add.at(out_ptr, new_idx[owner[ok]] + 1, 1)
+    out_ptr = np.cumsum(out_ptr)
+    node = {k: v[keep].copy() for k, v in g.node.items()}
+    if n2:
+        _, node["sub_id"] = np.unique(node["sub_id"], return_inverse=True)
+        node["sub_id"] = node["sub_id"].astype(np.int32)
+    out = TrackGraph(n2, s2, slot_ptr.astype(np.int32), out_ptr.astype(np.int32), out_slot, node, slot,
+                     int(node["sub_id"].max()) + 1 if n2 else 0)
+    check_layout(out)
+    return out
+
+
+def refresh_send_mw(g: TrackGraph) -> TrackGraph:
+    """send_mw[k] of the edge u -> v = u's track_state_estimates[v]['mixture_weight'],
+    read from the slot (receiver u, key v) -- after a device stage rewrote tse_mw
+    (compute_mixture_weights, helper.py:76-96). Absent entry -> NaN (as pack())."""
+    S = g.n_slots
+    dst = g.slot_dst().astype(np.int64)
+    src = g.slot["slot_src"].astype(np.int64)
+    N = max(g.n_nodes, 1)
+    ins = np.nonzero(src >= 0)[0]
+    code = dst[ins] * N + src[ins]                 # slot (receiver, sender)
+    order = np.argsort(code, kind="stable")
+    sc = code[order]
+    e = np.nonzero(g.slot["is_edge"].astype(bool))[0]
+    want = src[e] * N + dst[e]                     # reverse slot (receiver u, sender v)
+    pos = np.searchsorted(sc, want)
+    pos_c = np.minimum(pos, max(sc.size - 1, 0))
+    hit = (pos < sc.size) & (sc[pos_c] == want) if sc.size else np.zeros(e.size, bool)
+    mw = np.full(S, NAN)
+    rk = ins[order[pos_c[hit]]]
+    vals = np.where(g.slot["tse_rank"][rk] >= 0, g.slot["tse_mw"][rk], NAN)
+    mw[e[hit]] = vals
+    g.slot["send_mw"] = mw
+    return g

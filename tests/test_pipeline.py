@@ -1,0 +1,117 @@
+"""The whole track-finding loop (run_gnn_trackml_mod.sh:61-146, iterations 1-3) on
+the committed volume-7 event, against the reference's own run of it
+(tests/golden/pipeline_vol7.npz, make_golden_pipeline.py).
+
+The reference numbers its output files in glob() order, so candidates, remaining and
+fragment subgraphs are compared as sets of node-id sets; each candidate's p-values
+follow it. Bars: every set exact; p-values 1e-9 relative for the oracle (same numpy
+calls as the reference) and 1e-7 for the GPU (test_extract.py explains the margin).
+
+The oracle loop runs the CPU restatement's stages on the same packed graphs and the
+same host subset step (gtf.graph.subset) the device pipeline uses, so it pins both
+the restatement's stage chain and that host logic against the reference."""
+import os
+
+import numpy as np
+import pytest
+
+import gtf_oracle as O
+from fixtures import GOLDEN
+from gtf.graph import refresh_send_mw, subset
+from gtf.params import Params
+
+PREFIX = os.path.join(GOLDEN, "kat134", "event_1_filtered_graph_")
+EX = dict(p_accept=0.01, fragment=4, separation=10.0, merge_threshold=8.0, sigma0xy=0.3, sigma0rz=0.4,
+          endcap_boundary=550.0)
+
+
+def _fixture():
+    z = np.load(os.path.join(GOLDEN, "pipeline_vol7.npz"), allow_pickle=False)
+    out = {}
+    for it in (1, 2, 3):
+        grp = {}
+        for name in ("cand", "rem", "frag"):
+            ptr, ids = z["it%d__%s_ptr" % (it, name)], z["it%d__%s_ids" % (it, name)]
+            grp[name] = [frozenset(int(x) for x in ids[ptr[i]:ptr[i + 1]]) for i in range(len(ptr) - 1)]
+        grp["pval"] = {c: (a, b) for c, a, b in zip(grp["cand"], z["it%d__pval_xy" % it], z["it%d__pval_zr" % it])}
+        out[it] = grp
+    return out
+
+
+def _pclose(a, b, rtol):
+    if a == b:
+        return True
+    if abs(a - b) <= rtol * abs(b):
+        return True
+    return a > 0 and b > 0 and abs(np.log(a) - np.log(b)) <= rtol * abs(np.log(b))
+
+
+def _check(it, cands, pxy, pzr, rem, frag, exp, rtol):
+    e = exp[it]
+    got = [frozenset(int(x) for x in c) for c in cands]
+    assert len(got) == len(e["cand"]), (it, len(got), len(e["cand"]))
+    assert set(got) == set(e["cand"]), it
+    for c, a, b in zip(got, pxy, pzr):
+        ea, eb = e["pval"][c]
+        assert _pclose(float(a), float(ea), rtol) and _pclose(float(b), float(eb), rtol), (it, sorted(c), a, ea, b, eb)
+    assert set(frozenset(int(x) for x in r) for r in rem) == set(e["rem"]), it
+    assert len(rem) == len(e["rem"])
+    assert set(frozenset(int(x) for x in f) for f in frag) == set(e["frag"]), it
+    assert len(frag) == len(e["frag"])
+
+
+def _oracle_loop(iterations=3):
+    from gtf.pipeline import CLUSTER_FIRST, CLUSTER_LATER, event_layout
+    p = Params()
+    g, vivl = event_layout(PREFIX, 7, 7)
+    O.compute_track_state_estimates(g, p)
+    O.compute_prior_probabilities(g, "tse")
+    O.compute_mixture_weights(g, "tse")
+    O.query_node_degree_in_edges(g)
+    refresh_send_mw(g)
+    res = []
+    for it in range(1, iterations + 1):
+        if it == 1:
+            O.cluster_stage(g, "tse", CLUSTER_FIRST[0], CLUSTER_FIRST[1], p)
+        elif it % 2 == 0:
+            O.extrapolate_stage(g, p)
+        else:
+            O.cluster_stage(g, "uts", CLUSTER_LATER[0], CLUSTER_LATER[1], p)
+        r = O.extract_candidates(g, vivl, **EX)
+        nid = g.node["node_id"]
+        res.append(([nid[c] for c in r["extracted"]], r["pval_xy"], r["pval_zr"], [nid[c] for c in r["remaining"]],
+                    [nid[c] for c in r["fragments"]]))
+        keep = np.zeros(g.n_nodes, bool)
+        for c in r["remaining"]:
+            keep[c] = True
+        g.node["gnn"] = r["gnn_after"]
+        g = subset(g, keep)
+        refresh_send_mw(g)
+        vivl = vivl[keep]
+        if it % 2 == 0:
+            O.update_stage(g, p)
+    return res
+
+
+def test_oracle_pipeline_matches_reference_run():
+    exp = _fixture()
+    for it, r in enumerate(_oracle_loop(), 1):
+        _check(it, *r, exp, 1e-9)
+
+
+def test_fixture_counts():
+    """the reference's own run: 1055/160/491, 110/129/10, 2/129/0"""
+    exp = _fixture()
+    assert [(len(exp[i]["cand"]), len(exp[i]["rem"]), len(exp[i]["frag"])) for i in (1, 2, 3)] == \
+        [(1055, 160, 491), (110, 129, 10), (2, 129, 0)]
+
+
+@pytest.mark.gpu
+def test_gpu_pipeline_matches_reference_run():
+    from gtf import pipeline
+    exp = _fixture()
+    g, vivl = pipeline.build_event(PREFIX, 7, 7)
+    its = pipeline.run(g, vivl, iterations=3)
+    assert [i.index for i in its] == [1, 2, 3]
+    for i in its:
+        _check(i.index, i.candidates, i.pval_xy, i.pval_zr, i.remaining, i.fragments, exp, 1e-7)

@@ -22,12 +22,15 @@ from .graph import TrackGraph
 
 
 def read_nodes(path: str, min_volume: int, max_volume: int):
-    a = np.genfromtxt(path, delimiter=",", names=True, dtype=None, encoding=None)
+    """the reference's pandas parser (helper.load_nodes_edges, helper.py:524-531)"""
+    import pandas as pd
+    a = pd.read_csv(path)
     lo, hi = min_volume * 1000, (max_volume + 1) * 1000
-    keep = (a["layer_id"] >= lo) & (a["layer_id"] <= hi)
-    a = a[keep]
-    x, y, z = a["x"].astype(np.float64), a["y"].astype(np.float64), a["z"].astype(np.float64)
-    return a["node_idx"].astype(np.int64), x, y, z, np.sqrt(x**2 + y**2), a["layer_id"].astype(np.int64)
+    lid = a["layer_id"].to_numpy()
+    keep = (lid >= lo) & (lid <= hi)
+    x, y, z = (a[c].to_numpy(np.float64)[keep] for c in ("x", "y", "z"))
+    return (a["node_idx"].to_numpy(np.int64)[keep], x, y, z, np.sqrt(x**2 + y**2),
+            lid[keep].astype(np.int64))
 
 
 def read_edges(path: str):
@@ -104,3 +107,52 @@ def build_networkx(event_prefix: str, min_volume: int, max_volume: int, truth_cs
             G.add_edge(b, a)
     G = nx.DiGraph(G)
     return [G.subgraph(c).copy() for c in nx.weakly_connected_components(G)]
+
+
+def build_event_csr(event_prefix: str, min_volume: int, max_volume: int):
+    """Event conversion's graph straight to the packed CSR (gtf_build_event_csr):
+    the same TrackGraph as pack() of build_networkx's subgraphs with their
+    track_state_estimates keys in the reference's set order, without networkx.
+    Returns (graph with empty states -- every edge active, has_tse set, tse_rank in
+    dict order -- and vivl [N, 2] = (volume_id, in_volume_layer_id))."""
+    import ctypes
+    from . import _native as nat
+    from .graph import NODE_FIELDS, SLOT_FIELDS, check_layout, empty_arrays
+    ids, x, y, z, r, layer = read_nodes(event_prefix + "nodes.csv", min_volume, max_volume)
+    n2, n1 = read_edges(event_prefix + "edges.csv")
+    N, R = int(ids.size), int(n1.size)
+    ids = np.ascontiguousarray(ids, np.int64)
+    a, b = np.ascontiguousarray(n1, np.int64), np.ascontiguousarray(n2, np.int64)
+    o = {"order": np.zeros(max(N, 1), np.int32), "sub_id": np.zeros(max(N, 1), np.int32),
+         "slot_ptr": np.zeros(N + 1, np.int32), "out_ptr": np.zeros(N + 1, np.int32),
+         "slot_src": np.zeros(max(2 * R, 1), np.int32), "tse_rank": np.zeros(max(2 * R, 1), np.int32),
+         "out_slot": np.zeros(max(2 * R, 1), np.int32)}
+    vp = lambda t: ctypes.c_void_p(t.ctypes.data)  # noqa: E731
+    ev = nat.GtfEventCsr(N, R, vp(ids) if N else None, vp(a) if R else None, vp(b) if R else None,
+                         vp(o["order"]), vp(o["sub_id"]), vp(o["slot_ptr"]), vp(o["slot_src"]), vp(o["tse_rank"]),
+                         vp(o["out_ptr"]), vp(o["out_slot"]), 0, 0, 0)
+    nat.check(nat.lib().gtf_build_event_csr(ctypes.byref(ev)))
+    E = int(ev.n_edges)
+    order = o["order"][:N].astype(np.int64)
+    node, slot = empty_arrays(NODE_FIELDS, N), empty_arrays(SLOT_FIELDS, E)
+    gnn = np.stack([x, y, z, r], axis=1)[order]
+    node["gnn"] = gnn
+    node["xyzr"] = gnn.copy()
+    node["layer"] = (layer[order] % 100).astype(np.float64)
+    node["has_tse"][:] = 1
+    node["tag"] = ids[order]
+    node["node_id"] = ids[order]
+    node["sub_id"] = o["sub_id"][:N].copy()
+    src = o["slot_src"][:E].copy()
+    slot["slot_src"] = src
+    slot["slot_key"] = ids[order][src] if E else np.zeros(0, np.int64)
+    slot["is_edge"][:] = 1
+    slot["rev_edge"][:] = 1
+    slot["act"][:] = 1
+    slot["tse_rank"] = o["tse_rank"][:E].copy()
+    g = TrackGraph(N, E, o["slot_ptr"].copy(), o["out_ptr"].copy(), o["out_slot"][:E].copy(), node, slot,
+                   int(ev.n_subgraphs))
+    check_layout(g)
+    lay = layer[order]
+    vivl = np.stack([(lay / 1000).astype(np.int64), lay % 100], 1).astype(np.float64)
+    return g, vivl

@@ -16,12 +16,12 @@ the extraction's verdict (:func:`gtf.graph.subset`, the packed form of
 coordinate mutation (close-proximity merging, extract_track_candidates.py:91-118)
 carried over.
 
-Event conversion (:func:`build_event`, event_conversion.py:53-101): the networkx
-graph and its orders come from :func:`gtf.io.build_networkx` (the reference's node,
-successor and weakly-connected-component orders, and the set order of the
-track_state_estimates keys, helper.py:277,350-351); the states, priors, mixture
-weights and degrees are computed on the device (gtf_track_state_estimates +
-gtf_node_ops).
+Event conversion (:func:`build_event`, event_conversion.py:53-101): the packed graph
+and its orders come from gtf_build_event_csr (csrc/gtf_build.cpp: the reference's
+node, successor and weakly-connected-component orders and the set order of the
+track_state_estimates keys, helper.py:277,350-351, without networkx); the states,
+priors, mixture weights and degrees are computed on the device
+(gtf_track_state_estimates + gtf_node_ops).
 """
 from __future__ import annotations
 
@@ -53,12 +53,20 @@ class Iteration:
     seconds: dict
 
 
-def event_layout(event_prefix: str, min_volume: int, max_volume: int):
+def event_layout(event_prefix: str, min_volume: int, max_volume: int, builder: str = "native"):
     """Host half of event conversion: the packed network in the reference's orders,
     with empty track_state_estimates dicts keyed in their set order and every edge
-    active (helper.initialize_edge_activation). Returns (graph, vivl[N, 2])."""
-    import networkx as nx
+    active (helper.initialize_edge_activation). Returns (graph, vivl[N, 2]).
+
+    builder "native": gtf_build_event_csr (C++, CSV rows -> CSR, CPython set orders
+    reproduced); "networkx": the reference's own construction through networkx and
+    pack() (gtf.io.build_networkx) -- the slow path the native one is tested against."""
     from . import io
+    if builder == "native":
+        return io.build_event_csr(event_prefix, min_volume, max_volume)
+    if builder != "networkx":
+        raise ValueError("builder must be 'native' or 'networkx'")
+    import networkx as nx
     subs = io.build_networkx(event_prefix, min_volume, max_volume)
     for G in subs:
         for node in G.nodes():
@@ -71,12 +79,13 @@ def event_layout(event_prefix: str, min_volume: int, max_volume: int):
     return g, vivl
 
 
-def build_event(event_prefix: str, min_volume: int, max_volume: int, p: Params = None, device="cuda"):
+def build_event(event_prefix: str, min_volume: int, max_volume: int, p: Params = None, device="cuda",
+                builder: str = "native"):
     """event_conversion.py:53-101: CSVs -> packed network with track_state_estimates,
     activation 1, priors, mixture weights and degrees. Returns (graph, vivl[N, 2])."""
     from .device import DeviceGraph
     p = p or Params()
-    g, vivl = event_layout(event_prefix, min_volume, max_volume)
+    g, vivl = event_layout(event_prefix, min_volume, max_volume, builder)
     if g.n_nodes == 0:
         return g, vivl
     d = DeviceGraph(g, device)

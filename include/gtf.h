@@ -320,6 +320,33 @@ typedef struct gtf_kl_out {
  * config-5 tolerance sweep). sv/cov outputs are fp64 in both modes. */
 int gtf_parabolic_kl(const gtf_kl_graph* g, int32_t dtype, const gtf_kl_out* out, gtf_stream_t stream);
 
+/* ---- event conversion: CSV rows -> packed CSR in the reference's orders -------------
+ * Replaces helper.construct_graph + nx.DiGraph + the weakly-connected-component
+ * subgraph copies of event_conversion.py:63-84 (helper.py:465-521) and the key order of
+ * helper.compute_track_state_estimates' dicts (helper.py:277, 350-351). Host function
+ * (no device work): the packed graph then goes to the GPU, where
+ * gtf_track_state_estimates and gtf_node_ops compute the states, priors, mixture
+ * weights and degrees. Orders are CPython 3.10 set orders, reproduced exactly. */
+typedef struct gtf_event_csr {
+    int64_t n_nodes;          /* in: nodes kept by the volume window, CSV order */
+    int64_t n_rows;           /* in: edges.csv rows */
+    const int64_t* node_id;   /* in: [n_nodes] node_idx, unique, in [0, 2^61 - 1) */
+    const int64_t* row_a;     /* in: [n_rows] second column (node1): add_edge(a, b) first */
+    const int64_t* row_b;     /* in: [n_rows] first column (node2) */
+    int32_t* order;           /* out: [n_nodes] CSV index of packed node i */
+    int32_t* sub_id;          /* out: [n_nodes] subgraph (weakly connected component) */
+    int32_t* slot_ptr;        /* out: [n_nodes + 1] */
+    int32_t* slot_src;        /* out: [2 * n_rows] packed sender per slot (ascending per receiver) */
+    int32_t* tse_rank;        /* out: [2 * n_rows] track_state_estimates dict position */
+    int32_t* out_ptr;         /* out: [n_nodes + 1] */
+    int32_t* out_slot;        /* out: [2 * n_rows] successor order */
+    int64_t n_edges;          /* out: directed edges (= slots) */
+    int32_t n_subgraphs;      /* out */
+    int32_t pad_;
+} gtf_event_csr;
+
+int gtf_build_event_csr(gtf_event_csr* ev);
+
 const char* gtf_last_error(void);
 const char* gtf_version(void);
 

@@ -240,4 +240,74 @@ int gtf_build_event_csr(gtf_event_csr* ev) {
     return 0;
 }
 
+int gtf_candidate_order(const gtf_candidate_graph* cg, int32_t* order_key) {
+    if (!cg || cg->n_nodes < 0 || !order_key ||
+        (cg->n_nodes && (!cg->slot_ptr || !cg->out_ptr || !cg->sub_id || !cg->node_id)) ||
+        (cg->n_slots && (!cg->slot_src || !cg->is_edge || !cg->act)) || (cg->n_edges && !cg->out_slot)) {
+        gtf::set_error("gtf_candidate_order: bad arguments");
+        return -2;
+    }
+    const int32_t N = cg->n_nodes;
+    std::vector<int32_t> dst(cg->n_slots);
+    for (int32_t v = 0; v < N; v++)
+        for (int32_t k = cg->slot_ptr[v]; k < cg->slot_ptr[v + 1]; k++) dst[k] = v;
+    std::vector<uint8_t> seen(N, 0);
+    std::vector<int32_t> level, nextlevel, members;
+    int32_t lo = 0;
+    while (lo < N) {
+        int32_t hi = lo + 1;
+        while (hi < N && cg->sub_id[hi] == cg->sub_id[lo]) hi++;
+        if (cg->sub_id[hi - 1] != cg->sub_id[lo]) { gtf::set_error("gtf_candidate_order: sub_id not grouped"); return -2; }
+        bool inactive = false;
+        for (int32_t k = cg->slot_ptr[lo]; k < cg->slot_ptr[hi] && !inactive; k++)
+            inactive = cg->is_edge[k] && cg->act[k] == 0;
+        if (!inactive) {                     // CCA keeps the whole subgraph (:344-345)
+            for (int32_t v = lo; v < hi; v++) order_key[v] = v - lo;
+            lo = hi;
+            continue;
+        }
+        for (int32_t s = lo; s < hi; s++) {
+            if (seen[s]) continue;
+            PySet c;
+            members.clear();
+            auto visit = [&](int32_t w) {
+                if (seen[w]) return;
+                seen[w] = 1;
+                c.add(cg->node_id[w]);
+                members.push_back(w);
+                nextlevel.push_back(w);
+            };
+            seen[s] = 1;
+            c.add(cg->node_id[s]);
+            members.push_back(s);
+            level.assign(1, s);
+            while (!level.empty()) {
+                nextlevel.clear();
+                for (int32_t v : level) {
+                    for (int32_t j = cg->out_ptr[v]; j < cg->out_ptr[v + 1]; j++) {
+                        const int32_t k = cg->out_slot[j];
+                        if (cg->act[k] != 0) visit(dst[k]);          // successors, G order
+                    }
+                    for (int32_t k = cg->slot_ptr[v]; k < cg->slot_ptr[v + 1]; k++)
+                        if (cg->is_edge[k] && cg->act[k] != 0) visit(cg->slot_src[k]);   // predecessors
+                }
+                level.swap(nextlevel);
+            }
+            if (2 * (int64_t)members.size() < (int64_t)(hi - lo)) {
+                std::unordered_map<int64_t, int32_t> at;
+                for (int32_t m : members) at.emplace(cg->node_id[m], m);
+                PySet shown;
+                c.each([&](int64_t k) { shown.add(k); });
+                int32_t r = 0;
+                shown.each([&](int64_t k) { order_key[at[k]] = r++; });
+            } else {
+                std::sort(members.begin(), members.end());
+                for (size_t r = 0; r < members.size(); r++) order_key[members[r]] = (int32_t)r;
+            }
+        }
+        lo = hi;
+    }
+    return 0;
+}
+
 }  // extern "C"

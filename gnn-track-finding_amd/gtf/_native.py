@@ -70,6 +70,12 @@ class GtfEventCsr(ctypes.Structure):
                 ("out_ptr", P), ("out_slot", P), ("n_edges", ctypes.c_int64), ("n_subgraphs", I32), ("pad_", I32)]
 
 
+class GtfCandidateGraph(ctypes.Structure):
+    _fields_ = [("n_nodes", I32), ("n_slots", I32), ("n_edges", I32), ("pad_", I32), ("slot_ptr", P),
+                ("slot_src", P), ("is_edge", P), ("act", P), ("out_ptr", P), ("out_slot", P), ("sub_id", P),
+                ("node_id", P)]
+
+
 class GtfKlGraph(ctypes.Structure):
     _fields_ = [("n_nodes", I32), ("n_slots", I32), ("slot_ptr", P), ("slot_src", P), ("gnn", P), ("truth", P),
                 ("pair_ptr", P), ("list", P * 4), ("count", I32 * 4)]
@@ -97,7 +103,8 @@ SYMBOLS = ["gtf_workspace_bytes", "gtf_clear_errors", "gtf_read_errors", "gtf_ex
            "gtf_message_passing", "gtf_node_ops",
            "gtf_cluster", "gtf_pass", "gtf_pass_ev", "gtf_tag_prepare", "gtf_tag_sweep", "gtf_parabolic_kl", "gtf_track_state_estimates", "gtf_pass_shard",
            "gtf_shard_chunk_bytes", "gtf_shard_pack", "gtf_shard_unpack", "gtf_extract_workspace_bytes",
-           "gtf_extract_candidates", "gtf_build_event_csr", "gtf_last_error",
+           "gtf_extract_candidates", "gtf_build_event_csr", "gtf_candidate_order",
+           "gtf_last_error",
            "gtf_version"]
 
 OPS = {"ranks": 1, "priors_tse": 2, "priors_uts": 3, "reweight_uts": 4, "degree": 5, "prune": 6, "mw_tse": 7,
@@ -142,12 +149,14 @@ def lib():
     L.gtf_track_state_estimates.argtypes = [G, S, ctypes.POINTER(GtfTseExtra), PR, P]
     L.gtf_parabolic_kl.argtypes = [ctypes.POINTER(GtfKlGraph), I32, ctypes.POINTER(GtfKlOut), P]
     L.gtf_build_event_csr.argtypes = [ctypes.POINTER(GtfEventCsr)]
+    L.gtf_candidate_order.argtypes = [ctypes.POINTER(GtfCandidateGraph), P]
     L.gtf_last_error.restype = ctypes.c_char_p
     L.gtf_version.restype = ctypes.c_char_p
     for fn in ("gtf_clear_errors", "gtf_read_errors", "gtf_extrapolate", "gtf_update", "gtf_cluster", "gtf_pass",
                "gtf_pass_ev", "gtf_message_passing", "gtf_node_ops",
                "gtf_tag_prepare", "gtf_tag_sweep", "gtf_parabolic_kl", "gtf_track_state_estimates", "gtf_pass_shard", "gtf_shard_pack",
-               "gtf_shard_unpack", "gtf_extract_candidates", "gtf_build_event_csr"):
+               "gtf_shard_unpack", "gtf_extract_candidates", "gtf_build_event_csr",
+               "gtf_candidate_order"):
         getattr(L, fn).restype = ctypes.c_int
     _lib = L
     return L

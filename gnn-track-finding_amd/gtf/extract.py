@@ -80,13 +80,34 @@ def run(g: TrackGraph, vivl, params: Params, order_key=None, device="cuda", d=No
     return out
 
 
-def outputs(g: TrackGraph, res, fragment):
+def candidate_order(g: TrackGraph) -> np.ndarray:
+    """Each node's position inside its candidate in the reference's member order
+    (gtf_candidate_order: networkx CCA + subgraph-copy orders, :332-346), for run()'s
+    order_key. Host function on the packed graph's activation mask."""
+    N = g.n_nodes
+    a = {k: np.ascontiguousarray(v) for k, v in (
+        ("slot_ptr", g.slot_ptr.astype(np.int32)), ("slot_src", g.slot["slot_src"].astype(np.int32)),
+        ("is_edge", g.slot["is_edge"].astype(np.uint8)), ("act", g.slot["act"].astype(np.uint8)),
+        ("out_ptr", g.out_ptr.astype(np.int32)), ("out_slot", g.out_slot.astype(np.int32)),
+        ("sub_id", g.node["sub_id"].astype(np.int32)), ("node_id", g.node["node_id"].astype(np.int64)))}
+    vp = lambda x: ctypes.c_void_p(x.ctypes.data if x.size else 0)  # noqa: E731
+    cg = nat.GtfCandidateGraph(N, g.n_slots, g.n_edges, 0, vp(a["slot_ptr"]), vp(a["slot_src"]), vp(a["is_edge"]),
+                               vp(a["act"]), vp(a["out_ptr"]), vp(a["out_slot"]), vp(a["sub_id"]), vp(a["node_id"]))
+    out = np.zeros(max(N, 1), np.int32)
+    nat.check(nat.lib().gtf_candidate_order(ctypes.byref(cg), vp(out)))
+    return out[:N]
+
+
+def outputs(g: TrackGraph, res, fragment, order_key=None):
     """The stage's outputs from the device results: extracted candidates (node index
     arrays, in the reference's order), their p-values, remaining and fragment node
-    sets per subgraph (:423-430)."""
+    sets per subgraph (:423-430). order_key: member order inside each candidate (as
+    given to run()); default node order."""
     label, status, ext = res["label"], res["status"], res["ext"].astype(bool)
     roots = np.unique(label)                          # candidate order = first-node order
     extracted = [np.nonzero(label == r)[0] for r in roots if status[r] == EXTRACTED]
+    if order_key is not None:
+        extracted = [c[np.argsort(order_key[c], kind="stable")] for c in extracted]
     pxy = np.array([res["pxy"][r] for r in roots if status[r] == EXTRACTED])
     pzr = np.array([res["pzr"][r] for r in roots if status[r] == EXTRACTED])
     sub = g.node["sub_id"]

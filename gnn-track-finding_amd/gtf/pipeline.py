@@ -27,7 +27,7 @@ from __future__ import annotations
 
 import dataclasses
 import time
-from typing import List
+from typing import List, Optional
 
 import numpy as np
 
@@ -51,6 +51,9 @@ class Iteration:
     remaining: List[np.ndarray]
     fragments: List[np.ndarray]
     seconds: dict
+    network: Optional[TrackGraph] = None      # the stage's output graph (keep_graphs=True)
+    remaining_graph: Optional[TrackGraph] = None    # next iteration's input
+    remaining_vivl: Optional[np.ndarray] = None
 
 
 def event_layout(event_prefix: str, min_volume: int, max_volume: int, builder: str = "native"):
@@ -103,10 +106,11 @@ def _ids(g: TrackGraph, groups):
 
 
 def run(g: TrackGraph, vivl, iterations: int = 3, p: Params = None, ex: extract.Params = None,
-        device="cuda", first: int = 1) -> List[Iteration]:
+        device="cuda", first: int = 1, keep_graphs: bool = False) -> List[Iteration]:
     """Iterations ``first`` .. ``first + iterations - 1`` of the loop, starting from
     the stage input ``g`` (the event network for iteration 1). Stops early when
-    nothing remains."""
+    nothing remains. keep_graphs: also return each iteration's stage output and
+    remaining graphs (for saving, gtf.store)."""
     from .device import DeviceGraph
     p = p or Params()
     ex = ex or extract.Params()
@@ -134,10 +138,12 @@ def run(g: TrackGraph, vivl, iterations: int = 3, p: Params = None, ex: extract.
         d.raise_errors()
         torch.cuda.synchronize(d.device)
         t1 = time.perf_counter()
-        res = extract.run(g, vivl, ex, d=d)
         d.download(g)
+        order = extract.candidate_order(g)            # members in the reference's candidate order
+        res = extract.run(g, vivl, ex, order_key=order, d=d)
         t2 = time.perf_counter()
-        o = extract.outputs(g, res, ex.numhits)
+        o = extract.outputs(g, res, ex.numhits, order)
+        net = g.copy() if keep_graphs else None       # the stage's output, before the merging mutation
         keep = np.zeros(g.n_nodes, bool)
         for r in o["remaining"]:
             keep[r] = True
@@ -152,8 +158,11 @@ def run(g: TrackGraph, vivl, iterations: int = 3, p: Params = None, ex: extract.
             du.raise_errors()
             du.download(nxt)
         t3 = time.perf_counter()
-        out.append(Iteration(it, stage, _ids(g, o["extracted"]), o["pval_xy"], o["pval_zr"],
-                             _ids(g, o["remaining"]), _ids(g, o["fragments"]),
-                             {"stage": t1 - t0, "extract": t2 - t1, "next": t3 - t2}))
+        rec = Iteration(it, stage, _ids(g, o["extracted"]), o["pval_xy"], o["pval_zr"],
+                        _ids(g, o["remaining"]), _ids(g, o["fragments"]),
+                        {"stage": t1 - t0, "extract": t2 - t1, "next": t3 - t2})
+        if keep_graphs:
+            rec.network, rec.remaining_graph, rec.remaining_vivl = net, nxt, vivl[keep]
+        out.append(rec)
         g, vivl = nxt, vivl[keep]
     return out

@@ -347,6 +347,27 @@ typedef struct gtf_event_csr {
 
 int gtf_build_event_csr(gtf_event_csr* ev);
 
+/* Member order of every extraction candidate as the reference builds it: CCA over the
+ * active edges of each subgraph (extract_track_candidates.py:332-346) -- networkx
+ * weakly connected components, each copied as subGraph.subgraph(component) (set order
+ * when the component is under half the subgraph) -- or the whole subgraph when none of
+ * its edges is inactive. order_key[v] = v's position in its candidate: the order
+ * rotate_track's stable r-sort and the efficiency's particle vote break ties in.
+ * Host arrays of the packed graph; sub_id grouped (pack order). */
+typedef struct gtf_candidate_graph {
+    int32_t n_nodes, n_slots, n_edges, pad_;
+    const int32_t* slot_ptr;
+    const int32_t* slot_src;
+    const uint8_t* is_edge;
+    const uint8_t* act;
+    const int32_t* out_ptr;
+    const int32_t* out_slot;
+    const int32_t* sub_id;
+    const int64_t* node_id;
+} gtf_candidate_graph;
+
+int gtf_candidate_order(const gtf_candidate_graph* cg, int32_t* order_key);
+
 const char* gtf_last_error(void);
 const char* gtf_version(void);
 

@@ -44,7 +44,8 @@ def test_struct_layout_matches_header():
     py = {"gtf_graph": nat.GtfGraph, "gtf_nodes": nat.GtfNodes, "gtf_states": nat.GtfStates,
           "gtf_edges": nat.GtfEdges, "gtf_params": nat.GtfParams, "gtf_kl_graph": nat.GtfKlGraph, "gtf_tse_extra": nat.GtfTseExtra, "gtf_shard": nat.GtfShard,
           "gtf_extract_params": nat.GtfExtractParams, "gtf_extract_io": nat.GtfExtractIO,
-          "gtf_kl_out": nat.GtfKlOut, "gtf_event_csr": nat.GtfEventCsr}
+          "gtf_kl_out": nat.GtfKlOut, "gtf_event_csr": nat.GtfEventCsr,
+          "gtf_candidate_graph": nat.GtfCandidateGraph}
     lines = []
     for t, cls in py.items():
         lines += ['  printf("%s.%s %%zu\\n", offsetof(%s, %s));' % (t, f, t, f) for f, _ in cls._fields_]

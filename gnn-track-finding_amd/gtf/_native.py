@@ -121,6 +121,10 @@ def lib():
     if not os.path.exists(LIB_PATH):
         raise RuntimeError("libgtf.so not built at %s -- run __graft_entry__.build() "
                            "(hipcc --offload-arch=gfx950); there is no CPU fallback" % LIB_PATH)
+    # torch first: its bundled libamdhip64 (SONAME libamdhip64.so.7) then satisfies
+    # libgtf's NEEDED entry, so the process holds ONE HIP runtime. Loaded the other way
+    # round, torch pulls a second runtime and libgtf's calls see no device.
+    import torch  # noqa: F401
     L = ctypes.CDLL(LIB_PATH)
     L.gtf_workspace_bytes.restype = ctypes.c_size_t
     L.gtf_workspace_bytes.argtypes = [I32, I32]

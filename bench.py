@@ -131,6 +131,9 @@ def bench_sharded(workload, rank, world, dev, steps, warmup, params):
             "owned_slots_max": sd.plan.cap_slots, "collective": "all_gather_into_tensor (RCCL)"}
 
 
+# the fused node kernel: priors, side norm, reweights, update and KL clustering of every
+# receiver in one launch (gtf_pass.hip run_pass)
+NODE_KERNEL = "k_node_multi<update+cluster> (KL-distance kernel)"
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc", "pmc_c4.json")
 
 
@@ -230,8 +233,7 @@ def main():
     kern = {
         "k_sender": (avg(0, 1), None),
         "k_extrapolate": (avg(1, 2), None),
-        "k_node_multi<reweight,update>": (avg(2, 3), rf.reweight_bytes(g.n_slots, g.n_nodes)),
-        "k_node_multi<cluster> (KL-distance kernel)": (avg(3, 4), rf.kl_bytes(e_elig, int(elig.sum()))),
+        NODE_KERNEL: (avg(2, 3), rf.fused_node_bytes(g.n_slots, g.n_nodes, e_elig, int(elig.sum()))),
     }
     ext_ms = kern["k_sender"][0] + kern["k_extrapolate"][0]
     cands = {"k_sender+k_extrapolate": (ext_ms, rf.extrap_bytes(g.n_edges, g.n_nodes))}

@@ -256,6 +256,9 @@ __global__ void __launch_bounds__(BLOCK) k_extrapolate(gtf_graph g, gtf_nodes n,
 #define EXTRAP_OPS OP_RANKS, OP_PRIORS_UTS, OP_REWEIGHT_UTS, OP_PRIORS_UTS, OP_REWEIGHT_UTS, OP_DEGREE
 #define UPDATE_OPS OP_PRUNE, OP_PRIORS_TSE, OP_PRIORS_UTS, OP_REWEIGHT_UTS
 #define CLUSTER_UTS_OPS OP_CLUSTER_UTS, OP_DEGREE, OP_MW_UTS, OP_PRIORS_UTS
+#ifndef GTF_SPLIT_NODE
+#define GTF_SPLIT_NODE 0  // diagnostics build only: update and clustering in two launches
+#endif
 #define CLUSTER_TSE_OPS OP_CLUSTER_TSE, OP_DEGREE, OP_MW_TSE, OP_PRIORS_TSE
 
 struct Seg {
@@ -702,17 +705,26 @@ int launch_seq(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* ut
 
 #define SEQ(x) x, (int)sizeof(x)
 
-// the fused pass: message passing, then the node-local work in two launches (the light
-// reweight/update sequence at high occupancy, then clustering with its LDS staging)
+// the fused pass: message passing, then every node-local op (extrapolation's priors and
+// reweights, the update, KL clustering) in ONE node launch: each receiver's ops read and
+// write only its own slot segment (plus static coordinates), so there is no inter-node
+// dependency between the update and the clustering and one load/store round of the slot
+// state serves both. (GTF_SPLIT_NODE=1 builds the earlier two-launch variant for A/B.)
 int run_pass(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts, gtf_edges* e,
              const gtf_params* p, const gtf_shard* sh, void* ws, hipStream_t st, void* const* events) {
     Ws w = carve(ws, g->n_nodes, g->n_slots);
     int rc = launch_extrap_edges(g, n, uts, e, p, w, st, sh, events);
     if (rc) return rc;
+#if GTF_SPLIT_NODE
     rc = launch_seq<EXTRAP_OPS, UPDATE_OPS>(g, n, tse, uts, e, p, w, 0.0, 0.0, st);
     if (rc) return rc;
     if (events) (void)hipEventRecord((hipEvent_t)events[3], st);
     rc = launch_seq<CLUSTER_UTS_OPS>(g, n, tse, uts, e, p, w, p->cluster_chi2, p->cluster_kl, st);
+#else
+    rc = launch_seq<EXTRAP_OPS, UPDATE_OPS, CLUSTER_UTS_OPS>(g, n, tse, uts, e, p, w, p->cluster_chi2,
+                                                             p->cluster_kl, st);
+    if (events) (void)hipEventRecord((hipEvent_t)events[3], st);
+#endif
     if (events) (void)hipEventRecord((hipEvent_t)events[4], st);
     return rc;
 }

@@ -19,8 +19,10 @@ Per kernel of gtf_pass (DESIGN.md "Roofline"):
     likelihood 8, prior 8, sender layer 8, stored x 8, TSE rank 4 and prior 8 (= 57,
     +1 reverse-edge flag = 58); write weight 8, prior 8, lr 8, side 1, edge weight 8,
     activation 1, TSE prior 8 (= 42) -- plus 6 B per node (flags, degree);
-  * k_node_multi<cluster> = the KL-distance kernel: SURVEY §8d's B_KL = 89 B per
+  * the clustering ops = the KL-distance work: SURVEY §8d's B_KL = 89 B per
     in-edge of an eligible node (3 <= |states| <= 15) + 176 B per eligible node.
+  * gtf_pass runs both op sequences in ONE node launch (the fused node kernel, "the
+    KL-distance kernel" of the bench line): reweight/update bytes + B_KL.
 
 Parabolic-model KL kernel (gtf_parabolic_kl, §8 a17), minimal unique traffic:
   * 24 B per node of the batch (GNN x, y and truth id, read once: neighbours
@@ -57,6 +59,12 @@ def reweight_bytes(n_slots, n_nodes):
 
 def kl_bytes(e_elig, n_elig):
     return KL_PER_EDGE * e_elig + KL_PER_NODE * n_elig
+
+
+def fused_node_bytes(n_slots, n_nodes, e_elig, n_elig):
+    """The fused node kernel (gtf_pass): the reweight/update traffic of every slot plus
+    the KL-distance traffic of the eligible nodes' in-edges (each read once)."""
+    return reweight_bytes(n_slots, n_nodes) + kl_bytes(e_elig, n_elig)
 
 
 def pass_bytes(n_edges, n_nodes):

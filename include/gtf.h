@@ -169,9 +169,9 @@ int gtf_cluster(const gtf_graph* g, gtf_nodes* n, gtf_states* states, gtf_edges*
 int gtf_pass(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts, gtf_edges* e,
              const gtf_params* p, void* workspace, gtf_stream_t stream);
 /* gtf_pass with hipEvent_t events[5] recorded on the stream before the sender scan,
- * after it, after the edge extrapolation kernel, after the reweight/update node kernel
- * and after the clustering node kernel (per-kernel timing for the roofline report;
- * events may be NULL). */
+ * after it, after the edge extrapolation kernel, after the fused node kernel (priors,
+ * reweights, update and KL clustering in one launch) and at the end of the pass
+ * (per-kernel timing for the roofline report; events may be NULL). */
 int gtf_pass_ev(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts, gtf_edges* e,
                 const gtf_params* p, void* workspace, gtf_stream_t stream, void* const* events);
 

@@ -14,6 +14,8 @@ Layout under ROOTDIR (the run script's directories, one file each):
     iteration_i/remaining/graph.npz          the next iteration's input (after update on even i)
     iteration_i/fragments/fragments.npz      node ids of the track fragments
     timings.json                             wall time per stage
+    metrics.json                             with --truth: reconstruction efficiency and purities
+                                             (gtf.metrics; the run script's last step, :143-146)
 
 --start S > 1 resumes from ROOTDIR/iteration_{S-1}/remaining/graph.npz, as the run
 script's commented "iteration by iteration" mode does (:79-81).
@@ -56,6 +58,8 @@ def main(argv=None):
     ap.add_argument("--start", type=int, default=1)
     ap.add_argument("--end", type=int, default=3)
     ap.add_argument("--device", default="cuda")
+    ap.add_argument("--truth", help="EVENT_TRUTH dir: score the candidates (reconstruction_efficiency.py)")
+    ap.add_argument("--mapping", default="full-mapping-minCurv-0.3-800.csv", help="mapping file under --truth")
     args = ap.parse_args(argv)
     if args.start < 1 or args.end < args.start:
         ap.error("need 1 <= start <= end")
@@ -97,6 +101,17 @@ def main(argv=None):
               % (it.index, it.stage, len(it.candidates), len(it.remaining), len(it.fragments)))
     with open(os.path.join(_dir(root), "timings.json"), "w") as f:
         json.dump(times, f, indent=1)
+    if args.truth and its:
+        from extract import reconstruction_efficiency as re_cli
+        from gtf import metrics
+        res = {}
+        for name, cum in (("last_iteration", False), ("cumulative", True)):
+            r = re_cli.score(args.truth, root, args.min_volume, args.max_volume, its[-1].index, args.mapping, cum)
+            res[name] = metrics.summary(r)
+            print("%s: %d / %d reference tracks reconstructed, efficiency %s %%"
+                  % (name, r.n_reconstructed, r.n_reference, r.efficiency_str))
+        with open(os.path.join(root, "metrics.json"), "w") as f:
+            json.dump(res, f, indent=1)
     return 0
 
 

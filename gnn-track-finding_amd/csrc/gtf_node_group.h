@@ -1,5 +1,5 @@
 // gtf_node_group.h -- the node-local op sequence with G lanes per receiver node
-// (G = 8, 16, 32, 64 for nodes with <= 8, 16, 32, 64 slots), one slot per lane.
+// (G = 4, 8, 16, 32, 64 for nodes with <= 4, 8, 16, 32, 64 slots), one slot per lane.
 //
 // Why: every stage after message passing reduces over one node's in-edge slot
 // segment. One thread per node serialises O(d^2) loops over
@@ -545,15 +545,16 @@ __device__ __forceinline__ void node_seq_body(const gtf_graph& g, gtf_nodes& n, 
 }
 
 struct Buckets {
-    const int32_t* list[4];  // node lists for G = 64, 32, 16, 8 (slowest first)
-    int32_t count[4];
-    int32_t blocks[4];
+    const int32_t* list[5];  // node lists for G = 64, 32, 16, 8, 4 (slowest first)
+    int32_t count[5];
+    int32_t blocks[5];
 };
 
 template <int G>
 constexpr size_t stage_bytes() { return (size_t)(BLOCK / G) * sizeof(StageT<(G < 16 ? G : 16)>); }
 constexpr size_t node_smem_bytes() {
-    size_t m = stage_bytes<8>();
+    size_t m = stage_bytes<4>();
+    m = stage_bytes<8>() > m ? stage_bytes<8>() : m;
     m = stage_bytes<16>() > m ? stage_bytes<16>() : m;
     m = stage_bytes<32>() > m ? stage_bytes<32>() : m;
     m = stage_bytes<64>() > m ? stage_bytes<64>() : m;
@@ -591,7 +592,12 @@ __global__ void __launch_bounds__(BLOCK) k_node_multi(gtf_graph g, gtf_nodes n, 
         return;
     }
     b -= bk.blocks[2];
-    node_seq_body<8, OPS...>(g, n, tse, uts, e, p, w, chi2_thr, kl_thr, bk.list[3], bk.count[3], b, smem);
+    if (b < bk.blocks[3]) {
+        node_seq_body<8, OPS...>(g, n, tse, uts, e, p, w, chi2_thr, kl_thr, bk.list[3], bk.count[3], b, smem);
+        return;
+    }
+    b -= bk.blocks[3];
+    node_seq_body<4, OPS...>(g, n, tse, uts, e, p, w, chi2_thr, kl_thr, bk.list[4], bk.count[4], b, smem);
 }
 
 // run-time op sequence (gtf_node_ops): any order of any ops

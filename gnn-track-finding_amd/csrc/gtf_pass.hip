@@ -612,7 +612,7 @@ void finish_ops(NodeOps& ops, const gtf_states* tse, const gtf_states* uts) {
 void launch_serial_rest(const gtf_graph* g, gtf_nodes* n, const gtf_states& T, const gtf_states& U, gtf_edges* e,
                         const gtf_params* p, Ws w, const NodeOps& ops, double chi2, double kl, hipStream_t st) {
     if (g->sched) {
-        const int ng = g->n_g8 + g->n_g16 + g->n_g32 + g->n_g64;
+        const int ng = g->n_g4 + g->n_g8 + g->n_g16 + g->n_g32 + g->n_g64;
         const int nbig = g->n_big;
         if (nbig > 0)
             hipLaunchKernelGGL(k_node, dim3(grid(nbig)), dim3(BLOCK), 0, st, *g, *n, T, U, *e, *p, w, ops, chi2, kl,
@@ -644,6 +644,10 @@ int launch_ops(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* ut
     if (g->n_nodes > 0 && ops.n > 0) {
         if (g->sched) {
             const int32_t* l = g->sched;
+            if (g->n_g4 > 0)
+                hipLaunchKernelGGL(k_node_group<4>, dim3((g->n_g4 + BLOCK / 4 - 1) / (BLOCK / 4)), dim3(BLOCK), 0, st,
+                                   *g, *n, T, U, *e, *p, w, ops, chi2, kl, l, g->n_g4);
+            l += g->n_g4;
             if (g->n_g8 > 0)
                 hipLaunchKernelGGL(k_node_group<8>, dim3((g->n_g8 + BLOCK / 8 - 1) / (BLOCK / 8)), dim3(BLOCK), 0, st,
                                    *g, *n, T, U, *e, *p, w, ops, chi2, kl, l, g->n_g8);
@@ -681,12 +685,13 @@ int launch_seq(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* ut
     if (g->n_nodes > 0) {
         if (g->sched) {
             Buckets bk;
-            const int cnt[4] = {g->n_g64, g->n_g32, g->n_g16, g->n_g8};
-            const int gs[4] = {64, 32, 16, 8};
-            const int32_t* starts[4] = {g->sched + g->n_g8 + g->n_g16 + g->n_g32, g->sched + g->n_g8 + g->n_g16,
-                                        g->sched + g->n_g8, g->sched};
+            const int cnt[5] = {g->n_g64, g->n_g32, g->n_g16, g->n_g8, g->n_g4};
+            const int gs[5] = {64, 32, 16, 8, 4};
+            const int32_t* s8 = g->sched + g->n_g4;
+            const int32_t* starts[5] = {s8 + g->n_g8 + g->n_g16 + g->n_g32, s8 + g->n_g8 + g->n_g16, s8 + g->n_g8,
+                                        s8, g->sched};
             int total = 0;
-            for (int q = 0; q < 4; q++) {
+            for (int q = 0; q < 5; q++) {
                 bk.list[q] = starts[q];
                 bk.count[q] = cnt[q];
                 bk.blocks[q] = (cnt[q] + BLOCK / gs[q] - 1) / (BLOCK / gs[q]);

@@ -293,9 +293,10 @@ extern "C" int gtf_track_state_estimates(const gtf_graph* g, gtf_states* tse, co
         gtf::set_error("gtf_track_state_estimates: needs the node schedule, graph arrays and TSE outputs");
         return -2;
     }
-    const int n8 = g->n_g8, n16 = g->n_g16, n32 = g->n_g32, n64 = g->n_g64;
+    // nodes with <= 4 slots (n_g4, scheduled first) take the 8-lane path
+    const int n8 = g->n_g4 + g->n_g8, n16 = g->n_g16, n32 = g->n_g32, n64 = g->n_g64;
     const int rest = g->n_big;
-    if (rest < 0 || n8 < 0 || n16 < 0 || n32 < 0 || n64 < 0) {
+    if (rest < 0 || g->n_g4 < 0 || g->n_g8 < 0 || n16 < 0 || n32 < 0 || n64 < 0) {
         gtf::set_error("gtf_track_state_estimates: bad schedule counts");
         return -2;
     }

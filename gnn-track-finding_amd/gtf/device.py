@@ -20,7 +20,7 @@ import ctypes
 import numpy as np
 
 from . import _native as nat
-from .graph import TrackGraph, NODE_FIELDS, SLOT_FIELDS
+from .graph import BUCKETS, TrackGraph, NODE_FIELDS, SLOT_FIELDS
 from .params import Params
 
 STATIC_SLOT = ("slot_src", "is_edge", "rev_edge", "send_mw")
@@ -67,13 +67,12 @@ class DeviceGraph:
         # slot-count-bucketed node schedule for the node-local kernels (G lanes per node)
         deg = np.diff(g.slot_ptr.astype(np.int64))
         idx = np.arange(g.n_nodes, dtype=np.int32)
-        edges = [(0, 8), (9, 16), (17, 32), (33, 64)]
-        buckets = [idx[(deg >= lo) & (deg <= hi)] for lo, hi in edges]
+        buckets = [idx[(deg >= lo) & (deg <= hi)] for lo, hi in BUCKETS]
         rest = idx[deg > 64]
         up("sched", np.concatenate(buckets + [rest]).astype(np.int32))
         self.n_g_all = [int(b.size) for b in buckets]
         self.n_big = int(rest.size)
-        self.n_g = self.n_g_all if schedule else [0, 0, 0, 0]
+        self.n_g = self.n_g_all if schedule else [0] * len(BUCKETS)
         self.use_sched = schedule
         for f in ("gnn", "xyzr", "layer") + MUTABLE_NODE:
             up(f, g.node[f])
@@ -121,12 +120,13 @@ class DeviceGraph:
                                p("slot_ptr"), p("slot_src"),
                                p("slot_dst"), p("out_ptr"), p("out_slot"), p("slot_outpos"), p("is_edge"), p("rev_edge"), p("solo"),
                                p("gnn"), p("xyzr"), p("layer"),
-                               p("sched") if self.use_sched else ctypes.c_void_p(0), *self.n_g, p("out_dst"), p("slot_layer"))
+                               p("sched") if self.use_sched else ctypes.c_void_p(0), *self.n_g[1:], p("out_dst"),
+                               p("slot_layer"), self.n_g[0])
         self.cg_sched = nat.GtfGraph(self.n_nodes, self.n_slots, self.n_edges, self.n_big, p("slot_ptr"),
                                      p("slot_src"),
                                      p("slot_dst"), p("out_ptr"), p("out_slot"), p("slot_outpos"), p("is_edge"),
                                      p("rev_edge"), p("solo"), p("gnn"), p("xyzr"), p("layer"), p("sched"),
-                                     *self.n_g_all, p("out_dst"), p("slot_layer"))
+                                     *self.n_g_all[1:], p("out_dst"), p("slot_layer"), self.n_g_all[0])
         self.cn = nat.GtfNodes(*[p(f) for f in MUTABLE_NODE])
         self.cuts = nat.GtfStates(p("uts_rank"), p("uts_sv"), p("uts_tau"), p("uts_cov"), p("uts_xyzr"),
                                   p("uts_lik"), p("uts_mw"), p("uts_prior"), p("uts_lr"), p("uts_side"),

@@ -39,6 +39,10 @@ import numpy as np
 F64 = np.float64
 NAN = float("nan")
 
+# slot-count buckets of the node-kernel schedule (gtf_graph.sched): 4, 8, 16, 32, 64 lanes
+# per node; nodes with more slots run one thread each (n_big)
+BUCKETS = ((0, 4), (5, 8), (9, 16), (17, 32), (33, 64))
+
 # covariance packing order
 COV5 = ((0, 0), (0, 1), (1, 0), (1, 1), (2, 2))
 

@@ -24,9 +24,7 @@ import ctypes
 import numpy as np
 
 from . import _native as nat
-from .graph import TrackGraph
-
-BUCKETS = ((0, 8), (9, 16), (17, 32), (33, 64))   # lane-group buckets of the node kernels
+from .graph import BUCKETS, TrackGraph
 
 
 class ShardPlan:
@@ -64,7 +62,7 @@ class ShardPlan:
         return np.unique(np.concatenate([halo.astype(np.int64), own])).astype(np.int32)
 
     def schedule(self, r: int):
-        """(sched, [n_g8, n_g16, n_g32, n_g64], n_big) of the owned receivers"""
+        """(sched, [n_g4, n_g8, n_g16, n_g32, n_g64], n_big) of the owned receivers"""
         deg = np.diff(self._g.slot_ptr.astype(np.int64))
         idx = np.arange(self.node_lo[r], self.node_hi[r], dtype=np.int32)
         d = deg[idx]
@@ -110,8 +108,8 @@ class ShardedDeviceGraph:
         vp = lambda t: ctypes.c_void_p(t.data_ptr() if t.numel() else 0)  # noqa: E731
         self.cg = nat.GtfGraph(d.n_nodes, d.n_slots, d.n_edges, n_big, p("slot_ptr"), p("slot_src"), p("slot_dst"),
                                p("out_ptr"), p("out_slot"), p("slot_outpos"), p("is_edge"), p("rev_edge"),
-                               p("solo"), p("gnn"), p("xyzr"), p("layer"), vp(self.sched), *n_g, p("out_dst"),
-                               p("slot_layer"))
+                               p("solo"), p("gnn"), p("xyzr"), p("layer"), vp(self.sched), *n_g[1:], p("out_dst"),
+                               p("slot_layer"), n_g[0])
         pl = self.plan
         self.shard = nat.GtfShard(vp(self.senders), int(self.senders.numel()), int(pl.node_lo[rank]),
                                   int(pl.node_hi[rank]), int(pl.slot_lo[rank]), int(pl.slot_hi[rank]))

@@ -40,7 +40,7 @@ typedef struct gtf_graph {
     int32_t n_nodes;
     int32_t n_slots;          /* slots = (receiver, sender) pairs, receiver-major */
     int32_t n_edges;          /* directed edges = slots with is_edge == 1 */
-    int32_t n_big;            /* schedule entries after the four lane-group buckets (> 64 slots) */
+    int32_t n_big;            /* schedule entries after the lane-group buckets (> 64 slots) */
     const int32_t* slot_ptr;  /* [N+1] slot segment of each receiver */
     const int32_t* slot_src;  /* [S]   sender node index, -1 = orphan state key */
     const int32_t* slot_dst;  /* [S]   receiver node index */
@@ -54,10 +54,11 @@ typedef struct gtf_graph {
     const double*  xyzr;      /* [N*4] node attribute 'xyzr' */
     const double*  layer;     /* [N]   in_volume_layer_id */
     /* optional node schedule for the node-local stages (NULL = one thread per node):
-     * node indices bucketed by slot count -- n_g8 nodes with <= 8 slots, then n_g16 with
-     * 9..16, n_g32 with 17..32, n_g64 with 33..64 (a group of that many lanes per node),
-     * then n_big nodes with more slots (one thread per node). Built once per graph
-     * (gtf/device.py); a shard's graph view holds the schedule of its own receivers. */
+     * node indices bucketed by slot count -- n_g4 nodes with <= 4 slots (n_g4 is the LAST
+     * field of this struct, added after the others), then n_g8 nodes with <= 8 slots,
+     * n_g16 with 9..16, n_g32 with 17..32, n_g64 with 33..64 (a group of that many lanes
+     * per node), then n_big nodes with more slots (one thread per node). Built once per
+     * graph (gtf/device.py); a shard's graph view holds the schedule of its own receivers. */
     const int32_t* sched;     /* [N] */
     int32_t n_g8;
     int32_t n_g16;
@@ -67,6 +68,8 @@ typedef struct gtf_graph {
                                  scan a dependent gather), or NULL */
     const double* slot_layer; /* [S] layer of each slot's sender (NaN for orphans) = layer[slot_src]:
                                  a coalesced read in the node kernels instead of a gather, or NULL */
+    int32_t n_g4;             /* schedule entries before the n_g8 bucket: nodes with <= 4 slots
+                                 (4 lanes per node; 0 = none, the n_g8 bucket then starts at 0) */
 } gtf_graph;
 
 /* ---- per-node mutable state ------------------------------------------------ */

@@ -27,11 +27,11 @@ def main():
     full = list(d.n_g)
     res = {"n_g": full, "n_big": d.n_big}
     cp = d.cparams(p)
-    for name, keep in (("all", (0, 1, 2, 3)), ("g8", (0,)), ("g16", (1,)), ("g32", (2,)), ("g64", (3,)),
-                       ("none", ())):
+    for name, keep in (("all", (0, 1, 2, 3, 4)), ("g4", (0,)), ("g8", (1,)), ("g16", (2,)), ("g32", (3,)),
+                       ("g64", (4,)), ("none", ())):
         cg = nat.GtfGraph()
         ctypes.memmove(ctypes.byref(cg), ctypes.byref(d.cg), ctypes.sizeof(cg))
-        cg.n_g8, cg.n_g16, cg.n_g32, cg.n_g64 = [full[i] if i in keep else 0 for i in range(4)]
+        cg.n_g4, cg.n_g8, cg.n_g16, cg.n_g32, cg.n_g64 = [full[i] if i in keep else 0 for i in range(5)]
         ts = []
         for r in range(12):
             d.restore(snap)

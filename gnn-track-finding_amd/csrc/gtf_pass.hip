@@ -94,13 +94,16 @@ __global__ void __launch_bounds__(BLOCK) k_sender(gtf_graph g, gtf_nodes n, gtf_
     const int gl = threadIdx.x & (SG - 1);
     if (gi >= count) return;  // group-uniform
     const int u = list ? list[gi] : gi;
-    if (!n.has_merged[u]) return;
+    // the sender's flag, out-range, state and coordinates in one round of loads
+    const uint8_t hm = n.has_merged[u];
     const int ob = g.out_ptr[u], oe = g.out_ptr[u + 1];
-    if (ob == oe) return;
     const double a = n.merged_state[3 * (int64_t)u + 0];
     const double b = n.merged_state[3 * (int64_t)u + 1];
-    const double* ng = g.gnn + 4 * (int64_t)u;
+    const double ngl[4] = {g.gnn[4 * (int64_t)u], g.gnn[4 * (int64_t)u + 1], g.gnn[4 * (int64_t)u + 2],
+                           g.gnn[4 * (int64_t)u + 3]};
+    const double* ng = ngl;
     double carry = n.merged_cov[5 * (int64_t)u + 3];
+    if (!hm || ob == oe) return;
     for (int base = ob; base < oe; base += SG) {
         const int i = base + gl;
         double vm = -1.0;
@@ -108,7 +111,9 @@ __global__ void __launch_bounds__(BLOCK) k_sender(gtf_graph g, gtf_nodes n, gtf_
         if (i < oe) {
             k = g.out_slot[i];
             const int v = g.out_dst ? g.out_dst[i] : g.slot_dst[k];
-            if (e.act[k] == 1) vm = highland_var_ms(a, b, ng, g.gnn + 4 * (int64_t)v, p.endcap_boundary);
+            const double nb[4] = {g.gnn[4 * (int64_t)v], g.gnn[4 * (int64_t)v + 1], g.gnn[4 * (int64_t)v + 2],
+                                  g.gnn[4 * (int64_t)v + 3]};   // loaded beside the activation, not after it
+            if (e.act[k] == 1) vm = highland_var_ms(a, b, ng, nb, p.endcap_boundary);
         }
         double c = carry;
         for (int m = 0; m < SG; m++) {
@@ -130,17 +135,24 @@ __global__ void __launch_bounds__(BLOCK) k_extrapolate(gtf_graph g, gtf_nodes n,
                                                        gtf_params p, Ws w, int slot_lo, int slot_hi) {
     const int k = slot_lo + xcd_local(blockIdx.x, gridDim.x) * BLOCK + threadIdx.x;
     if (k >= slot_hi) return;
+    // Two levels of loads instead of a chain: everything indexed by the slot, then
+    // everything indexed by its sender / receiver, issued before any early exit (the
+    // exits would otherwise serialise each load behind the previous one's branch).
+    const uint8_t is_edge = g.is_edge[k], act = e.act[k];
+    const int src = g.slot_src[k], v = g.slot_dst[k];
+    const double2 vc = w.vc[k];        // written by k_sender for active edges of merged senders
+    const double smw = e.send_mw[k];
     uts.fresh[k] = 0;
-    if (!g.is_edge[k]) return;
-    const int u = g.slot_src[k];
-    if (!n.has_merged[u]) return;
-    if (e.act[k] != 1) return;
-    const int v = g.slot_dst[k];
+    const int u = src >= 0 ? src : 0;   // orphan keys have no sender
     const double* ng = g.gnn + 4 * (int64_t)u;  // sender ("node" in the reference)
     const double* nb = g.gnn + 4 * (int64_t)v;  // receiver ("neighbour")
-    const double node_x = ng[0], node_y = ng[1], node_z = ng[2];
-    const double nbx = nb[0], nby = nb[1], nbz = nb[2];
+    const uint8_t hm = n.has_merged[u];
+    const double node_x = ng[0], node_y = ng[1], node_z = ng[2], node_r = ng[3];
+    const double nbx = nb[0], nby = nb[1], nbz = nb[2], nbr = nb[3];
     const double a = n.merged_state[3 * u + 0], b = n.merged_state[3 * u + 1], c = n.merged_state[3 * u + 2];
+    const double* mcp = n.merged_cov + 5 * (int64_t)u;
+    const double mc00 = mcp[0], mc01 = mcp[1], mc10 = mcp[2], mc22 = mcp[4];
+    if (!is_edge || src < 0 || !hm || act != 1) return;
 
     // cos/sin of atan2(y, x) as x/h, y/h (h = |(x, y)|): the same angles as the
     // reference's atan2 -> cos/sin round trips, to a couple of ulps, without fp64 libm
@@ -177,10 +189,8 @@ __global__ void __launch_bounds__(BLOCK) k_extrapolate(gtf_graph g, gtf_nodes n,
     const double dc_dc = (ds_dc * bracket) + cp;
     const Mat3 F = {{{da_da, da_db, da_dc}, {db_da, db_db, db_dc}, {dc_da, dc_db, dc_dc}}};
 
-    const double2 vc = w.vc[k];
     const double var_ms = vc.x;
-    const double* mcp = n.merged_cov + 5 * (int64_t)u;
-    const Mat3 C = {{{mcp[0], mcp[1], 0.0}, {mcp[2], vc.y, 0.0}, {0.0, 0.0, mcp[4]}}};  // :128
+    const Mat3 C = {{{mc00, mc01, 0.0}, {mc10, vc.y, 0.0}, {0.0, 0.0, mc22}}};  // :128
     const double m[3] = {a, b, c};
     double xe[3];
     mv3(F, m, xe);                                                                 // :129
@@ -219,7 +229,7 @@ __global__ void __launch_bounds__(BLOCK) k_extrapolate(gtf_graph g, gtf_nodes n,
     P11 = P11 + (K1 * sig2) * K1;
 
     // tau and its variance (:326-358) -- NOT squared here, unlike helper.py:421
-    const double dr = nb[3] - ng[3];
+    const double dr = nbr - node_r;
     const double dz = nbz - node_z;
     const double tau = dz / dr;
     double sigma_r = p.sigma0rz, sigma_z = p.sigma0rz2;
@@ -232,7 +242,6 @@ __global__ void __launch_bounds__(BLOCK) k_extrapolate(gtf_graph g, gtf_nodes n,
     vt = vt + (J2 * (sigma_r * sigma_r)) * J2;
     vt = vt + (J3 * (sigma_rn * sigma_rn)) * J3;
 
-    const double smw = e.send_mw[k];
     if (isnan(smw)) raise_flag(w.err, GTF_ERR_SEND_MW_MISSING);
     uts.sv[3 * (int64_t)k + 0] = xu0;
     uts.sv[3 * (int64_t)k + 1] = xu1;
@@ -240,7 +249,7 @@ __global__ void __launch_bounds__(BLOCK) k_extrapolate(gtf_graph g, gtf_nodes n,
     uts.tau[k] = tau;
     store_cov5(uts.cov, k, Cov5{P00, P01, P10, P11, vt + var_ms});
     double* sx = uts.xyzr + 4 * (int64_t)k;
-    sx[0] = ng[0]; sx[1] = ng[1]; sx[2] = ng[2]; sx[3] = ng[3];
+    sx[0] = node_x; sx[1] = node_y; sx[2] = node_z; sx[3] = node_r;
     uts.lik[k] = lik;
     uts.mw[k] = smw;                                                               // :384
     uts.prior[k] = NAN;

@@ -443,11 +443,18 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
 template <int G>
 __device__ __forceinline__ bool node_load(NodeCtx<G>& c, const gtf_graph& g, const gtf_nodes& n,
                                           const gtf_states& tse, const gtf_states& uts, const gtf_edges& e,
-                                          const int32_t* list, int count, int gi, bool uses_tse, bool uses_uts) {
+                                          const int32_t* list, const int32_t* seg, int count, int gi, bool uses_tse,
+                                          bool uses_uts) {
     if (gi >= count) return false;  // group-uniform
     c.v = list[gi];
-    c.lo = g.slot_ptr[c.v];
-    c.d = g.slot_ptr[c.v + 1] - c.lo;
+    if (seg) {  // the slot segment stored beside the schedule entry: no dependent slot_ptr gather
+        const int2 sg = reinterpret_cast<const int2*>(seg)[gi];
+        c.lo = sg.x;
+        c.d = sg.y - sg.x;
+    } else {
+        c.lo = g.slot_ptr[c.v];
+        c.d = g.slot_ptr[c.v + 1] - c.lo;
+    }
     c.k = c.lo + c.grp.gl;
     c.valid = c.grp.gl < c.d;
     const int k = c.k;
@@ -530,13 +537,13 @@ struct OpSeq {
 template <int G, int... OPS>
 __device__ __forceinline__ void node_seq_body(const gtf_graph& g, gtf_nodes& n, gtf_states& tse, gtf_states& uts,
                                               gtf_edges& e, const gtf_params& p, const Ws& w, double chi2_thr,
-                                              double kl_thr, const int32_t* list, int count, int bid,
-                                              char* smem) {
+                                              double kl_thr, const int32_t* list, const int32_t* seg, int count,
+                                              int bid, char* smem) {
     using Q = OpSeq<OPS...>;
     using Stage = StageT<(G < 16 ? G : 16)>;
     NodeCtx<G> c;
     const int gi = (bid * BLOCK + (int)threadIdx.x) / G;
-    if (!node_load(c, g, n, tse, uts, e, list, count, gi, Q::uses_tse, Q::uses_uts)) return;
+    if (!node_load(c, g, n, tse, uts, e, list, seg, count, gi, Q::uses_tse, Q::uses_uts)) return;
     double* sval = (double*)smem + (threadIdx.x & ~63);
     Stage* stg = (Stage*)(smem + BLOCK * sizeof(double)) + (Q::cluster ? (int)threadIdx.x / G : 0);
     const bool has_tse = n.has_tse[c.v], has_uts = n.has_uts[c.v];
@@ -546,6 +553,7 @@ __device__ __forceinline__ void node_seq_body(const gtf_graph& g, gtf_nodes& n, 
 
 struct Buckets {
     const int32_t* list[5];  // node lists for G = 64, 32, 16, 8, 4 (slowest first)
+    const int32_t* seg[5];   // their slot segments (gtf_graph.sched_seg) or NULL
     int32_t count[5];
     int32_t blocks[5];
 };
@@ -575,29 +583,29 @@ __global__ void __launch_bounds__(BLOCK) k_node_multi(gtf_graph g, gtf_nodes n, 
     // the costly nodes of a node range on one XCD.
     int b = blockIdx.x;
     if (b < bk.blocks[0]) {
-        node_seq_body<64, OPS...>(g, n, tse, uts, e, p, w, chi2_thr, kl_thr, bk.list[0], bk.count[0], b,
+        node_seq_body<64, OPS...>(g, n, tse, uts, e, p, w, chi2_thr, kl_thr, bk.list[0], bk.seg[0], bk.count[0], b,
                                   smem);
         return;
     }
     b -= bk.blocks[0];
     if (b < bk.blocks[1]) {
-        node_seq_body<32, OPS...>(g, n, tse, uts, e, p, w, chi2_thr, kl_thr, bk.list[1], bk.count[1], b,
+        node_seq_body<32, OPS...>(g, n, tse, uts, e, p, w, chi2_thr, kl_thr, bk.list[1], bk.seg[1], bk.count[1], b,
                                   smem);
         return;
     }
     b -= bk.blocks[1];
     if (b < bk.blocks[2]) {
-        node_seq_body<16, OPS...>(g, n, tse, uts, e, p, w, chi2_thr, kl_thr, bk.list[2], bk.count[2], b,
+        node_seq_body<16, OPS...>(g, n, tse, uts, e, p, w, chi2_thr, kl_thr, bk.list[2], bk.seg[2], bk.count[2], b,
                                   smem);
         return;
     }
     b -= bk.blocks[2];
     if (b < bk.blocks[3]) {
-        node_seq_body<8, OPS...>(g, n, tse, uts, e, p, w, chi2_thr, kl_thr, bk.list[3], bk.count[3], b, smem);
+        node_seq_body<8, OPS...>(g, n, tse, uts, e, p, w, chi2_thr, kl_thr, bk.list[3], bk.seg[3], bk.count[3], b, smem);
         return;
     }
     b -= bk.blocks[3];
-    node_seq_body<4, OPS...>(g, n, tse, uts, e, p, w, chi2_thr, kl_thr, bk.list[4], bk.count[4], b, smem);
+    node_seq_body<4, OPS...>(g, n, tse, uts, e, p, w, chi2_thr, kl_thr, bk.list[4], bk.seg[4], bk.count[4], b, smem);
 }
 
 // run-time op sequence (gtf_node_ops): any order of any ops
@@ -605,13 +613,13 @@ template <int G>
 __global__ void __launch_bounds__(BLOCK) k_node_group(gtf_graph g, gtf_nodes n, gtf_states tse, gtf_states uts,
                                                       gtf_edges e, gtf_params p, Ws w, NodeOps ops,
                                                       double chi2_thr, double kl_thr, const int32_t* list,
-                                                      int count) {
+                                                      const int32_t* seg, int count) {
     using Stage = StageT<(G < 16 ? G : 16)>;
     __shared__ double s_val[BLOCK];
     __shared__ Stage s_stage[BLOCK / G];
     NodeCtx<G> c;
     const int gi = (blockIdx.x * BLOCK + (int)threadIdx.x) / G;
-    if (!node_load(c, g, n, tse, uts, e, list, count, gi, ops.uses_tse, ops.uses_uts)) return;
+    if (!node_load(c, g, n, tse, uts, e, list, seg, count, gi, ops.uses_tse, ops.uses_uts)) return;
     double* sval = s_val + (threadIdx.x & ~63);
     Stage* stg = s_stage + (int)threadIdx.x / G;
     const bool has_tse = n.has_tse[c.v], has_uts = n.has_uts[c.v];

@@ -653,25 +653,27 @@ int launch_ops(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* ut
     if (g->n_nodes > 0 && ops.n > 0) {
         if (g->sched) {
             const int32_t* l = g->sched;
+            // slot segments of the schedule entries from l on (NULL without sched_seg)
+            auto seg = [&](const int32_t* at) { return g->sched_seg ? g->sched_seg + 2 * (at - g->sched) : nullptr; };
             if (g->n_g4 > 0)
                 hipLaunchKernelGGL(k_node_group<4>, dim3((g->n_g4 + BLOCK / 4 - 1) / (BLOCK / 4)), dim3(BLOCK), 0, st,
-                                   *g, *n, T, U, *e, *p, w, ops, chi2, kl, l, g->n_g4);
+                                   *g, *n, T, U, *e, *p, w, ops, chi2, kl, l, seg(l), g->n_g4);
             l += g->n_g4;
             if (g->n_g8 > 0)
                 hipLaunchKernelGGL(k_node_group<8>, dim3((g->n_g8 + BLOCK / 8 - 1) / (BLOCK / 8)), dim3(BLOCK), 0, st,
-                                   *g, *n, T, U, *e, *p, w, ops, chi2, kl, l, g->n_g8);
+                                   *g, *n, T, U, *e, *p, w, ops, chi2, kl, l, seg(l), g->n_g8);
             l += g->n_g8;
             if (g->n_g16 > 0)
                 hipLaunchKernelGGL(k_node_group<16>, dim3((g->n_g16 + BLOCK / 16 - 1) / (BLOCK / 16)), dim3(BLOCK), 0,
-                                   st, *g, *n, T, U, *e, *p, w, ops, chi2, kl, l, g->n_g16);
+                                   st, *g, *n, T, U, *e, *p, w, ops, chi2, kl, l, seg(l), g->n_g16);
             l += g->n_g16;
             if (g->n_g32 > 0)
                 hipLaunchKernelGGL(k_node_group<32>, dim3((g->n_g32 + BLOCK / 32 - 1) / (BLOCK / 32)), dim3(BLOCK), 0,
-                                   st, *g, *n, T, U, *e, *p, w, ops, chi2, kl, l, g->n_g32);
+                                   st, *g, *n, T, U, *e, *p, w, ops, chi2, kl, l, seg(l), g->n_g32);
             l += g->n_g32;
             if (g->n_g64 > 0)
                 hipLaunchKernelGGL(k_node_group<64>, dim3((g->n_g64 + BLOCK / 64 - 1) / (BLOCK / 64)), dim3(BLOCK), 0,
-                                   st, *g, *n, T, U, *e, *p, w, ops, chi2, kl, l, g->n_g64);
+                                   st, *g, *n, T, U, *e, *p, w, ops, chi2, kl, l, seg(l), g->n_g64);
         }
         launch_serial_rest(g, n, T, U, e, p, w, ops, chi2, kl, st);
     }
@@ -702,6 +704,7 @@ int launch_seq(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* ut
             int total = 0;
             for (int q = 0; q < 5; q++) {
                 bk.list[q] = starts[q];
+                bk.seg[q] = g->sched_seg ? g->sched_seg + 2 * (starts[q] - g->sched) : nullptr;
                 bk.count[q] = cnt[q];
                 bk.blocks[q] = (cnt[q] + BLOCK / gs[q] - 1) / (BLOCK / gs[q]);
                 total += bk.blocks[q];

@@ -28,6 +28,13 @@ MUTABLE_NODE = ("has_merged", "merged_state", "merged_cov", "merged_prior", "has
 STATE_FIELDS = ("rank", "sv", "tau", "cov", "xyzr", "lik", "mw", "prior", "lr", "side", "fresh")
 
 
+def sched_segments(slot_ptr, sched):
+    """gtf_graph.sched_seg: (slot_ptr[v], slot_ptr[v + 1]) of every schedule entry v"""
+    sp = np.asarray(slot_ptr, dtype=np.int64)
+    v = np.asarray(sched, dtype=np.int64)
+    return np.stack([sp[v], sp[v + 1]], axis=1).astype(np.int32).reshape(-1)
+
+
 def _torch():
     import torch
     if not torch.cuda.is_available():
@@ -69,7 +76,9 @@ class DeviceGraph:
         idx = np.arange(g.n_nodes, dtype=np.int32)
         buckets = [idx[(deg >= lo) & (deg <= hi)] for lo, hi in BUCKETS]
         rest = idx[deg > 64]
-        up("sched", np.concatenate(buckets + [rest]).astype(np.int32))
+        sched = np.concatenate(buckets + [rest]).astype(np.int32)
+        up("sched", sched)
+        up("sched_seg", sched_segments(g.slot_ptr, sched))
         self.n_g_all = [int(b.size) for b in buckets]
         self.n_big = int(rest.size)
         self.n_g = self.n_g_all if schedule else [0] * len(BUCKETS)
@@ -121,12 +130,13 @@ class DeviceGraph:
                                p("slot_dst"), p("out_ptr"), p("out_slot"), p("slot_outpos"), p("is_edge"), p("rev_edge"), p("solo"),
                                p("gnn"), p("xyzr"), p("layer"),
                                p("sched") if self.use_sched else ctypes.c_void_p(0), *self.n_g[1:], p("out_dst"),
-                               p("slot_layer"), self.n_g[0])
+                               p("slot_layer"), self.n_g[0], p("sched_seg") if self.use_sched else ctypes.c_void_p(0))
         self.cg_sched = nat.GtfGraph(self.n_nodes, self.n_slots, self.n_edges, self.n_big, p("slot_ptr"),
                                      p("slot_src"),
                                      p("slot_dst"), p("out_ptr"), p("out_slot"), p("slot_outpos"), p("is_edge"),
                                      p("rev_edge"), p("solo"), p("gnn"), p("xyzr"), p("layer"), p("sched"),
-                                     *self.n_g_all[1:], p("out_dst"), p("slot_layer"), self.n_g_all[0])
+                                     *self.n_g_all[1:], p("out_dst"), p("slot_layer"), self.n_g_all[0],
+                                     p("sched_seg"))
         self.cn = nat.GtfNodes(*[p(f) for f in MUTABLE_NODE])
         self.cuts = nat.GtfStates(p("uts_rank"), p("uts_sv"), p("uts_tau"), p("uts_cov"), p("uts_xyzr"),
                                   p("uts_lik"), p("uts_mw"), p("uts_prior"), p("uts_lr"), p("uts_side"),

@@ -92,7 +92,7 @@ class ShardedDeviceGraph:
 
     def __init__(self, g: TrackGraph, rank: int, world: int, device="cuda", backend="nccl", group=None):
         import torch
-        from .device import DeviceGraph
+        from .device import DeviceGraph, sched_segments
         self.torch = torch
         self.rank, self.world, self.backend, self.group = rank, world, backend, group
         self.plan = ShardPlan(g, world)
@@ -103,13 +103,14 @@ class ShardedDeviceGraph:
         self.senders = up(self.plan.senders(rank))
         sched, n_g, n_big = self.plan.schedule(rank)
         self.sched = up(sched)
+        self.sched_seg = up(sched_segments(g.slot_ptr, sched))
         self.ranges = up(self.plan.ranges())
         p = d.ptr
         vp = lambda t: ctypes.c_void_p(t.data_ptr() if t.numel() else 0)  # noqa: E731
         self.cg = nat.GtfGraph(d.n_nodes, d.n_slots, d.n_edges, n_big, p("slot_ptr"), p("slot_src"), p("slot_dst"),
                                p("out_ptr"), p("out_slot"), p("slot_outpos"), p("is_edge"), p("rev_edge"),
                                p("solo"), p("gnn"), p("xyzr"), p("layer"), vp(self.sched), *n_g[1:], p("out_dst"),
-                               p("slot_layer"), n_g[0])
+                               p("slot_layer"), n_g[0], vp(self.sched_seg))
         pl = self.plan
         self.shard = nat.GtfShard(vp(self.senders), int(self.senders.numel()), int(pl.node_lo[rank]),
                                   int(pl.node_hi[rank]), int(pl.slot_lo[rank]), int(pl.slot_hi[rank]))

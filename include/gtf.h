@@ -70,6 +70,9 @@ typedef struct gtf_graph {
                                  a coalesced read in the node kernels instead of a gather, or NULL */
     int32_t n_g4;             /* schedule entries before the n_g8 bucket: nodes with <= 4 slots
                                  (4 lanes per node; 0 = none, the n_g8 bucket then starts at 0) */
+    const int32_t* sched_seg; /* [2*len(sched)] slot segment (slot_ptr[v], slot_ptr[v+1]) of each
+                                 schedule entry v, read beside it: the node kernels then reach the
+                                 slots without a dependent slot_ptr gather; or NULL */
 } gtf_graph;
 
 /* ---- per-node mutable state ------------------------------------------------ */

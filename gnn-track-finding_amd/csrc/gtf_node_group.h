@@ -66,6 +66,9 @@ struct LaneDict {
     bool dirty;
     int pos;         // cached dict position (-1 absent), valid while pos_ok
     bool pos_ok;
+    int last;        // group lane of the last dict key (largest rank), valid while pos_ok
+    bool has_last;   // the dict has a key (valid while pos_ok)
+    bool last_ok;
 };
 
 template <int G>
@@ -78,6 +81,8 @@ struct NodeCtx {
     double layer;
     unsigned long long same_layer;  // lanes whose sender has this lane's layer (lazy)
     bool same_layer_ok;
+    unsigned long long same_x;      // lanes whose stored UTS x equals this lane's (lazy; NaN: itself)
+    bool same_x_ok;
     LaneDict tse, uts;
     double lik, lr, x0, edge_mw;
     int8_t side;
@@ -171,30 +176,41 @@ __device__ __forceinline__ void g_reweight(NodeCtx<G>& c, double* sval, const do
                                            uint32_t* err) {
     LaneDict& st = c.uts;
     const bool act = lane_active(c, st.rank);
-    // last dict key = the present key with the largest rank (stale loop variable, :131,138)
-    const int maxr = c.grp.max_i(c.valid ? st.rank : -1);
-    const unsigned long long lastb = c.grp.bits(c.valid && st.rank == maxr && maxr >= 0);
-    const int last = lastb ? __ffsll((long long)lastb) - 1 : 0;
+    // last dict key = the present key with the largest rank (stale loop variable, :131,138);
+    // kept until the key set changes (ranks / prune)
+    if (!st.last_ok) {
+        const int maxr = c.grp.max_i(c.valid ? st.rank : -1);
+        const unsigned long long lastb = c.grp.bits(c.valid && st.rank == maxr && maxr >= 0);
+        st.last = lastb ? __ffsll((long long)lastb) - 1 : 0;
+        st.last_ok = true;
+    }
+    const int last = st.last;
     const int last_is_edge = c.grp.shfl((int)c.is_edge, last);
     const int last_act = c.grp.shfl((int)c.act, last);
     const double node_x = gnn[4 * (int64_t)c.v];
     const bool left = c.x0 < node_x;
-    // distinct x values per side (len(set(coords))): one iteration per distinct value
-    int dl = 0, dr = 0;
-    {
-        bool done = !act;
+    // distinct x values per side (len(set(coords))): the classes of equal stored x are
+    // built once per node (one iteration per distinct value; a NaN is only equal to
+    // itself, as set() keeps every NaN object); a key counts if it is the first active
+    // key of its class -- equal x, same side
+    if (!c.same_x_ok) {
+        bool done = !c.valid || c.x0 != c.x0;
+        c.same_x = c.valid ? (1ull << c.grp.gl) : 0ull;
         while (true) {
             const unsigned long long todo = c.grp.bits(!done);
             if (!todo) break;
             const int leader = __ffsll((long long)todo) - 1;
             const double X = c.grp.shfl(c.x0, leader);
-            if (X < node_x) dl++; else dr++;
-            if (!done && c.x0 == X) done = true;
-            if (X != X) {  // NaN: set() keeps every NaN object -> each counts once
-                if (c.grp.gl == leader) done = true;
-            }
+            const bool mine = !done && c.x0 == X;
+            const unsigned long long m = c.grp.bits(mine);
+            if (mine) { c.same_x = m; done = true; }
         }
+        c.same_x_ok = true;
     }
+    const unsigned long long A = c.grp.bits(act);
+    const bool first = act && (c.same_x & A & ((1ull << c.grp.gl) - 1ull)) == 0ull;
+    const int dl = c.grp.count(first && left);
+    const int dr = c.grp.count(first && !left);
     const int nact = c.grp.count(act);
     if (nact > 0) {
         if (!last_is_edge && c.grp.gl == 0) atomicOr(err, (uint32_t)GTF_ERR_STALE_KEY_NO_EDGE);
@@ -235,6 +251,7 @@ __device__ __forceinline__ void g_prune(NodeCtx<G>& c, bool has_tse, bool has_ut
         st.dirty = true;
     }
     st.pos_ok = false;
+    st.last_ok = false;
 }
 
 template <int G>
@@ -262,6 +279,7 @@ __device__ __forceinline__ void g_ranks(NodeCtx<G>& c) {
         st.dirty = true;
     }
     st.pos_ok = false;
+    st.last_ok = false;
 }
 
 // per-group LDS staging of up to 15 states (structure of arrays): the state, its
@@ -466,8 +484,10 @@ __device__ __forceinline__ bool node_load(NodeCtx<G>& c, const gtf_graph& g, con
     c.layer = g.slot_layer ? (c.valid ? g.slot_layer[k] : NAN) : (c.src >= 0 ? g.layer[c.src] : NAN);
     c.same_layer = 0;
     c.same_layer_ok = false;
-    c.tse = LaneDict{-1, 0.0, 0.0, false, -1, false};
-    c.uts = LaneDict{-1, 0.0, 0.0, false, -1, false};
+    c.same_x = 0;
+    c.same_x_ok = false;
+    c.tse = LaneDict{-1, 0.0, 0.0, false, -1, false, 0, false, false};
+    c.uts = LaneDict{-1, 0.0, 0.0, false, -1, false, 0, false, false};
     c.lik = 0; c.lr = 0; c.x0 = 0; c.edge_mw = 0; c.side = -1; c.fresh = 0;
     c.uts_dirty_lr = false; c.edge_mw_dirty = false; c.degree = 0; c.degree_set = false;
     if (uses_tse && c.valid) {
@@ -547,7 +567,12 @@ __device__ __forceinline__ void node_seq_body(const gtf_graph& g, gtf_nodes& n, 
     double* sval = (double*)smem + (threadIdx.x & ~63);
     Stage* stg = (Stage*)(smem + BLOCK * sizeof(double)) + (Q::cluster ? (int)threadIdx.x / G : 0);
     const bool has_tse = n.has_tse[c.v], has_uts = n.has_uts[c.v];
+#if GTF_ABLATE == 4
+    // diagnostics build: the node's loads and stores only (every field marked dirty)
+    if (has_tse || has_uts) { c.uts.dirty = true; c.tse.dirty = true; c.uts_dirty_lr = true; c.edge_mw_dirty = true; }
+#else
     (node_op<G, OPS, Stage>(c, g, n, tse, uts, p, w, sval, stg, chi2_thr, kl_thr, has_tse, has_uts), ...);
+#endif
     node_store(c, n, tse, uts, e);
 }
 

@@ -20,7 +20,7 @@ import ctypes
 import numpy as np
 
 from . import _native as nat
-from .graph import BUCKETS, TrackGraph, NODE_FIELDS, SLOT_FIELDS
+from .graph import BUCKETS, TrackGraph, NODE_FIELDS, SLOT_FIELDS, renumber
 from .params import Params
 
 STATIC_SLOT = ("slot_src", "is_edge", "rev_edge", "send_mw")
@@ -42,9 +42,31 @@ def _torch():
     return torch
 
 
+def schedule_order(slot_ptr):
+    """node indices bucketed by slot count as the node-kernel schedule takes them
+    (BUCKETS, then the nodes beyond 64 slots), node order inside a bucket"""
+    deg = np.diff(np.asarray(slot_ptr, dtype=np.int64))
+    idx = np.arange(deg.size, dtype=np.int64)
+    return np.concatenate([idx[(deg >= lo) & (deg <= hi)] for lo, hi in BUCKETS] + [idx[deg > 64]])
+
+
 class DeviceGraph:
-    def __init__(self, g: TrackGraph, device: str = "cuda", schedule: bool = True):
+    """layout "natural": the host graph's node and slot order. layout "schedule": nodes
+    renumbered into schedule order (graph.renumber), so the lane groups of one
+    wavefront take adjacent slot segments and every slot load of the node kernel is
+    one contiguous run; download() maps the results back to the host order. The
+    stage methods are layout-independent (the pass is equivariant under renumber)."""
+
+    def __init__(self, g: TrackGraph, device: str = "cuda", schedule: bool = True, layout: str = "natural"):
         torch = _torch()
+        self.layout = layout
+        self.order = self.slot_perm = None
+        if layout == "schedule":
+            self.order = schedule_order(g.slot_ptr)
+            g, self.slot_perm = renumber(g, self.order)
+        elif layout != "natural":
+            raise ValueError("layout must be 'natural' or 'schedule'")
+        self.slot_ptr_host = g.slot_ptr
         self.torch = torch
         self.device = torch.device(device)
         self.lib = nat.lib()
@@ -223,6 +245,7 @@ class DeviceGraph:
         tse_sv / tse_cov / tse_tau / tse_xyzr / tse_theta / tse_var_ms on the device and
         returns the per-node attributes (xy/zr_edge_gradient_mean_var,
         angle_of_rotation, translation) as device tensors."""
+        self._natural_only("track_state_estimates")
         torch = self.torch
         N = self.n_nodes
         nan = float("nan")
@@ -241,6 +264,7 @@ class DeviceGraph:
     # ------------------------------------------------------- tag propagation
     def tag_propagation(self, tags, radius, threshold=0.1, max_sweeps=100000):
         """Jacobi sweeps until flips / processed <= threshold (tag_propagation.py:137)."""
+        self._natural_only("tag_propagation")
         torch = self.torch
         dev = self.device
         E = self.n_edges
@@ -267,14 +291,26 @@ class DeviceGraph:
 
     # ---------------------------------------------------------------- results
     def download(self, g: TrackGraph) -> TrackGraph:
-        """copy the mutable arrays back into the host TrackGraph (in place)"""
+        """copy the mutable arrays back into the host TrackGraph (in place, host order)"""
         for f in MUTABLE_NODE:
-            g.node[f][...] = self.t[f].cpu().numpy().reshape(g.node[f].shape)
+            a = self.t[f].cpu().numpy().reshape(g.node[f].shape)
+            if self.order is None:
+                g.node[f][...] = a
+            else:
+                g.node[f][self.order] = a
         for f in SLOT_FIELDS:
             if f in STATIC_SLOT or f == "slot_key":
                 continue
-            g.slot[f][...] = self.t[f].cpu().numpy().reshape(g.slot[f].shape)
+            a = self.t[f].cpu().numpy().reshape(g.slot[f].shape)
+            if self.slot_perm is None:
+                g.slot[f][...] = a
+            else:
+                g.slot[f][self.slot_perm] = a
         return g
+
+    def _natural_only(self, what):
+        if self.layout != "natural":
+            raise NotImplementedError("%s takes node-indexed host arrays: use layout='natural'" % what)
 
     # arrays whose values decide how much work the next pass does: restoring
     # them makes every benchmark step process the same input

@@ -178,6 +178,47 @@ def check_layout(g: TrackGraph) -> None:
         assert g.slot[name].shape == (S,) + shape and g.slot[name].dtype == dt, name
 
 
+def renumber(g: TrackGraph, order) -> tuple:
+    """The same graph with node i' = order[i'] of g: node arrays permuted, every
+    receiver's slot segment moved along unchanged (its slots keep their order, so
+    dict insertion order and the reference's per-receiver orders are untouched),
+    slot_src remapped, every sender's out-list kept in successor order. The pass is
+    equivariant under this relabelling (its semantics reach node order only through
+    slot order, out-list order and explicit dict ranks). Returns (graph, slot_perm)
+    with new slot s' = old slot slot_perm[s']; g.node[f][order] and
+    g.slot[f][slot_perm] give the new arrays, and the inverse scatters them back."""
+    order = np.asarray(order, dtype=np.int64)
+    N = g.n_nodes
+    if order.shape != (N,) or (N and not np.array_equal(np.sort(order), np.arange(N))):
+        raise ValueError("order must be a permutation of the %d nodes" % N)
+    sp = g.slot_ptr.astype(np.int64)
+    deg = np.diff(sp)
+    new_sp = np.zeros(N + 1, np.int64)
+    np.cumsum(deg[order], out=new_sp[1:])
+    # new slot s' of new node i' (offset j in its segment) = old slot sp[order[i']] + j
+    owner = np.repeat(np.arange(N, dtype=np.int64), deg[order])
+    slot_perm = sp[order][owner] + (np.arange(new_sp[-1]) - new_sp[owner]) if N else np.zeros(0, np.int64)
+    new_of_old_node = np.empty(N, np.int64)
+    new_of_old_node[order] = np.arange(N)
+    new_of_old_slot = np.empty(g.n_slots, np.int64)
+    new_of_old_slot[slot_perm] = np.arange(g.n_slots)
+    node = {k: v[order].copy() for k, v in g.node.items()}
+    slot = {k: v[slot_perm].copy() for k, v in g.slot.items()}
+    src = slot["slot_src"].astype(np.int64)
+    slot["slot_src"] = np.where(src >= 0, new_of_old_node[np.maximum(src, 0)], -1).astype(g.slot["slot_src"].dtype)
+    op = g.out_ptr.astype(np.int64)
+    odeg = np.diff(op)
+    new_op = np.zeros(N + 1, np.int64)
+    np.cumsum(odeg[order], out=new_op[1:])
+    oown = np.repeat(np.arange(N, dtype=np.int64), odeg[order])
+    old_pos = op[order][oown] + (np.arange(new_op[-1]) - new_op[oown]) if N else np.zeros(0, np.int64)
+    out_slot = new_of_old_slot[g.out_slot.astype(np.int64)[old_pos]] if g.n_edges else g.out_slot.copy()
+    h = TrackGraph(N, g.n_slots, new_sp.astype(np.int32), new_op.astype(np.int32), out_slot.astype(np.int32),
+                   node, slot, g.n_subgraphs)
+    check_layout(h)
+    return h, slot_perm
+
+
 # --------------------------------------------------------------------------
 # pack: list[nx.DiGraph] -> TrackGraph
 # --------------------------------------------------------------------------

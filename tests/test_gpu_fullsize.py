@@ -29,13 +29,18 @@ def c4():
 
 def _state(d):
     """every array a pass may write (DeviceGraph.snapshot's default set)"""
-    return {k: v.cpu().numpy() for k, v in d.snapshot().items()}
+    return {k: v.cpu().numpy().reshape(-1) for k, v in d.snapshot().items()}
+
+
+def _state_keys(g):
+    from gtf.device import MUTABLE_NODE, STATIC_SLOT
+    return set(MUTABLE_NODE) | {k for k in g.slot if k not in STATIC_SLOT and k != "slot_key"}
 
 
 def _same(a, b, what):
     assert a.keys() == b.keys()
     for k in a:
-        x, y = a[k], b[k]
+        x, y = np.asarray(a[k]).reshape(-1), np.asarray(b[k]).reshape(-1)
         if x.dtype.kind == "f":
             eq = (x == y) | (np.isnan(x) & np.isnan(y))
         else:
@@ -45,6 +50,13 @@ def _same(a, b, what):
 
 def _run(g, how, p):
     from gtf.device import DeviceGraph
+    if how == "schedule_layout":   # nodes renumbered into schedule order, results mapped back
+        d = DeviceGraph(g, layout="schedule")
+        d.clear_errors()
+        d.full_pass(p)
+        got = d.download(g.copy())
+        return ({k: v for k, v in list(got.node.items()) + list(got.slot.items()) if k in _state_keys(g)},
+                d.errors())
     d = DeviceGraph(g, schedule=(how != "thread_per_node"))
     d.clear_errors()
     if how in ("fused", "thread_per_node"):
@@ -66,7 +78,7 @@ def test_fused_pass_equals_stagewise_and_other_implementations(c4):
     p = Params()
     ref, ref_flags = _run(c4, "fused", p)
     assert ref["act"].sum() > 0 and ref["has_merged"].sum() > 0
-    for how in ("stages", "interpreter", "thread_per_node"):
+    for how in ("stages", "interpreter", "thread_per_node", "schedule_layout"):
         got, flags = _run(c4, how, p)
         assert flags == ref_flags, how
         _same(got, ref, how)

@@ -1,0 +1,41 @@
+"""graph.renumber (the DeviceGraph "schedule" layout) on the host: a relabelling that
+keeps every receiver's slot segment and every sender's out-list in order."""
+import numpy as np
+
+from gtf import graph, synth
+from gtf.device import schedule_order
+
+
+def test_renumber_round_trip_and_layout():
+    g = synth.event(seed=2, n_tracks=200, fake_mean=synth.C4_FAKE)
+    order = np.random.default_rng(1).permutation(g.n_nodes)
+    h, perm = graph.renumber(g, order)
+    # segments move whole: the new segment of node i' is the old segment of order[i']
+    assert np.array_equal(np.diff(h.slot_ptr), np.diff(g.slot_ptr)[order])
+    assert np.array_equal(h.slot["act"], g.slot["act"][perm])
+    # slot_src relabelled, same sender per slot
+    src_old = g.slot["slot_src"][perm]
+    assert np.array_equal(np.where(src_old >= 0, np.argsort(order)[np.maximum(src_old, 0)], -1), h.slot["slot_src"])
+    # each sender's successors, in order, are the same receivers
+    inv = np.argsort(order)
+    for u in range(0, g.n_nodes, 97):
+        a = g.slot_dst()[g.out_slot[g.out_ptr[u]:g.out_ptr[u + 1]]]
+        b = h.slot_dst()[h.out_slot[h.out_ptr[inv[u]]:h.out_ptr[inv[u] + 1]]]
+        assert np.array_equal(inv[a], b)
+    # the inverse relabelling restores every array
+    back, perm2 = graph.renumber(h, np.argsort(order))
+    for k in g.node:
+        assert np.array_equal(back.node[k], g.node[k], equal_nan=True), k
+    for k in g.slot:
+        assert np.array_equal(back.slot[k], g.slot[k], equal_nan=g.slot[k].dtype.kind == "f"), k
+    assert np.array_equal(back.out_slot, g.out_slot) and np.array_equal(back.slot_ptr, g.slot_ptr)
+
+
+def test_schedule_order_groups_buckets():
+    g = synth.event(seed=5, n_tracks=300, fake_mean=synth.C4_FAKE)
+    order = schedule_order(g.slot_ptr)
+    assert np.array_equal(np.sort(order), np.arange(g.n_nodes))
+    h, _ = graph.renumber(g, order)
+    deg = np.diff(h.slot_ptr)
+    bucket = np.searchsorted([4, 8, 16, 32, 64], deg)   # 0..5 = g4, g8, g16, g32, g64, beyond
+    assert np.all(np.diff(bucket) >= 0)                  # one contiguous node range per bucket

@@ -87,16 +87,12 @@ __device__ __forceinline__ double highland_var_ms(double a, double b, const doub
 // (var_ms, running value) record goes to the edge's slot, where k_extrapolate reads
 // it coalesced instead of gathering it through the sender's out-list.
 // ---------------------------------------------------------------------------
-constexpr int SG = 8;
-__global__ void __launch_bounds__(BLOCK) k_sender(gtf_graph g, gtf_nodes n, gtf_edges e, gtf_params p, Ws w,
-                                                  const int32_t* list, int count) {
-    const int gi = (xcd_local(blockIdx.x, gridDim.x) * BLOCK + (int)threadIdx.x) / SG;
-    const int gl = threadIdx.x & (SG - 1);
-    if (gi >= count) return;  // group-uniform
-    const int u = list ? list[gi] : gi;
-    // the sender's flag, out-range, state and coordinates in one round of loads
+// one sender u over its out-list [ob, oe) with SG lanes (lane gl), chunks of SG
+template <int SG>
+__device__ __forceinline__ void sender_scan(const gtf_graph& g, gtf_nodes& n, const gtf_edges& e,
+                                            const gtf_params& p, const Ws& w, int u, int ob, int oe, int gl) {
+    // the sender's flag, state and coordinates in one round of loads
     const uint8_t hm = n.has_merged[u];
-    const int ob = g.out_ptr[u], oe = g.out_ptr[u + 1];
     const double a = n.merged_state[3 * (int64_t)u + 0];
     const double b = n.merged_state[3 * (int64_t)u + 1];
     const double ngl[4] = {g.gnn[4 * (int64_t)u], g.gnn[4 * (int64_t)u + 1], g.gnn[4 * (int64_t)u + 2],
@@ -126,6 +122,46 @@ __global__ void __launch_bounds__(BLOCK) k_sender(gtf_graph g, gtf_nodes n, gtf_
         carry = __shfl(c, SG - 1, SG);  // lanes past the end carry the full sum
     }
     if (gl == 0) n.merged_cov[5 * (int64_t)u + 3] = carry;
+}
+
+// every node (list NULL) or a list of senders (a shard's), 8 lanes per sender
+constexpr int SG = 8;
+__global__ void __launch_bounds__(BLOCK) k_sender(gtf_graph g, gtf_nodes n, gtf_edges e, gtf_params p, Ws w,
+                                                  const int32_t* list, int count) {
+    const int gi = (xcd_local(blockIdx.x, gridDim.x) * BLOCK + (int)threadIdx.x) / SG;
+    if (gi >= count) return;  // group-uniform
+    const int u = list ? list[gi] : gi;
+    sender_scan<SG>(g, n, e, p, w, u, g.out_ptr[u], g.out_ptr[u + 1], threadIdx.x & (SG - 1));
+}
+
+// the sender schedule (gtf_graph.out_sched): senders with 1..4 out-edges on 4 lanes,
+// 5..8 on 8, more on 16, each entry carrying the sender's out-range (no dependent
+// out_ptr gather). One launch; each bucket's blocks form a range padded to a multiple
+// of 8, XCD-contiguous inside the range (neighbouring senders' receivers share an L2).
+struct SendBuckets {
+    const int4* list[3];
+    int32_t count[3];
+    int32_t blocks[3];  // padded to multiples of 8
+};
+
+template <int G>
+__device__ __forceinline__ void sender_bucket(const gtf_graph& g, gtf_nodes& n, const gtf_edges& e,
+                                              const gtf_params& p, const Ws& w, const int4* list, int count,
+                                              int b, int nb) {
+    const int gi = (xcd_local(b, nb) * BLOCK + (int)threadIdx.x) / G;
+    if (gi >= count) return;  // group-uniform
+    const int4 en = list[gi];
+    sender_scan<G>(g, n, e, p, w, en.x, en.y, en.z, threadIdx.x & (G - 1));
+}
+
+__global__ void __launch_bounds__(BLOCK) k_sender_sched(gtf_graph g, gtf_nodes n, gtf_edges e, gtf_params p, Ws w,
+                                                        SendBuckets sb) {
+    int b = blockIdx.x;
+    if (b < sb.blocks[0]) { sender_bucket<4>(g, n, e, p, w, sb.list[0], sb.count[0], b, sb.blocks[0]); return; }
+    b -= sb.blocks[0];
+    if (b < sb.blocks[1]) { sender_bucket<8>(g, n, e, p, w, sb.list[1], sb.count[1], b, sb.blocks[1]); return; }
+    b -= sb.blocks[1];
+    sender_bucket<16>(g, n, e, p, w, sb.list[2], sb.count[2], b, sb.blocks[2]);
 }
 
 // ---------------------------------------------------------------------------
@@ -592,9 +628,26 @@ int launch_extrap_edges(const gtf_graph* g, gtf_nodes* n, gtf_states* uts, gtf_e
     const int count = sh ? sh->n_senders : g->n_nodes;
     const int slot_lo = sh ? sh->slot_lo : 0, slot_hi = sh ? sh->slot_hi : g->n_slots;
     if (events) (void)hipEventRecord((hipEvent_t)events[0], st);
-    if (g->n_slots > 0 && count > 0)
-        hipLaunchKernelGGL(k_sender, dim3((count + BLOCK / SG - 1) / (BLOCK / SG)), dim3(BLOCK), 0, st, *g, *n, *e,
-                           *p, w, list, count);
+    if (g->n_slots > 0 && count > 0) {
+        if (!sh && g->out_sched) {
+            SendBuckets sb;
+            const int cnt[3] = {g->n_o4, g->n_o8, g->n_o16}, gs[3] = {4, 8, 16};
+            const int4* l = reinterpret_cast<const int4*>(g->out_sched);
+            int total = 0;
+            for (int q = 0; q < 3; q++) {
+                sb.list[q] = l;
+                l += cnt[q];
+                sb.count[q] = cnt[q];
+                sb.blocks[q] = pad8((cnt[q] + BLOCK / gs[q] - 1) / (BLOCK / gs[q]));
+                total += sb.blocks[q];
+            }
+            if (total > 0)
+                hipLaunchKernelGGL(k_sender_sched, dim3(total), dim3(BLOCK), 0, st, *g, *n, *e, *p, w, sb);
+        } else {
+            hipLaunchKernelGGL(k_sender, dim3((count + BLOCK / SG - 1) / (BLOCK / SG)), dim3(BLOCK), 0, st, *g, *n,
+                               *e, *p, w, list, count);
+        }
+    }
     if (events) (void)hipEventRecord((hipEvent_t)events[1], st);
     if (slot_hi > slot_lo)
         hipLaunchKernelGGL(k_extrapolate, dim3(grid(slot_hi - slot_lo)), dim3(BLOCK), 0, st, *g, *n, *uts, *e, *p,

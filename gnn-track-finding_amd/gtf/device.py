@@ -35,6 +35,18 @@ def sched_segments(slot_ptr, sched):
     return np.stack([sp[v], sp[v + 1]], axis=1).astype(np.int32).reshape(-1)
 
 
+def sender_schedule(out_ptr):
+    """gtf_graph.out_sched: (sender, out begin, out end, 0) of every node with an
+    out-edge, bucketed by out-degree 1..4 / 5..8 / more; returns (array, counts)"""
+    op = np.asarray(out_ptr, dtype=np.int64)
+    od = np.diff(op)
+    idx = np.arange(od.size, dtype=np.int64)
+    parts = [idx[(od >= 1) & (od <= 4)], idx[(od >= 5) & (od <= 8)], idx[od > 8]]
+    u = np.concatenate(parts)
+    q = np.stack([u, op[u], op[u + 1], np.zeros_like(u)], axis=1).astype(np.int32).reshape(-1)
+    return q, [int(x.size) for x in parts]
+
+
 def _torch():
     import torch
     if not torch.cuda.is_available():
@@ -101,6 +113,8 @@ class DeviceGraph:
         sched = np.concatenate(buckets + [rest]).astype(np.int32)
         up("sched", sched)
         up("sched_seg", sched_segments(g.slot_ptr, sched))
+        osched, self.n_o = sender_schedule(g.out_ptr)
+        up("out_sched", osched)
         self.n_g_all = [int(b.size) for b in buckets]
         self.n_big = int(rest.size)
         self.n_g = self.n_g_all if schedule else [0] * len(BUCKETS)
@@ -152,13 +166,14 @@ class DeviceGraph:
                                p("slot_dst"), p("out_ptr"), p("out_slot"), p("slot_outpos"), p("is_edge"), p("rev_edge"), p("solo"),
                                p("gnn"), p("xyzr"), p("layer"),
                                p("sched") if self.use_sched else ctypes.c_void_p(0), *self.n_g[1:], p("out_dst"),
-                               p("slot_layer"), self.n_g[0], p("sched_seg") if self.use_sched else ctypes.c_void_p(0))
+                               p("slot_layer"), self.n_g[0], p("sched_seg") if self.use_sched else ctypes.c_void_p(0),
+                               p("out_sched") if self.use_sched else ctypes.c_void_p(0), *self.n_o)
         self.cg_sched = nat.GtfGraph(self.n_nodes, self.n_slots, self.n_edges, self.n_big, p("slot_ptr"),
                                      p("slot_src"),
                                      p("slot_dst"), p("out_ptr"), p("out_slot"), p("slot_outpos"), p("is_edge"),
                                      p("rev_edge"), p("solo"), p("gnn"), p("xyzr"), p("layer"), p("sched"),
                                      *self.n_g_all[1:], p("out_dst"), p("slot_layer"), self.n_g_all[0],
-                                     p("sched_seg"))
+                                     p("sched_seg"), p("out_sched"), *self.n_o)
         self.cn = nat.GtfNodes(*[p(f) for f in MUTABLE_NODE])
         self.cuts = nat.GtfStates(p("uts_rank"), p("uts_sv"), p("uts_tau"), p("uts_cov"), p("uts_xyzr"),
                                   p("uts_lik"), p("uts_mw"), p("uts_prior"), p("uts_lr"), p("uts_side"),

@@ -73,6 +73,14 @@ typedef struct gtf_graph {
     const int32_t* sched_seg; /* [2*len(sched)] slot segment (slot_ptr[v], slot_ptr[v+1]) of each
                                  schedule entry v, read beside it: the node kernels then reach the
                                  slots without a dependent slot_ptr gather; or NULL */
+    /* optional sender schedule for the var_ms scan (NULL = 8 lanes for every node): one
+     * (sender, out_ptr[sender], out_ptr[sender+1], 0) int32 quadruple per sender with an
+     * out-edge -- n_o4 senders with 1..4 out-edges (4 lanes each), then n_o8 with 5..8
+     * (8 lanes), then n_o16 with more (16 lanes). Not used by gtf_pass_shard. */
+    const int32_t* out_sched;  /* [4*(n_o4+n_o8+n_o16)] */
+    int32_t n_o4;
+    int32_t n_o8;
+    int32_t n_o16;
 } gtf_graph;
 
 /* ---- per-node mutable state ------------------------------------------------ */

@@ -39,3 +39,20 @@ def test_schedule_order_groups_buckets():
     deg = np.diff(h.slot_ptr)
     bucket = np.searchsorted([4, 8, 16, 32, 64], deg)   # 0..5 = g4, g8, g16, g32, g64, beyond
     assert np.all(np.diff(bucket) >= 0)                  # one contiguous node range per bucket
+
+
+def test_schedule_arrays():
+    """gtf_graph.sched_seg and out_sched as DeviceGraph uploads them"""
+    from gtf.device import sched_segments, sender_schedule
+    g = synth.event(seed=6, n_tracks=150, fake_mean=synth.C4_FAKE)
+    order = schedule_order(g.slot_ptr)
+    seg = sched_segments(g.slot_ptr, order).reshape(-1, 2)
+    assert np.array_equal(seg[:, 0], g.slot_ptr[order]) and np.array_equal(seg[:, 1], g.slot_ptr[order + 1])
+    q, counts = sender_schedule(g.out_ptr)
+    q = q.reshape(-1, 4)
+    od = np.diff(g.out_ptr)
+    assert sum(counts) == int((od > 0).sum()) == q.shape[0]
+    u = q[:, 0]
+    assert np.array_equal(q[:, 1], g.out_ptr[u]) and np.array_equal(q[:, 2], g.out_ptr[u + 1])
+    b = np.repeat([0, 1, 2], counts)
+    assert np.all(od[u][b == 0] <= 4) and np.all((od[u][b == 1] >= 5) & (od[u][b == 1] <= 8)) and np.all(od[u][b == 2] > 8)

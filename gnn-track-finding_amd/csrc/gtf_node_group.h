@@ -60,10 +60,12 @@ struct Grp {
 };
 
 // per-lane (per-slot) registers of one state dict
+enum : uint8_t { D_RANK = 1, D_MW = 2, D_PRIOR = 4 };  // LaneDict.dirty: fields to store
+
 struct LaneDict {
     int rank;
     double mw, prior;
-    bool dirty;
+    uint8_t dirty;   // D_* bits of the fields an op changed
     int pos;         // cached dict position (-1 absent), valid while pos_ok
     bool pos_ok;
     int last;        // group lane of the last dict key (largest rank), valid while pos_ok
@@ -77,7 +79,6 @@ struct NodeCtx {
     int v, lo, d, k;
     bool valid;
     uint8_t is_edge, rev_edge, act, act0;
-    int src;
     double layer;
     unsigned long long same_layer;  // lanes whose sender has this lane's layer (lazy)
     bool same_layer_ok;
@@ -166,7 +167,7 @@ __device__ __forceinline__ void g_priors(NodeCtx<G>& c, LaneDict& st) {
     const unsigned long long A = c.grp.bits(act);
     if (act) {
         st.prior = 1.0 / (double)__popcll(A & c.same_layer);
-        st.dirty = true;
+        st.dirty |= D_PRIOR;
     }
 }
 
@@ -225,7 +226,7 @@ __device__ __forceinline__ void g_reweight(NodeCtx<G>& c, double* sval, const do
         double wgt = (st.mw * c.lik * st.prior) / denom;
         wgt = wgt / c.lr;
         st.mw = wgt;
-        st.dirty = true;
+        st.dirty |= D_MW;
         c.edge_mw = wgt;
         c.edge_mw_dirty = true;
         c.act = (wgt < thr) ? 0 : 1;
@@ -248,7 +249,7 @@ __device__ __forceinline__ void g_prune(NodeCtx<G>& c, bool has_tse, bool has_ut
     LaneDict& st = has_uts ? c.uts : c.tse;
     if (c.valid && st.rank >= 0 && !c.rev_edge) {
         st.rank = -1;
-        st.dirty = true;
+        st.dirty |= D_RANK;
     }
     st.pos_ok = false;
     st.last_ok = false;
@@ -263,7 +264,7 @@ __device__ __forceinline__ void g_mixture_weights(NodeCtx<G>& c, LaneDict& st, b
     }
     if (c.valid && st.rank >= 0) {
         st.mw = 1.0 / (double)cnt;
-        st.dirty = true;
+        st.dirty |= D_MW;
     }
 }
 
@@ -276,7 +277,7 @@ __device__ __forceinline__ void g_ranks(NodeCtx<G>& c) {
     if (isnew) {
         const unsigned long long below = nb & ((1ull << c.grp.gl) - 1ull);
         st.rank = maxr + 1 + __popcll(below);
-        st.dirty = true;
+        st.dirty |= D_RANK;
     }
     st.pos_ok = false;
     st.last_ok = false;
@@ -458,11 +459,16 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
 // ---------------------------------------------------------------------------
 // kernels: load a node's slots into lane registers, run the ops, write back
 // ---------------------------------------------------------------------------
+// the per-slot fields an op sequence reads from memory (the others it only writes)
+struct Need {
+    bool tse_rank, tse_prior, uts_rank, uts_mw, uts_prior, uts_lik, uts_x0, uts_fresh;
+};
+
 template <int G>
 __device__ __forceinline__ bool node_load(NodeCtx<G>& c, const gtf_graph& g, const gtf_nodes& n,
                                           const gtf_states& tse, const gtf_states& uts, const gtf_edges& e,
-                                          const int32_t* list, const int32_t* seg, int count, int gi, bool uses_tse,
-                                          bool uses_uts) {
+                                          const int32_t* list, const int32_t* seg, int count, int gi,
+                                          const Need& nd) {
     if (gi >= count) return false;  // group-uniform
     c.v = list[gi];
     if (seg) {  // the slot segment stored beside the schedule entry: no dependent slot_ptr gather
@@ -480,30 +486,31 @@ __device__ __forceinline__ bool node_load(NodeCtx<G>& c, const gtf_graph& g, con
     c.rev_edge = c.valid ? g.rev_edge[k] : 0;
     c.act = c.valid ? e.act[k] : 0;
     c.act0 = c.act;
-    c.src = c.valid ? g.slot_src[k] : -1;
-    c.layer = g.slot_layer ? (c.valid ? g.slot_layer[k] : NAN) : (c.src >= 0 ? g.layer[c.src] : NAN);
+    if (g.slot_layer) {
+        c.layer = c.valid ? g.slot_layer[k] : NAN;
+    } else {
+        const int src = c.valid ? g.slot_src[k] : -1;
+        c.layer = src >= 0 ? g.layer[src] : NAN;
+    }
     c.same_layer = 0;
     c.same_layer_ok = false;
     c.same_x = 0;
     c.same_x_ok = false;
-    c.tse = LaneDict{-1, 0.0, 0.0, false, -1, false, 0, false, false};
-    c.uts = LaneDict{-1, 0.0, 0.0, false, -1, false, 0, false, false};
+    c.tse = LaneDict{-1, 0.0, 0.0, 0, -1, false, 0, false, false};
+    c.uts = LaneDict{-1, 0.0, 0.0, 0, -1, false, 0, false, false};
     c.lik = 0; c.lr = 0; c.x0 = 0; c.edge_mw = 0; c.side = -1; c.fresh = 0;
     c.uts_dirty_lr = false; c.edge_mw_dirty = false; c.degree = 0; c.degree_set = false;
-    if (uses_tse && c.valid) {
-        c.tse.rank = tse.rank[k];
-        c.tse.mw = tse.mw[k];
-        c.tse.prior = tse.prior[k];
-    }
-    if (uses_uts && c.valid) {
-        c.uts.rank = uts.rank[k];
-        c.uts.mw = uts.mw[k];
-        c.uts.prior = uts.prior[k];
-        c.lik = uts.lik[k];
-        c.lr = uts.lr[k];
-        c.side = uts.side[k];
-        c.x0 = uts.xyzr[4 * (int64_t)k];
-        c.fresh = uts.fresh[k];
+    // only what an op reads: mw of the TSE dict, lr and side are written, never read
+    // (the reweight sets lr / side of every key it weighs before using them)
+    if (c.valid) {
+        if (nd.tse_rank) c.tse.rank = tse.rank[k];
+        if (nd.tse_prior) c.tse.prior = tse.prior[k];
+        if (nd.uts_rank) c.uts.rank = uts.rank[k];
+        if (nd.uts_mw) c.uts.mw = uts.mw[k];
+        if (nd.uts_prior) c.uts.prior = uts.prior[k];
+        if (nd.uts_lik) c.lik = uts.lik[k];
+        if (nd.uts_x0) c.x0 = uts.xyzr[4 * (int64_t)k];
+        if (nd.uts_fresh) c.fresh = uts.fresh[k];
     }
     return true;
 }
@@ -515,8 +522,12 @@ __device__ __forceinline__ void node_store(NodeCtx<G>& c, gtf_nodes& n, gtf_stat
     if (c.valid) {
         if (c.act != c.act0) e.act[k] = c.act;
         if (c.edge_mw_dirty) e.edge_mw[k] = c.edge_mw;
-        if (c.tse.dirty) { tse.rank[k] = c.tse.rank; tse.mw[k] = c.tse.mw; tse.prior[k] = c.tse.prior; }
-        if (c.uts.dirty) { uts.rank[k] = c.uts.rank; uts.mw[k] = c.uts.mw; uts.prior[k] = c.uts.prior; }
+        if (c.tse.dirty & D_RANK) tse.rank[k] = c.tse.rank;
+        if (c.tse.dirty & D_MW) tse.mw[k] = c.tse.mw;
+        if (c.tse.dirty & D_PRIOR) tse.prior[k] = c.tse.prior;
+        if (c.uts.dirty & D_RANK) uts.rank[k] = c.uts.rank;
+        if (c.uts.dirty & D_MW) uts.mw[k] = c.uts.mw;
+        if (c.uts.dirty & D_PRIOR) uts.prior[k] = c.uts.prior;
         if (c.uts_dirty_lr) { uts.lr[k] = c.lr; uts.side[k] = c.side; }
     }
     if (c.degree_set && c.grp.gl == 0) n.degree[c.v] = c.degree;
@@ -550,6 +561,10 @@ struct OpSeq {
     static constexpr bool uses_uts = ((OPS == OP_RANKS || OPS == OP_PRIORS_UTS || OPS == OP_REWEIGHT_UTS ||
                                        OPS == OP_MW_UTS || OPS == OP_CLUSTER_UTS || OPS == OP_PRUNE) || ...);
     static constexpr bool cluster = ((OPS == OP_CLUSTER_TSE || OPS == OP_CLUSTER_UTS) || ...);
+    static constexpr bool reweight = ((OPS == OP_REWEIGHT_UTS) || ...);
+    static constexpr Need need{uses_tse, ((OPS == OP_CLUSTER_TSE) || ...), uses_uts, reweight,
+                               reweight || ((OPS == OP_CLUSTER_UTS) || ...), reweight, reweight,
+                               ((OPS == OP_RANKS) || ...)};
 };
 
 // compile-time op sequence for one group size: dead ops are compiled out.
@@ -563,13 +578,13 @@ __device__ __forceinline__ void node_seq_body(const gtf_graph& g, gtf_nodes& n, 
     using Stage = StageT<(G < 16 ? G : 16)>;
     NodeCtx<G> c;
     const int gi = (bid * BLOCK + (int)threadIdx.x) / G;
-    if (!node_load(c, g, n, tse, uts, e, list, seg, count, gi, Q::uses_tse, Q::uses_uts)) return;
+    if (!node_load(c, g, n, tse, uts, e, list, seg, count, gi, Q::need)) return;
     double* sval = (double*)smem + (threadIdx.x & ~63);
     Stage* stg = (Stage*)(smem + BLOCK * sizeof(double)) + (Q::cluster ? (int)threadIdx.x / G : 0);
     const bool has_tse = n.has_tse[c.v], has_uts = n.has_uts[c.v];
 #if GTF_ABLATE == 4
     // diagnostics build: the node's loads and stores only (every field marked dirty)
-    if (has_tse || has_uts) { c.uts.dirty = true; c.tse.dirty = true; c.uts_dirty_lr = true; c.edge_mw_dirty = true; }
+    if (has_tse || has_uts) { c.uts.dirty = c.tse.dirty = D_RANK | D_MW | D_PRIOR; c.uts_dirty_lr = true; c.edge_mw_dirty = true; }
 #else
     (node_op<G, OPS, Stage>(c, g, n, tse, uts, p, w, sval, stg, chi2_thr, kl_thr, has_tse, has_uts), ...);
 #endif
@@ -644,7 +659,9 @@ __global__ void __launch_bounds__(BLOCK) k_node_group(gtf_graph g, gtf_nodes n, 
     __shared__ Stage s_stage[BLOCK / G];
     NodeCtx<G> c;
     const int gi = (blockIdx.x * BLOCK + (int)threadIdx.x) / G;
-    if (!node_load(c, g, n, tse, uts, e, list, seg, count, gi, ops.uses_tse, ops.uses_uts)) return;
+    const Need nd{(bool)ops.uses_tse, (bool)ops.uses_tse, (bool)ops.uses_uts, (bool)ops.uses_uts,
+                  (bool)ops.uses_uts, (bool)ops.uses_uts, (bool)ops.uses_uts, (bool)ops.uses_uts};
+    if (!node_load(c, g, n, tse, uts, e, list, seg, count, gi, nd)) return;
     double* sval = s_val + (threadIdx.x & ~63);
     Stage* stg = s_stage + (int)threadIdx.x / G;
     const bool has_tse = n.has_tse[c.v], has_uts = n.has_uts[c.v];

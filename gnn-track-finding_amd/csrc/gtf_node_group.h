@@ -592,16 +592,17 @@ __device__ __forceinline__ void node_seq_body(const gtf_graph& g, gtf_nodes& n, 
 }
 
 struct Buckets {
-    const int32_t* list[5];  // node lists for G = 64, 32, 16, 8, 4 (slowest first)
-    const int32_t* seg[5];   // their slot segments (gtf_graph.sched_seg) or NULL
-    int32_t count[5];
-    int32_t blocks[5];
+    const int32_t* list[6];  // node lists for G = 64, 32, 16, 8, 4, 2 (slowest first)
+    const int32_t* seg[6];   // their slot segments (gtf_graph.sched_seg) or NULL
+    int32_t count[6];
+    int32_t blocks[6];
 };
 
 template <int G>
 constexpr size_t stage_bytes() { return (size_t)(BLOCK / G) * sizeof(StageT<(G < 16 ? G : 16)>); }
 constexpr size_t node_smem_bytes() {
-    size_t m = stage_bytes<4>();
+    size_t m = stage_bytes<2>();
+    m = stage_bytes<4>() > m ? stage_bytes<4>() : m;
     m = stage_bytes<8>() > m ? stage_bytes<8>() : m;
     m = stage_bytes<16>() > m ? stage_bytes<16>() : m;
     m = stage_bytes<32>() > m ? stage_bytes<32>() : m;
@@ -645,7 +646,13 @@ __global__ void __launch_bounds__(BLOCK) k_node_multi(gtf_graph g, gtf_nodes n, 
         return;
     }
     b -= bk.blocks[3];
-    node_seq_body<4, OPS...>(g, n, tse, uts, e, p, w, chi2_thr, kl_thr, bk.list[4], bk.seg[4], bk.count[4], b, smem);
+    if (b < bk.blocks[4]) {
+        node_seq_body<4, OPS...>(g, n, tse, uts, e, p, w, chi2_thr, kl_thr, bk.list[4], bk.seg[4], bk.count[4], b,
+                                 smem);
+        return;
+    }
+    b -= bk.blocks[4];
+    node_seq_body<2, OPS...>(g, n, tse, uts, e, p, w, chi2_thr, kl_thr, bk.list[5], bk.seg[5], bk.count[5], b, smem);
 }
 
 // run-time op sequence (gtf_node_ops): any order of any ops

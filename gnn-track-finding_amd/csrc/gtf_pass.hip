@@ -708,10 +708,15 @@ int launch_ops(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* ut
             const int32_t* l = g->sched;
             // slot segments of the schedule entries from l on (NULL without sched_seg)
             auto seg = [&](const int32_t* at) { return g->sched_seg ? g->sched_seg + 2 * (at - g->sched) : nullptr; };
-            if (g->n_g4 > 0)
-                hipLaunchKernelGGL(k_node_group<4>, dim3((g->n_g4 + BLOCK / 4 - 1) / (BLOCK / 4)), dim3(BLOCK), 0, st,
-                                   *g, *n, T, U, *e, *p, w, ops, chi2, kl, l, seg(l), g->n_g4);
-            l += g->n_g4;
+            const int n2 = g->n_g2 > 0 && g->n_g2 <= g->n_g4 ? g->n_g2 : 0, n4 = g->n_g4 - n2;
+            if (n2 > 0)
+                hipLaunchKernelGGL(k_node_group<2>, dim3((n2 + BLOCK / 2 - 1) / (BLOCK / 2)), dim3(BLOCK), 0, st,
+                                   *g, *n, T, U, *e, *p, w, ops, chi2, kl, l, seg(l), n2);
+            l += n2;
+            if (n4 > 0)
+                hipLaunchKernelGGL(k_node_group<4>, dim3((n4 + BLOCK / 4 - 1) / (BLOCK / 4)), dim3(BLOCK), 0, st,
+                                   *g, *n, T, U, *e, *p, w, ops, chi2, kl, l, seg(l), n4);
+            l += n4;
             if (g->n_g8 > 0)
                 hipLaunchKernelGGL(k_node_group<8>, dim3((g->n_g8 + BLOCK / 8 - 1) / (BLOCK / 8)), dim3(BLOCK), 0, st,
                                    *g, *n, T, U, *e, *p, w, ops, chi2, kl, l, seg(l), g->n_g8);
@@ -749,13 +754,15 @@ int launch_seq(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* ut
     if (g->n_nodes > 0) {
         if (g->sched) {
             Buckets bk;
-            const int cnt[5] = {g->n_g64, g->n_g32, g->n_g16, g->n_g8, g->n_g4};
-            const int gs[5] = {64, 32, 16, 8, 4};
+            // the first n_g2 entries of the <= 4-slot bucket have <= 2 slots: 2 lanes each
+            const int n2 = g->n_g2 > 0 && g->n_g2 <= g->n_g4 ? g->n_g2 : 0;
+            const int cnt[6] = {g->n_g64, g->n_g32, g->n_g16, g->n_g8, g->n_g4 - n2, n2};
+            const int gs[6] = {64, 32, 16, 8, 4, 2};
             const int32_t* s8 = g->sched + g->n_g4;
-            const int32_t* starts[5] = {s8 + g->n_g8 + g->n_g16 + g->n_g32, s8 + g->n_g8 + g->n_g16, s8 + g->n_g8,
-                                        s8, g->sched};
+            const int32_t* starts[6] = {s8 + g->n_g8 + g->n_g16 + g->n_g32, s8 + g->n_g8 + g->n_g16, s8 + g->n_g8,
+                                        s8, g->sched + n2, g->sched};
             int total = 0;
-            for (int q = 0; q < 5; q++) {
+            for (int q = 0; q < 6; q++) {
                 bk.list[q] = starts[q];
                 bk.seg[q] = g->sched_seg ? g->sched_seg + 2 * (starts[q] - g->sched) : nullptr;
                 bk.count[q] = cnt[q];

@@ -109,6 +109,9 @@ class DeviceGraph:
         deg = np.diff(g.slot_ptr.astype(np.int64))
         idx = np.arange(g.n_nodes, dtype=np.int32)
         buckets = [idx[(deg >= lo) & (deg <= hi)] for lo, hi in BUCKETS]
+        # the <= 2-slot nodes first in the <= 4-slot bucket: they run on 2 lanes (gtf_graph.n_g2)
+        buckets[0] = np.concatenate([buckets[0][deg[buckets[0]] <= 2], buckets[0][deg[buckets[0]] > 2]])
+        self.n_g2 = int((deg[buckets[0]] <= 2).sum())
         rest = idx[deg > 64]
         sched = np.concatenate(buckets + [rest]).astype(np.int32)
         up("sched", sched)
@@ -167,13 +170,14 @@ class DeviceGraph:
                                p("gnn"), p("xyzr"), p("layer"),
                                p("sched") if self.use_sched else ctypes.c_void_p(0), *self.n_g[1:], p("out_dst"),
                                p("slot_layer"), self.n_g[0], p("sched_seg") if self.use_sched else ctypes.c_void_p(0),
-                               p("out_sched") if self.use_sched else ctypes.c_void_p(0), *self.n_o)
+                               p("out_sched") if self.use_sched else ctypes.c_void_p(0), *self.n_o,
+                               self.n_g2 if self.use_sched else 0)
         self.cg_sched = nat.GtfGraph(self.n_nodes, self.n_slots, self.n_edges, self.n_big, p("slot_ptr"),
                                      p("slot_src"),
                                      p("slot_dst"), p("out_ptr"), p("out_slot"), p("slot_outpos"), p("is_edge"),
                                      p("rev_edge"), p("solo"), p("gnn"), p("xyzr"), p("layer"), p("sched"),
                                      *self.n_g_all[1:], p("out_dst"), p("slot_layer"), self.n_g_all[0],
-                                     p("sched_seg"), p("out_sched"), *self.n_o)
+                                     p("sched_seg"), p("out_sched"), *self.n_o, self.n_g2)
         self.cn = nat.GtfNodes(*[p(f) for f in MUTABLE_NODE])
         self.cuts = nat.GtfStates(p("uts_rank"), p("uts_sv"), p("uts_tau"), p("uts_cov"), p("uts_xyzr"),
                                   p("uts_lik"), p("uts_mw"), p("uts_prior"), p("uts_lr"), p("uts_side"),

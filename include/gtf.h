@@ -81,6 +81,8 @@ typedef struct gtf_graph {
     int32_t n_o4;
     int32_t n_o8;
     int32_t n_o16;
+    int32_t n_g2;             /* the first n_g2 entries of the n_g4 bucket have <= 2 slots and run on
+                                 2 lanes per node in gtf_pass / the node ops (0 = all on 4 lanes) */
 } gtf_graph;
 
 /* ---- per-node mutable state ------------------------------------------------ */

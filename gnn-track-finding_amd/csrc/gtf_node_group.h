@@ -519,6 +519,10 @@ template <int G>
 __device__ __forceinline__ void node_store(NodeCtx<G>& c, gtf_nodes& n, gtf_states& tse, gtf_states& uts,
                                            gtf_edges& e) {
     const int k = c.k;
+#if GTF_ABLATE == 6
+    if (c.valid && c.act != c.act0) e.act[k] = c.act;   // diagnostics build: the activation store only
+    return;
+#endif
     if (c.valid) {
         if (c.act != c.act0) e.act[k] = c.act;
         if (c.edge_mw_dirty) e.edge_mw[k] = c.edge_mw;

@@ -798,8 +798,21 @@ int run_pass(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts,
     if (events) (void)hipEventRecord((hipEvent_t)events[3], st);
     rc = launch_seq<CLUSTER_UTS_OPS>(g, n, tse, uts, e, p, w, p->cluster_chi2, p->cluster_kl, st);
 #else
+#ifndef GTF_SEQ_VARIANT
+#define GTF_SEQ_VARIANT 0  // diagnostics builds: 1..4 = a prefix of the op sequence only
+#endif
+#if GTF_SEQ_VARIANT == 1
+    rc = launch_seq<OP_RANKS, OP_PRIORS_UTS>(g, n, tse, uts, e, p, w, 0.0, 0.0, st);
+#elif GTF_SEQ_VARIANT == 2
+    rc = launch_seq<OP_RANKS, OP_PRIORS_UTS, OP_REWEIGHT_UTS>(g, n, tse, uts, e, p, w, 0.0, 0.0, st);
+#elif GTF_SEQ_VARIANT == 3
+    rc = launch_seq<EXTRAP_OPS>(g, n, tse, uts, e, p, w, 0.0, 0.0, st);
+#elif GTF_SEQ_VARIANT == 4
+    rc = launch_seq<EXTRAP_OPS, UPDATE_OPS>(g, n, tse, uts, e, p, w, 0.0, 0.0, st);
+#else
     rc = launch_seq<EXTRAP_OPS, UPDATE_OPS, CLUSTER_UTS_OPS>(g, n, tse, uts, e, p, w, p->cluster_chi2,
                                                              p->cluster_kl, st);
+#endif
     if (events) (void)hipEventRecord((hipEvent_t)events[3], st);
 #endif
     if (events) (void)hipEventRecord((hipEvent_t)events[4], st);

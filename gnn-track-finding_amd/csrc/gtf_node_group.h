@@ -57,6 +57,43 @@ struct Grp {
         for (int o = G / 2; o > 0; o >>= 1) x |= __shfl_xor(x, o, G);
         return x;
     }
+    __device__ __forceinline__ int size() const { return G; }
+    __device__ __forceinline__ int stage_base() const { return 0; }  // one stage struct per group
+};
+
+// G = 0: variable-size lane segments packed back to back in a wavefront (gtf_graph.pack_ent):
+// the group is lanes [gbase, gbase + gsize) of the wave. Reductions are segmented
+// shuffle-down steps (wmax = the wave's largest segment, wave-uniform) followed by a
+// broadcast from the segment's first lane; the clustering stage is one per wavefront,
+// the group's states at [gbase + i].
+template <>
+struct Grp<0> {
+    int gl, gbase, gsize, wmax;
+    unsigned long long lowmask;
+    __device__ __forceinline__ Grp() {}
+    __device__ __forceinline__ unsigned long long bits(bool pred) const { return (__ballot(pred) >> gbase) & lowmask; }
+    __device__ __forceinline__ int count(bool pred) const { return __popcll(bits(pred)); }
+    __device__ __forceinline__ bool any(bool pred) const { return bits(pred) != 0ull; }
+    template <typename T>
+    __device__ __forceinline__ T shfl(T x, int src) const { return __shfl(x, gbase + src); }
+    template <typename T, typename Op>
+    __device__ __forceinline__ T reduce(T x, Op op) const {
+        for (int o = 1; o < wmax; o <<= 1) {
+            const T y = __shfl_down(x, o);
+            if (gl + o < gsize) x = op(x, y);
+        }
+        return __shfl(x, gbase);
+    }
+    __device__ __forceinline__ int max_i(int x) const { return reduce(x, [](int a, int b) { return max(a, b); }); }
+    __device__ __forceinline__ int min_i(int x) const { return reduce(x, [](int a, int b) { return min(a, b); }); }
+    __device__ __forceinline__ double min_d(double x) const {  // NaN-free inputs
+        return reduce(x, [](double a, double b) { return fmin(a, b); });
+    }
+    __device__ __forceinline__ unsigned or_u(unsigned x) const {
+        return reduce(x, [](unsigned a, unsigned b) { return a | b; });
+    }
+    __device__ __forceinline__ int size() const { return gsize; }
+    __device__ __forceinline__ int stage_base() const { return gbase; }
 };
 
 // per-lane (per-slot) registers of one state dict
@@ -112,7 +149,7 @@ __device__ __forceinline__ int dict_pos(const NodeCtx<G>& c, LaneDict& st) {
         pos = __popcll(below);
     } else {
         pos = 0;
-        for (int j = 0; j < G; j++) {
+        for (int j = 0; j < c.grp.size(); j++) {
             const int rj = c.grp.shfl(st.rank, j);
             pos += (rj >= 0 && rj < st.rank) ? 1 : 0;
         }
@@ -330,25 +367,26 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
     const int d = c.grp.count(pres);
     if (d <= 2 || d >= 16) return;                                                 // :207
     const int pos = dict_pos(c, st);
+    const int sb = c.grp.stage_base();   // this group's first entry in the stage arrays
     const double xa = xyzr_node[0], za = xyzr_node[2], ra = xyzr_node[3];
     if (pres) {
         const int64_t k = c.k;
-        stg->a[pos] = S.sv[3 * k];
-        stg->b[pos] = S.sv[3 * k + 1];
-        stg->c[pos] = S.sv[3 * k + 2];
-        stg->tau[pos] = S.tau[k];
+        stg->a[sb + pos] = S.sv[3 * k];
+        stg->b[sb + pos] = S.sv[3 * k + 1];
+        stg->c[sb + pos] = S.sv[3 * k + 2];
+        stg->tau[sb + pos] = S.tau[k];
         const double* cv = S.cov + 5 * k;
         const Cov5 C{cv[0], cv[1], cv[2], cv[3], cv[4]};
         const Cov5 I = inv_cov5(C);
-        stg->c00[pos] = C.c00; stg->c01[pos] = C.c01; stg->c10[pos] = C.c10; stg->c11[pos] = C.c11;
-        stg->c22[pos] = C.c22;
-        stg->i00[pos] = I.c00; stg->i01[pos] = I.c01; stg->i10[pos] = I.c10; stg->i11[pos] = I.c11;
-        stg->i22[pos] = I.c22;
+        stg->c00[sb + pos] = C.c00; stg->c01[sb + pos] = C.c01; stg->c10[sb + pos] = C.c10; stg->c11[sb + pos] = C.c11;
+        stg->c22[sb + pos] = C.c22;
+        stg->i00[sb + pos] = I.c00; stg->i01[sb + pos] = I.c01; stg->i10[sb + pos] = I.c10; stg->i11[sb + pos] = I.c11;
+        stg->i22[sb + pos] = I.c22;
         const TauGeo t = tau_geo(S.xyzr[4 * k], S.xyzr[4 * k + 2], S.xyzr[4 * k + 3], za, ra, p.sigma0rz2, p.sigma0rz,
                                  p.sigma0rz, p.sigma0rz2, p.endcap_boundary);
-        stg->q[pos] = t.q; stg->w[pos] = t.w; stg->tg[pos] = t.tau;
-        stg->ec[pos] = fabs(S.xyzr[4 * k]) >= p.endcap_boundary;
-        stg->prior[pos] = st.prior;
+        stg->q[sb + pos] = t.q; stg->w[sb + pos] = t.w; stg->tg[sb + pos] = t.tau;
+        stg->ec[sb + pos] = fabs(S.xyzr[4 * k]) >= p.endcap_boundary;
+        stg->prior[sb + pos] = st.prior;
     }
     wave_lds_sync();
     const double szb2 = p.sigma0rz2 * p.sigma0rz2, srb2 = p.sigma0rz * p.sigma0rz;   // barrel sigma_z^2, sigma_r^2
@@ -360,12 +398,12 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
     int lt0 = 1 << 20, lt1 = 1 << 20;
     unsigned lmask = 0;
     bool lnan = false, lnz = false;
-    for (int t = c.grp.gl; t < npairs; t += G) {
+    for (int t = c.grp.gl; t < npairs; t += c.grp.size()) {
         int i, j;
         pair_ij(t, i, j);
-        const double D = mahalanobis_geo(stg->a[i], stg->b[i], stage_cov(stg, i), stg->a[j], stg->b[j],
-                                         stage_cov(stg, j), sza2, sra2, stage_geo(stg, i, szb2, srb2),
-                                         stage_geo(stg, j, szb2, srb2));
+        const double D = mahalanobis_geo(stg->a[sb + i], stg->b[sb + i], stage_cov(stg, sb + i), stg->a[sb + j], stg->b[sb + j],
+                                         stage_cov(stg, sb + j), sza2, sra2, stage_geo(stg, sb + i, szb2, srb2),
+                                         stage_geo(stg, sb + j, szb2, srb2));
         if (D == 0.0) continue;  // zeros are excluded (np.nonzero)
         lnz = true;
         if (D != D) { lnan = true; continue; }
@@ -398,16 +436,16 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
     double pm[3], jm[3];
     Cov5 mc;
     {
-        const Cov5 i0 = stage_inv(stg, p0), i1 = stage_inv(stg, p1);
+        const Cov5 i0 = stage_inv(stg, sb + p0), i1 = stage_inv(stg, sb + p1);
         mc = inv_cov5(add_cov5(i0, i1));
-        const double ps0[3] = {stg->a[p0], stg->b[p0], stg->c[p0]};
-        const double ps1[3] = {stg->a[p1], stg->b[p1], stg->c[p1]};
-        const double js0[3] = {ps0[0], ps0[1], stg->tau[p0]};
-        const double js1[3] = {ps1[0], ps1[1], stg->tau[p1]};
+        const double ps0[3] = {stg->a[sb + p0], stg->b[sb + p0], stg->c[sb + p0]};
+        const double ps1[3] = {stg->a[sb + p1], stg->b[sb + p1], stg->c[sb + p1]};
+        const double js0[3] = {ps0[0], ps0[1], stg->tau[sb + p0]};
+        const double js1[3] = {ps1[0], ps1[1], stg->tau[sb + p1]};
         merge_with_inv(ps0, i0, ps1, i1, mc, pm);
         merge_with_inv(js0, i0, js1, i1, mc, jm);
     }
-    double mprior = stg->prior[p0] + stg->prior[p1];
+    double mprior = stg->prior[sb + p0] + stg->prior[sb + p1];
     unsigned alive = ((1u << d) - 1u) & ~tiemask;
     if (alive == 0) {
         if (c.grp.gl == 0) atomicOr(err, (uint32_t)GTF_ERR_TIE_EMPTIED);
@@ -418,8 +456,8 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
             double D = INFINITY;
             bool dn = false;
             if (me) {
-                const double js_me[3] = {stg->a[pos], stg->b[pos], stg->tau[pos]};
-                D = kl_with_inv(js_me, stage_cov(stg, pos), stage_inv(stg, pos), jm, mc, im);
+                const double js_me[3] = {stg->a[sb + pos], stg->b[sb + pos], stg->tau[sb + pos]};
+                D = kl_with_inv(js_me, stage_cov(stg, sb + pos), stage_inv(stg, sb + pos), jm, mc, im);
                 if (D != D) { dn = true; D = INFINITY; }
             }
             if (c.grp.any(dn)) {
@@ -429,17 +467,17 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
             const double mind = c.grp.min_d(D);
             if (!(mind < kl_thr)) break;
             const int m = c.grp.min_i((me && D == mind) ? pos : 99);  // first minimum (list.index)
-            const Cov5 ii = stage_inv(stg, m);
+            const Cov5 ii = stage_inv(stg, sb + m);
             const Cov5 nmc = inv_cov5(add_cov5(ii, im));
-            const double ps[3] = {stg->a[m], stg->b[m], stg->c[m]};
-            const double js[3] = {ps[0], ps[1], stg->tau[m]};
+            const double ps[3] = {stg->a[sb + m], stg->b[sb + m], stg->c[sb + m]};
+            const double js[3] = {ps[0], ps[1], stg->tau[sb + m]};
             double npm[3], njm[3];
             merge_with_inv(ps, ii, pm, im, nmc, npm);
             merge_with_inv(js, ii, jm, im, nmc, njm);
             pm[0] = npm[0]; pm[1] = npm[1]; pm[2] = npm[2];
             jm[0] = njm[0]; jm[1] = njm[1]; jm[2] = njm[2];
             mc = nmc;
-            mprior = stg->prior[m] + mprior;
+            mprior = stg->prior[sb + m] + mprior;
             alive &= ~(1u << m);
             if (alive == 0) break;
         }
@@ -465,6 +503,10 @@ struct Need {
 };
 
 template <int G>
+__device__ __forceinline__ bool node_fields(NodeCtx<G>& c, const gtf_graph& g, const gtf_states& tse,
+                                            const gtf_states& uts, const gtf_edges& e, const Need& nd);
+
+template <int G>
 __device__ __forceinline__ bool node_load(NodeCtx<G>& c, const gtf_graph& g, const gtf_nodes& n,
                                           const gtf_states& tse, const gtf_states& uts, const gtf_edges& e,
                                           const int32_t* list, const int32_t* seg, int count, int gi,
@@ -479,6 +521,13 @@ __device__ __forceinline__ bool node_load(NodeCtx<G>& c, const gtf_graph& g, con
         c.lo = g.slot_ptr[c.v];
         c.d = g.slot_ptr[c.v + 1] - c.lo;
     }
+    return node_fields(c, g, tse, uts, e, nd);
+}
+
+// the per-slot fields of the lane's slot (c.v, c.lo, c.d and the group set)
+template <int G>
+__device__ __forceinline__ bool node_fields(NodeCtx<G>& c, const gtf_graph& g, const gtf_states& tse,
+                                            const gtf_states& uts, const gtf_edges& e, const Need& nd) {
     c.k = c.lo + c.grp.gl;
     c.valid = c.grp.gl < c.d;
     const int k = c.k;
@@ -657,6 +706,52 @@ __global__ void __launch_bounds__(BLOCK) k_node_multi(gtf_graph g, gtf_nodes n, 
     }
     b -= bk.blocks[4];
     node_seq_body<2, OPS...>(g, n, tse, uts, e, p, w, chi2_thr, kl_thr, bk.list[5], bk.seg[5], bk.count[5], b, smem);
+}
+
+// Packed lane segments (gtf_graph.pack_ent / pack_wave): wavefront wv takes the entries
+// [pack_wave[wv], pack_wave[wv + 1]), each (v, slot_ptr[v], slot_ptr[v+1], first lane),
+// one lane per slot (one for a slot-free node) back to back, so 90+ % of the lanes hold a
+// slot instead of the 59-88 % of power-of-two groups. Same op code as the groups (G = 0).
+template <int... OPS>
+__global__ void __launch_bounds__(BLOCK) k_node_pack(gtf_graph g, gtf_nodes n, gtf_states tse, gtf_states uts,
+                                                     gtf_edges e, gtf_params p, Ws w, double chi2_thr, double kl_thr) {
+    using Q = OpSeq<OPS...>;
+    using Stage = StageT<64>;   // one per wavefront, a group's states at [gbase + i]
+    __shared__ __attribute__((aligned(16))) char smem[BLOCK * sizeof(double) +
+                                                      (Q::cluster ? (BLOCK / 64) * sizeof(Stage) : 0)];
+    __shared__ uint8_t s_start[BLOCK];
+    const int wv = blockIdx.x * (BLOCK / 64) + (int)threadIdx.x / 64;
+    if (wv >= g.n_pack_waves) return;  // wavefront-uniform
+    const int lane = threadIdx.x & 63;
+    const int e0 = g.pack_wave[wv], ne = g.pack_wave[wv + 1] - e0;
+    int4 en = make_int4(0, 0, 0, 0);
+    if (lane < ne) en = reinterpret_cast<const int4*>(g.pack_ent)[e0 + lane];
+    uint8_t* st = s_start + (threadIdx.x & ~63);
+    st[lane] = 0;
+    wave_lds_sync();
+    if (lane < ne) st[en.w] = 1;
+    wave_lds_sync();
+    const unsigned long long M = __ballot(st[lane] != 0);
+    const int idx = __popcll(lane == 63 ? M : (M & ((2ull << lane) - 1ull))) - 1;  // my entry
+    NodeCtx<0> c;
+    c.v = __shfl(en.x, idx);
+    c.lo = __shfl(en.y, idx);
+    c.d = __shfl(en.z, idx) - c.lo;
+    c.grp.gbase = __shfl(en.w, idx);
+    c.grp.gsize = c.d > 0 ? c.d : 1;
+    c.grp.gl = lane - c.grp.gbase;
+    c.grp.lowmask = c.grp.gsize >= 64 ? ~0ull : ((1ull << c.grp.gsize) - 1ull);
+    int mx = c.grp.gsize;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
+    c.grp.wmax = mx;
+    if (c.grp.gl >= c.grp.gsize) return;  // past the last segment
+    if (!node_fields(c, g, tse, uts, e, Q::need)) return;
+    double* sval = (double*)smem + (threadIdx.x & ~63);
+    Stage* stg = (Stage*)(smem + BLOCK * sizeof(double)) + (Q::cluster ? (int)threadIdx.x / 64 : 0);
+    const bool has_tse = n.has_tse[c.v], has_uts = n.has_uts[c.v];
+    (node_op<0, OPS, Stage>(c, g, n, tse, uts, p, w, sval, stg, chi2_thr, kl_thr, has_tse, has_uts), ...);
+    node_store(c, n, tse, uts, e);
 }
 
 // run-time op sequence (gtf_node_ops): any order of any ops

@@ -769,7 +769,10 @@ int launch_seq(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* ut
                 bk.blocks[q] = (cnt[q] + BLOCK / gs[q] - 1) / (BLOCK / gs[q]);
                 total += bk.blocks[q];
             }
-            if (total > 0)
+            if (g->pack_ent && g->pack_wave && g->n_pack_waves > 0)   // every <= 64-slot node, packed
+                hipLaunchKernelGGL((k_node_pack<OPS...>), dim3((g->n_pack_waves + BLOCK / 64 - 1) / (BLOCK / 64)),
+                                   dim3(BLOCK), 0, st, *g, *n, T, U, *e, *p, w, chi2, kl);
+            else if (total > 0)
                 hipLaunchKernelGGL((k_node_multi<OPS...>), dim3(total), dim3(BLOCK), 0, st, *g, *n, T, U, *e, *p, w,
                                    chi2, kl, bk);
         }

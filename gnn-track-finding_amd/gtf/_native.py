@@ -22,7 +22,8 @@ class GtfGraph(ctypes.Structure):
                 ("is_edge", P), ("rev_edge", P), ("solo", P), ("gnn", P), ("xyzr", P), ("layer", P),
                 ("sched", P), ("n_g8", I32), ("n_g16", I32), ("n_g32", I32), ("n_g64", I32), ("out_dst", P),
                 ("slot_layer", P), ("n_g4", I32), ("sched_seg", P),
-                ("out_sched", P), ("n_o4", I32), ("n_o8", I32), ("n_o16", I32), ("n_g2", I32)]
+                ("out_sched", P), ("n_o4", I32), ("n_o8", I32), ("n_o16", I32), ("n_g2", I32),
+                ("pack_ent", P), ("pack_wave", P), ("n_pack_waves", I32)]
 
 
 class GtfNodes(ctypes.Structure):

@@ -47,6 +47,30 @@ def sender_schedule(out_ptr):
     return q, [int(x.size) for x in parts]
 
 
+def pack_schedule(slot_ptr):
+    """gtf_graph.pack_ent / pack_wave: the nodes with <= 64 slots, largest first, packed
+    greedily into wavefronts of 64 lanes (one lane per slot, one for a slot-free node);
+    returns (entries [4*n] int32 (v, lo, hi, first lane), wave_ptr [W+1] int32)"""
+    sp = np.asarray(slot_ptr, dtype=np.int64)
+    deg = np.diff(sp)
+    idx = np.nonzero(deg <= 64)[0]
+    order = idx[np.argsort(-deg[idx], kind="stable")]
+    size = np.maximum(deg[order], 1)
+    off = np.empty(order.size, np.int64)
+    starts = [0]
+    used = 0
+    for i, z in enumerate(size.tolist()):
+        if used + z > 64:
+            starts.append(i)
+            used = 0
+        off[i] = used
+        used += z
+    starts.append(order.size)
+    ent = np.stack([order, sp[order], sp[order + 1], off], axis=1).astype(np.int32).reshape(-1)
+    wave = np.asarray(starts if order.size else [0], dtype=np.int32)
+    return ent, wave
+
+
 def _torch():
     import torch
     if not torch.cuda.is_available():
@@ -63,13 +87,17 @@ def schedule_order(slot_ptr):
 
 
 class DeviceGraph:
-    """layout "natural": the host graph's node and slot order. layout "schedule": nodes
+    """pack: the fused pass's node kernel on packed variable-size lane segments
+    (gtf_graph.pack_ent) instead of power-of-two lane groups -- same results, same speed
+    on C4, kept as an option.
+    layout "natural": the host graph's node and slot order. layout "schedule": nodes
     renumbered into schedule order (graph.renumber), so the lane groups of one
     wavefront take adjacent slot segments and every slot load of the node kernel is
     one contiguous run; download() maps the results back to the host order. The
     stage methods are layout-independent (the pass is equivariant under renumber)."""
 
-    def __init__(self, g: TrackGraph, device: str = "cuda", schedule: bool = True, layout: str = "natural"):
+    def __init__(self, g: TrackGraph, device: str = "cuda", schedule: bool = True, layout: str = "natural",
+                 pack: bool = False):
         torch = _torch()
         self.layout = layout
         self.order = self.slot_perm = None
@@ -118,6 +146,10 @@ class DeviceGraph:
         up("sched_seg", sched_segments(g.slot_ptr, sched))
         osched, self.n_o = sender_schedule(g.out_ptr)
         up("out_sched", osched)
+        pent, pwave = pack_schedule(g.slot_ptr)
+        up("pack_ent", pent)
+        up("pack_wave", pwave)
+        self.n_pack_waves = int(pwave.size - 1)
         self.n_g_all = [int(b.size) for b in buckets]
         self.n_big = int(rest.size)
         self.n_g = self.n_g_all if schedule else [0] * len(BUCKETS)
@@ -131,7 +163,7 @@ class DeviceGraph:
         self._make_arena(self.PASS_INPUTS)
         ws_bytes = int(self.lib.gtf_workspace_bytes(g.n_nodes, g.n_slots))
         self.t["ws"] = torch.zeros(ws_bytes, dtype=torch.uint8, device=self.device)
-        self._build_structs()
+        self._build_structs(pack)
 
     # ---------------------------------------------------------------- memory
     def _make_arena(self, names):
@@ -162,7 +194,7 @@ class DeviceGraph:
         t = self.t[name]
         return ctypes.c_void_p(t.data_ptr() if t.numel() else 0)
 
-    def _build_structs(self):
+    def _build_structs(self, pack=True):
         p = self.ptr
         self.cg = nat.GtfGraph(self.n_nodes, self.n_slots, self.n_edges, self.n_big if self.use_sched else 0,
                                p("slot_ptr"), p("slot_src"),
@@ -171,7 +203,9 @@ class DeviceGraph:
                                p("sched") if self.use_sched else ctypes.c_void_p(0), *self.n_g[1:], p("out_dst"),
                                p("slot_layer"), self.n_g[0], p("sched_seg") if self.use_sched else ctypes.c_void_p(0),
                                p("out_sched") if self.use_sched else ctypes.c_void_p(0), *self.n_o,
-                               self.n_g2 if self.use_sched else 0)
+                               self.n_g2 if self.use_sched else 0,
+                               *((p("pack_ent"), p("pack_wave"), self.n_pack_waves) if self.use_sched and pack
+                                 else (ctypes.c_void_p(0), ctypes.c_void_p(0), 0)))
         self.cg_sched = nat.GtfGraph(self.n_nodes, self.n_slots, self.n_edges, self.n_big, p("slot_ptr"),
                                      p("slot_src"),
                                      p("slot_dst"), p("out_ptr"), p("out_slot"), p("slot_outpos"), p("is_edge"),

@@ -83,6 +83,13 @@ typedef struct gtf_graph {
     int32_t n_o16;
     int32_t n_g2;             /* the first n_g2 entries of the n_g4 bucket have <= 2 slots and run on
                                  2 lanes per node in gtf_pass / the node ops (0 = all on 4 lanes) */
+    /* optional packed schedule for gtf_pass's node kernel (replaces the lane-group buckets
+     * there; the > 64-slot nodes still come from sched): wavefront w takes the entries
+     * [pack_wave[w], pack_wave[w+1]) of pack_ent, each (v, slot_ptr[v], slot_ptr[v+1], first
+     * lane) as int32 quadruples, one lane per slot (one for a slot-free node), <= 64 lanes. */
+    const int32_t* pack_ent;  /* [4*n_entries] */
+    const int32_t* pack_wave; /* [n_pack_waves+1] */
+    int32_t n_pack_waves;
 } gtf_graph;
 
 /* ---- per-node mutable state ------------------------------------------------ */

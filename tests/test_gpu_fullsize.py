@@ -7,9 +7,10 @@ to the same results by construction:
   * the fused pass (gtf_pass: one node launch for every node-local op) equals the
     three stage entry points run one after the other (gtf_extrapolate -> gtf_update
     -> gtf_cluster, one launch per stage), bit for bit;
-  * both equal the run-time op interpreter (gtf_node_ops, k_node_group) and the
-    thread-per-node implementation (no schedule, k_node), which restate the same
-    reference functions with different code;
+  * both equal the run-time op interpreter (gtf_node_ops, k_node_group), the
+    thread-per-node implementation (no schedule, k_node), the packed variable-size lane
+    segments (k_node_pack) and the pass on nodes renumbered into schedule order, which
+    restate the same reference functions with different code or data order;
   * a pass is deterministic (two runs from the same input, bit-identical);
   * activations only switch off (reweight and clustering never re-activate an edge).
 """
@@ -50,8 +51,8 @@ def _same(a, b, what):
 
 def _run(g, how, p):
     from gtf.device import DeviceGraph
-    if how == "schedule_layout":   # nodes renumbered into schedule order, results mapped back
-        d = DeviceGraph(g, layout="schedule")
+    if how in ("schedule_layout", "packed"):   # renumbered nodes (results mapped back) / packed segments
+        d = DeviceGraph(g, layout="schedule") if how == "schedule_layout" else DeviceGraph(g, pack=True)
         d.clear_errors()
         d.full_pass(p)
         got = d.download(g.copy())
@@ -78,7 +79,7 @@ def test_fused_pass_equals_stagewise_and_other_implementations(c4):
     p = Params()
     ref, ref_flags = _run(c4, "fused", p)
     assert ref["act"].sum() > 0 and ref["has_merged"].sum() > 0
-    for how in ("stages", "interpreter", "thread_per_node", "schedule_layout"):
+    for how in ("stages", "interpreter", "thread_per_node", "schedule_layout", "packed"):
         got, flags = _run(c4, how, p)
         assert flags == ref_flags, how
         _same(got, ref, how)

@@ -56,3 +56,21 @@ def test_schedule_arrays():
     assert np.array_equal(q[:, 1], g.out_ptr[u]) and np.array_equal(q[:, 2], g.out_ptr[u + 1])
     b = np.repeat([0, 1, 2], counts)
     assert np.all(od[u][b == 0] <= 4) and np.all((od[u][b == 1] >= 5) & (od[u][b == 1] <= 8)) and np.all(od[u][b == 2] > 8)
+
+
+def test_pack_schedule():
+    """gtf_graph.pack_ent / pack_wave: every <= 64-slot node once, segments back to back,
+    no wavefront over 64 lanes"""
+    from gtf.device import pack_schedule
+    g = synth.event(seed=8, n_tracks=300, fake_mean=synth.C4_FAKE)
+    ent, wave = pack_schedule(g.slot_ptr)
+    ent = ent.reshape(-1, 4)
+    deg = np.diff(g.slot_ptr)
+    assert np.array_equal(np.sort(ent[:, 0]), np.nonzero(deg <= 64)[0])
+    assert np.array_equal(ent[:, 1], g.slot_ptr[ent[:, 0]]) and np.array_equal(ent[:, 2], g.slot_ptr[ent[:, 0] + 1])
+    size = np.maximum(ent[:, 2] - ent[:, 1], 1)
+    for w in range(wave.size - 1):
+        a, b = wave[w], wave[w + 1]
+        assert a < b and ent[a, 3] == 0
+        assert np.array_equal(ent[a + 1:b, 3], np.cumsum(size[a:b])[:-1])
+        assert ent[b - 1, 3] + size[b - 1] <= 64

@@ -122,7 +122,7 @@ struct NodeCtx {
     unsigned long long same_x;      // lanes whose stored UTS x equals this lane's (lazy; NaN: itself)
     bool same_x_ok;
     LaneDict tse, uts;
-    double lik, lr, x0, edge_mw;
+    double lik, lr, x0, edge_mw, smw;
     int8_t side;
     uint8_t fresh;
     bool uts_dirty_lr, edge_mw_dirty;
@@ -302,6 +302,22 @@ __device__ __forceinline__ void g_mixture_weights(NodeCtx<G>& c, LaneDict& st, b
     if (c.valid && st.rank >= 0) {
         st.mw = 1.0 / (double)cnt;
         st.dirty |= D_MW;
+    }
+}
+
+// the entries the last message passing (re)wrote carry the sender's TSE mixture weight
+// (extrapolate_merged_states.py:384) and no prior, lr or side yet (a fresh dict entry
+// the priors / side norm have not reached); set here with the node's other slot stores
+// instead of by k_extrapolate
+template <int G>
+__device__ __forceinline__ void g_fresh(NodeCtx<G>& c) {
+    if (c.valid && c.fresh) {
+        c.uts.mw = c.smw;
+        c.uts.prior = NAN;
+        c.uts.dirty |= D_MW | D_PRIOR;
+        c.lr = NAN;
+        c.side = -1;
+        c.uts_dirty_lr = true;
     }
 }
 
@@ -499,7 +515,7 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
 // ---------------------------------------------------------------------------
 // the per-slot fields an op sequence reads from memory (the others it only writes)
 struct Need {
-    bool tse_rank, tse_prior, uts_rank, uts_mw, uts_prior, uts_lik, uts_x0, uts_fresh;
+    bool tse_rank, tse_prior, uts_rank, uts_mw, uts_prior, uts_lik, uts_x0, uts_fresh, send_mw;
 };
 
 template <int G>
@@ -560,6 +576,7 @@ __device__ __forceinline__ bool node_fields(NodeCtx<G>& c, const gtf_graph& g, c
         if (nd.uts_lik) c.lik = uts.lik[k];
         if (nd.uts_x0) c.x0 = uts.xyzr[4 * (int64_t)k];
         if (nd.uts_fresh) c.fresh = uts.fresh[k];
+        if (nd.send_mw) c.smw = e.send_mw[k];
     }
     return true;
 }
@@ -591,6 +608,7 @@ __device__ __forceinline__ void node_op(NodeCtx<G>& c, const gtf_graph& g, gtf_n
                                         gtf_states& uts, const gtf_params& p, const Ws& w, double* sval,
                                         Stage* stg, double chi2_thr, double kl_thr, bool has_tse,
                                         bool has_uts) {
+    if constexpr (OP == OP_FRESH) g_fresh(c);
     if constexpr (OP == OP_RANKS) g_ranks(c);
     if constexpr (OP == OP_PRIORS_TSE) { if (has_tse) g_priors(c, c.tse); }
     if constexpr (OP == OP_PRIORS_UTS) { if (has_uts) g_priors(c, c.uts); }
@@ -611,13 +629,14 @@ template <int... OPS>
 struct OpSeq {
     static constexpr bool uses_tse =
         ((OPS == OP_PRIORS_TSE || OPS == OP_MW_TSE || OPS == OP_CLUSTER_TSE || OPS == OP_PRUNE) || ...);
-    static constexpr bool uses_uts = ((OPS == OP_RANKS || OPS == OP_PRIORS_UTS || OPS == OP_REWEIGHT_UTS ||
+    static constexpr bool uses_uts = ((OPS == OP_FRESH || OPS == OP_RANKS || OPS == OP_PRIORS_UTS || OPS == OP_REWEIGHT_UTS ||
                                        OPS == OP_MW_UTS || OPS == OP_CLUSTER_UTS || OPS == OP_PRUNE) || ...);
     static constexpr bool cluster = ((OPS == OP_CLUSTER_TSE || OPS == OP_CLUSTER_UTS) || ...);
     static constexpr bool reweight = ((OPS == OP_REWEIGHT_UTS) || ...);
+    static constexpr bool fresh = ((OPS == OP_FRESH) || ...);
     static constexpr Need need{uses_tse, ((OPS == OP_CLUSTER_TSE) || ...), uses_uts, reweight,
                                reweight || ((OPS == OP_CLUSTER_UTS) || ...), reweight, reweight,
-                               ((OPS == OP_RANKS) || ...)};
+                               ((OPS == OP_RANKS) || ...) || fresh, fresh};
 };
 
 // compile-time op sequence for one group size: dead ops are compiled out.
@@ -766,7 +785,8 @@ __global__ void __launch_bounds__(BLOCK) k_node_group(gtf_graph g, gtf_nodes n, 
     NodeCtx<G> c;
     const int gi = (blockIdx.x * BLOCK + (int)threadIdx.x) / G;
     const Need nd{(bool)ops.uses_tse, (bool)ops.uses_tse, (bool)ops.uses_uts, (bool)ops.uses_uts,
-                  (bool)ops.uses_uts, (bool)ops.uses_uts, (bool)ops.uses_uts, (bool)ops.uses_uts};
+                  (bool)ops.uses_uts, (bool)ops.uses_uts, (bool)ops.uses_uts, (bool)ops.uses_uts,
+                  (bool)ops.uses_uts};
     if (!node_load(c, g, n, tse, uts, e, list, seg, count, gi, nd)) return;
     double* sval = s_val + (threadIdx.x & ~63);
     Stage* stg = s_stage + (int)threadIdx.x / G;
@@ -775,6 +795,7 @@ __global__ void __launch_bounds__(BLOCK) k_node_group(gtf_graph g, gtf_nodes n, 
         switch (ops.op[i]) {
 #define GTF_CASE(OPC) \
     case OPC: node_op<G, OPC, Stage>(c, g, n, tse, uts, p, w, sval, stg, chi2_thr, kl_thr, has_tse, has_uts); break;
+            GTF_CASE(OP_FRESH)
             GTF_CASE(OP_RANKS)
             GTF_CASE(OP_PRIORS_TSE)
             GTF_CASE(OP_PRIORS_UTS)

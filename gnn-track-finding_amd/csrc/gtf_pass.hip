@@ -287,10 +287,8 @@ __global__ void __launch_bounds__(BLOCK) k_extrapolate(gtf_graph g, gtf_nodes n,
     double* sx = uts.xyzr + 4 * (int64_t)k;
     sx[0] = node_x; sx[1] = node_y; sx[2] = node_z; sx[3] = node_r;
     uts.lik[k] = lik;
-    uts.mw[k] = smw;                                                               // :384
-    uts.prior[k] = NAN;
-    uts.lr[k] = NAN;
-    uts.side[k] = -1;
+    // mixture_weight = smw (:384) and the empty prior / lr / side of a fresh entry are set
+    // by the node kernel's OP_FRESH, merged with its own stores of those fields
     uts.fresh[k] = 1;
     n.has_uts[v] = 1;  // benign same-value race between the receiver's accepted slots
 }
@@ -298,7 +296,7 @@ __global__ void __launch_bounds__(BLOCK) k_extrapolate(gtf_graph g, gtf_nodes n,
 // ---------------------------------------------------------------------------
 // node-local stages (1 thread per receiver node)
 // ---------------------------------------------------------------------------
-#define EXTRAP_OPS OP_RANKS, OP_PRIORS_UTS, OP_REWEIGHT_UTS, OP_PRIORS_UTS, OP_REWEIGHT_UTS, OP_DEGREE
+#define EXTRAP_OPS OP_FRESH, OP_RANKS, OP_PRIORS_UTS, OP_REWEIGHT_UTS, OP_PRIORS_UTS, OP_REWEIGHT_UTS, OP_DEGREE
 #define UPDATE_OPS OP_PRUNE, OP_PRIORS_TSE, OP_PRIORS_UTS, OP_REWEIGHT_UTS
 #define CLUSTER_UTS_OPS OP_CLUSTER_UTS, OP_DEGREE, OP_MW_UTS, OP_PRIORS_UTS
 #ifndef GTF_SPLIT_NODE
@@ -422,6 +420,17 @@ __device__ void node_mixture_weights(const gtf_graph& g, gtf_states& st, Seg s, 
     const double mw = 1.0 / (double)cnt;
     for (int k = s.lo; k < s.hi; k++)
         if (st.rank[k] >= 0) st.mw[k] = mw;
+}
+
+// the fields of the entries message passing (re)wrote (g_fresh, thread-per-node form)
+__device__ void node_fresh(gtf_states& uts, const gtf_edges& e, Seg s) {
+    for (int k = s.lo; k < s.hi; k++)
+        if (uts.fresh[k]) {
+            uts.mw[k] = e.send_mw[k];
+            uts.prior[k] = NAN;
+            uts.lr[k] = NAN;
+            uts.side[k] = -1;
+        }
 }
 
 // new UTS keys created by this message passing are appended after the existing
@@ -560,6 +569,7 @@ enum : int8_t {
     OP_MW_UTS = 8,
     OP_CLUSTER_TSE = 9,  // clustering.py:197-321 on track_state_estimates
     OP_CLUSTER_UTS = 10, // ... on updated_track_states
+    OP_FRESH = 11,       // finish the entries k_extrapolate wrote (weight = sender's, no prior/lr/side)
 };
 
 struct NodeOps {
@@ -577,6 +587,7 @@ __global__ void __launch_bounds__(BLOCK) k_node(gtf_graph g, gtf_nodes n, gtf_st
     const Seg s{g.slot_ptr[v], g.slot_ptr[v + 1]};
     for (int i = 0; i < ops.n; i++) {
         switch (ops.op[i]) {
+            case OP_FRESH: node_fresh(uts, e, s); break;
             case OP_RANKS: node_assign_ranks(uts, s); break;
             case OP_PRIORS_TSE: if (n.has_tse[v]) node_priors(g, e, tse, s); break;
             case OP_PRIORS_UTS: if (n.has_uts[v]) node_priors(g, e, uts, s); break;
@@ -662,7 +673,7 @@ void finish_ops(NodeOps& ops, const gtf_states* tse, const gtf_states* uts) {
     for (int i = 0; i < ops.n; i++) {
         const int o = ops.op[i];
         if (o == OP_PRIORS_TSE || o == OP_MW_TSE || o == OP_CLUSTER_TSE || o == OP_PRUNE) ops.uses_tse = 1;
-        if (o == OP_RANKS || o == OP_PRIORS_UTS || o == OP_REWEIGHT_UTS || o == OP_MW_UTS || o == OP_CLUSTER_UTS ||
+        if (o == OP_FRESH || o == OP_RANKS || o == OP_PRIORS_UTS || o == OP_REWEIGHT_UTS || o == OP_MW_UTS || o == OP_CLUSTER_UTS ||
             o == OP_PRUNE)
             ops.uses_uts = 1;
     }
@@ -854,7 +865,7 @@ int gtf_message_passing(const gtf_graph* g, gtf_nodes* n, gtf_states* uts, gtf_e
     Ws w = carve(ws, g->n_nodes, g->n_slots);
     rc = launch_extrap_edges(g, n, uts, e, p, w, (hipStream_t)stream);
     if (rc) return rc;
-    return launch_seq<OP_RANKS>(g, n, nullptr, uts, e, p, w, 0.0, 0.0, (hipStream_t)stream);
+    return launch_seq<OP_FRESH, OP_RANKS>(g, n, nullptr, uts, e, p, w, 0.0, 0.0, (hipStream_t)stream);
 }
 
 int gtf_node_ops(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts, gtf_edges* e,
@@ -863,7 +874,7 @@ int gtf_node_ops(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* 
     int rc = check_graph(g);
     if (rc) return rc;
     for (int i = 0; i < n_ops; i++)
-        if (ops[i] < OP_RANKS || ops[i] > OP_CLUSTER_UTS) {
+        if (ops[i] < OP_RANKS || ops[i] > OP_FRESH) {
             snprintf(g_err, sizeof(g_err), "unknown node op %d", (int)ops[i]);
             return -2;
         }

@@ -110,7 +110,7 @@ SYMBOLS = ["gtf_workspace_bytes", "gtf_clear_errors", "gtf_read_errors", "gtf_ex
            "gtf_version"]
 
 OPS = {"ranks": 1, "priors_tse": 2, "priors_uts": 3, "reweight_uts": 4, "degree": 5, "prune": 6, "mw_tse": 7,
-       "mw_uts": 8, "cluster_tse": 9, "cluster_uts": 10}
+       "mw_uts": 8, "cluster_tse": 9, "cluster_uts": 10, "fresh": 11}
 
 _lib = None
 

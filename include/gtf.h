@@ -159,7 +159,8 @@ int gtf_read_errors(void* workspace, uint32_t* flags, gtf_stream_t stream);
 int gtf_extrapolate(const gtf_graph* g, gtf_nodes* n, gtf_states* uts, gtf_edges* e,
                     const gtf_params* p, void* workspace, gtf_stream_t stream);
 /* message passing alone (extrapolate_merged_states.py:406-451): extrapolation of every
- * merged state along active out-edges, gate, Kalman update, UTS dict insertion. */
+ * merged state along active out-edges, gate, Kalman update, UTS dict insertion
+ * (GTF_OP_FRESH then GTF_OP_RANKS in the node kernel). */
 int gtf_message_passing(const gtf_graph* g, gtf_nodes* n, gtf_states* uts, gtf_edges* e,
                         const gtf_params* p, void* workspace, gtf_stream_t stream);
 
@@ -174,7 +175,10 @@ enum {
     GTF_OP_MW_TSE = 7,       /* helper.compute_mixture_weights(.., 'track_state_estimates') :76-96 */
     GTF_OP_MW_UTS = 8,
     GTF_OP_CLUSTER_TSE = 9,  /* clustering.py:197-321 on track_state_estimates */
-    GTF_OP_CLUSTER_UTS = 10
+    GTF_OP_CLUSTER_UTS = 10,
+    GTF_OP_FRESH = 11        /* the entries message passing (re)wrote (uts.fresh): mixture_weight =
+                                the sender's TSE weight (extrapolate_merged_states.py:384), prior / lr /
+                                side absent; gtf_message_passing / gtf_extrapolate / gtf_pass run it */
 };
 /* ops: host array of n_ops (<= 24) GTF_OP_* codes; thresholds used by the cluster ops. */
 int gtf_node_ops(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts, gtf_edges* e,

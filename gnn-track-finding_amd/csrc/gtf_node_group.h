@@ -639,6 +639,25 @@ struct OpSeq {
                                ((OPS == OP_RANKS) || ...) || fresh, fresh};
 };
 
+// has_uts of the node; where the sequence finishes message passing (OP_FRESH) a node that
+// received an entry gets its updated_track_states dict here (extrapolate_merged_states.py
+// :441-447), one store by the group's first lane instead of one per accepted slot
+template <int G>
+__device__ __forceinline__ bool fresh_has_uts(const NodeCtx<G>& c, gtf_nodes& n, bool with_fresh) {
+    bool h = n.has_uts[c.v];
+    if (with_fresh && !h && c.grp.any(c.valid && c.fresh)) {
+        h = true;
+        if (c.grp.gl == 0) n.has_uts[c.v] = 1;
+    }
+    return h;
+}
+
+__device__ __forceinline__ bool ops_have_fresh(const NodeOps& ops) {
+    for (int i = 0; i < ops.n; i++)
+        if (ops.op[i] == OP_FRESH) return true;
+    return false;
+}
+
 // compile-time op sequence for one group size: dead ops are compiled out.
 // `bid` is the block index inside this bucket's range of the launch.
 template <int G, int... OPS>
@@ -653,7 +672,8 @@ __device__ __forceinline__ void node_seq_body(const gtf_graph& g, gtf_nodes& n, 
     if (!node_load(c, g, n, tse, uts, e, list, seg, count, gi, Q::need)) return;
     double* sval = (double*)smem + (threadIdx.x & ~63);
     Stage* stg = (Stage*)(smem + BLOCK * sizeof(double)) + (Q::cluster ? (int)threadIdx.x / G : 0);
-    const bool has_tse = n.has_tse[c.v], has_uts = n.has_uts[c.v];
+    const bool has_tse = n.has_tse[c.v];
+    const bool has_uts = fresh_has_uts(c, n, Q::fresh);
 #if GTF_ABLATE == 4
     // diagnostics build: the node's loads and stores only (every field marked dirty)
     if (has_tse || has_uts) { c.uts.dirty = c.tse.dirty = D_RANK | D_MW | D_PRIOR; c.uts_dirty_lr = true; c.edge_mw_dirty = true; }
@@ -768,7 +788,8 @@ __global__ void __launch_bounds__(BLOCK) k_node_pack(gtf_graph g, gtf_nodes n, g
     if (!node_fields(c, g, tse, uts, e, Q::need)) return;
     double* sval = (double*)smem + (threadIdx.x & ~63);
     Stage* stg = (Stage*)(smem + BLOCK * sizeof(double)) + (Q::cluster ? (int)threadIdx.x / 64 : 0);
-    const bool has_tse = n.has_tse[c.v], has_uts = n.has_uts[c.v];
+    const bool has_tse = n.has_tse[c.v];
+    const bool has_uts = fresh_has_uts(c, n, Q::fresh);
     (node_op<0, OPS, Stage>(c, g, n, tse, uts, p, w, sval, stg, chi2_thr, kl_thr, has_tse, has_uts), ...);
     node_store(c, n, tse, uts, e);
 }
@@ -790,7 +811,8 @@ __global__ void __launch_bounds__(BLOCK) k_node_group(gtf_graph g, gtf_nodes n, 
     if (!node_load(c, g, n, tse, uts, e, list, seg, count, gi, nd)) return;
     double* sval = s_val + (threadIdx.x & ~63);
     Stage* stg = s_stage + (int)threadIdx.x / G;
-    const bool has_tse = n.has_tse[c.v], has_uts = n.has_uts[c.v];
+    const bool has_tse = n.has_tse[c.v];
+    const bool has_uts = fresh_has_uts(c, n, ops_have_fresh(ops));
     for (int i = 0; i < ops.n; i++) {
         switch (ops.op[i]) {
 #define GTF_CASE(OPC) \

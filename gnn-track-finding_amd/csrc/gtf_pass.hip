@@ -178,7 +178,6 @@ __global__ void __launch_bounds__(BLOCK) k_extrapolate(gtf_graph g, gtf_nodes n,
     const int src = g.slot_src[k], v = g.slot_dst[k];
     const double2 vc = w.vc[k];        // written by k_sender for active edges of merged senders
     const double smw = e.send_mw[k];
-    uts.fresh[k] = 0;
     const int u = src >= 0 ? src : 0;   // orphan keys have no sender
     const double* ng = g.gnn + 4 * (int64_t)u;  // sender ("node" in the reference)
     const double* nb = g.gnn + 4 * (int64_t)v;  // receiver ("neighbour")
@@ -188,7 +187,10 @@ __global__ void __launch_bounds__(BLOCK) k_extrapolate(gtf_graph g, gtf_nodes n,
     const double a = n.merged_state[3 * u + 0], b = n.merged_state[3 * u + 1], c = n.merged_state[3 * u + 2];
     const double* mcp = n.merged_cov + 5 * (int64_t)u;
     const double mc00 = mcp[0], mc01 = mcp[1], mc10 = mcp[2], mc22 = mcp[4];
-    if (!is_edge || src < 0 || !hm || act != 1) return;
+    if (!is_edge || src < 0 || !hm || act != 1) {
+        uts.fresh[k] = 0;
+        return;
+    }
 
     // cos/sin of atan2(y, x) as x/h, y/h (h = |(x, y)|): the same angles as the
     // reference's atan2 -> cos/sin round trips, to a couple of ulps, without fp64 libm
@@ -238,6 +240,7 @@ __global__ void __launch_bounds__(BLOCK) k_extrapolate(gtf_graph g, gtf_nodes n,
     const double chi2 = (resid * invS) * resid;                                    // :140
     if (!(chi2 <= p.chi2_cut)) {                                                   // :298
         e.act[k] = 0;                                                              // :393
+        uts.fresh[k] = 0;
         return;
     }
     const double lik = (1.0 / sqrt((2.0 * M_PI) * fabs(S))) * exp(-0.5 * chi2);  // :302-304
@@ -289,8 +292,7 @@ __global__ void __launch_bounds__(BLOCK) k_extrapolate(gtf_graph g, gtf_nodes n,
     uts.lik[k] = lik;
     // mixture_weight = smw (:384) and the empty prior / lr / side of a fresh entry are set
     // by the node kernel's OP_FRESH, merged with its own stores of those fields
-    uts.fresh[k] = 1;
-    n.has_uts[v] = 1;  // benign same-value race between the receiver's accepted slots
+    uts.fresh[k] = 1;   // the receiver's has_uts flag follows in the node kernel (OP_FRESH)
 }
 
 // ---------------------------------------------------------------------------
@@ -423,9 +425,10 @@ __device__ void node_mixture_weights(const gtf_graph& g, gtf_states& st, Seg s, 
 }
 
 // the fields of the entries message passing (re)wrote (g_fresh, thread-per-node form)
-__device__ void node_fresh(gtf_states& uts, const gtf_edges& e, Seg s) {
+__device__ void node_fresh(gtf_nodes& n, gtf_states& uts, const gtf_edges& e, Seg s, int v) {
     for (int k = s.lo; k < s.hi; k++)
         if (uts.fresh[k]) {
+            n.has_uts[v] = 1;
             uts.mw[k] = e.send_mw[k];
             uts.prior[k] = NAN;
             uts.lr[k] = NAN;
@@ -587,7 +590,7 @@ __global__ void __launch_bounds__(BLOCK) k_node(gtf_graph g, gtf_nodes n, gtf_st
     const Seg s{g.slot_ptr[v], g.slot_ptr[v + 1]};
     for (int i = 0; i < ops.n; i++) {
         switch (ops.op[i]) {
-            case OP_FRESH: node_fresh(uts, e, s); break;
+            case OP_FRESH: node_fresh(n, uts, e, s, v); break;
             case OP_RANKS: node_assign_ranks(uts, s); break;
             case OP_PRIORS_TSE: if (n.has_tse[v]) node_priors(g, e, tse, s); break;
             case OP_PRIORS_UTS: if (n.has_uts[v]) node_priors(g, e, uts, s); break;

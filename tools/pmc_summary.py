@@ -23,6 +23,7 @@ NAMES = {
     "k_node_multi<1, 3, 4, 3, 4, 5, 6, 2, 3, 4>": "k_node_multi<reweight,update>",
     "k_node_multi<10, 5, 8, 3>": "k_node_multi<cluster> (KL-distance kernel)",
     "k_node_multi<1, 3, 4, 3, 4, 5, 6, 2, 3, 4, 10, 5, 8, 3>": "k_node_multi<update+cluster> (KL-distance kernel)",
+    "k_node_multi<11, 1, 3, 4, 3, 4, 5, 6, 2, 3, 4, 10, 5, 8, 3>": "k_node_multi<update+cluster> (KL-distance kernel)",
 }
 
 

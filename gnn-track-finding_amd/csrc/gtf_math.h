@@ -227,6 +227,19 @@ __device__ __forceinline__ Mat3 mm3t(const Mat3& A, const Mat3& B) {
     return C;
 }
 
+// A * C for a block-diagonal C ([[c00 c01 0] [c10 c11 0] [0 0 c22]]): the products with
+// C's exact zeros, which add nothing to the reference's sums, are skipped
+__device__ __forceinline__ Mat3 mul_block(const Mat3& A, const Mat3& C) {
+    Mat3 R;
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        R.m[i][0] = A.m[i][0] * C.m[0][0] + A.m[i][1] * C.m[1][0];
+        R.m[i][1] = A.m[i][0] * C.m[0][1] + A.m[i][1] * C.m[1][1];
+        R.m[i][2] = A.m[i][2] * C.m[2][2];
+    }
+    return R;
+}
+
 __device__ __forceinline__ void mv3(const Mat3& A, const double x[3], double y[3]) {
 #pragma unroll
     for (int i = 0; i < 3; i++) {

@@ -232,7 +232,7 @@ __global__ void __launch_bounds__(BLOCK) k_extrapolate(gtf_graph g, gtf_nodes n,
     const double m[3] = {a, b, c};
     double xe[3];
     mv3(F, m, xe);                                                                 // :129
-    const Mat3 Pe = mm3t(mm3(F, C), F);                                            // :130
+    const Mat3 Pe = mm3t(mul_block(F, C), F);                                      // :130
     const double sig2 = p.sigma0xy * p.sigma0xy;
     const double S = Pe.m[2][2] + sig2;                                            // :138
     const double invS = 1.0 / S;
@@ -256,12 +256,19 @@ __global__ void __launch_bounds__(BLOCK) k_extrapolate(gtf_graph g, gtf_nodes n,
     const double K0 = Pp.m[0][2] * SI, K1 = Pp.m[1][2] * SI, K2 = Pp.m[2][2] * SI;
     const double xu0 = xp[0] + K0 * y, xu1 = xp[1] + K1 * y, xu2 = xp[2] + K2 * y;
     const Mat3 IKH = {{{1.0, 0.0, 0.0 - K0}, {0.0, 1.0, 0.0 - K1}, {0.0, 0.0, 1.0 - K2}}};
-    const Mat3 A = mm3(IKH, Pp);
+    // A = (I - K H) Pp, rows 0 and 1 (the only ones the aliased [a, b] block reads); the
+    // identity's exact zero / one entries contribute nothing to the reference's sums
+    Mat3 A;
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+        A.m[0][j] = Pp.m[0][j] + IKH.m[0][2] * Pp.m[2][j];
+        A.m[1][j] = Pp.m[1][j] + IKH.m[1][2] * Pp.m[2][j];
+    }
     // P = A IKH^T + (K R) K^T, only the [a,b] block survives the aliasing (:362-365)
-    double P00 = A.m[0][0] * IKH.m[0][0]; P00 = P00 + A.m[0][1] * IKH.m[0][1]; P00 = P00 + A.m[0][2] * IKH.m[0][2];
-    double P01 = A.m[0][0] * IKH.m[1][0]; P01 = P01 + A.m[0][1] * IKH.m[1][1]; P01 = P01 + A.m[0][2] * IKH.m[1][2];
-    double P10 = A.m[1][0] * IKH.m[0][0]; P10 = P10 + A.m[1][1] * IKH.m[0][1]; P10 = P10 + A.m[1][2] * IKH.m[0][2];
-    double P11 = A.m[1][0] * IKH.m[1][0]; P11 = P11 + A.m[1][1] * IKH.m[1][1]; P11 = P11 + A.m[1][2] * IKH.m[1][2];
+    double P00 = A.m[0][0] + A.m[0][2] * IKH.m[0][2];
+    double P01 = A.m[0][1] + A.m[0][2] * IKH.m[1][2];
+    double P10 = A.m[1][0] + A.m[1][2] * IKH.m[0][2];
+    double P11 = A.m[1][1] + A.m[1][2] * IKH.m[1][2];
     P00 = P00 + (K0 * sig2) * K0;
     P01 = P01 + (K0 * sig2) * K1;
     P10 = P10 + (K1 * sig2) * K0;

@@ -146,10 +146,12 @@ class DeviceGraph:
         up("sched_seg", sched_segments(g.slot_ptr, sched))
         osched, self.n_o = sender_schedule(g.out_ptr)
         up("out_sched", osched)
-        pent, pwave = pack_schedule(g.slot_ptr)
-        up("pack_ent", pent)
-        up("pack_wave", pwave)
-        self.n_pack_waves = int(pwave.size - 1)
+        self.n_pack_waves = 0
+        if pack:   # the packed lane segments are built only when asked for
+            pent, pwave = pack_schedule(g.slot_ptr)
+            up("pack_ent", pent)
+            up("pack_wave", pwave)
+            self.n_pack_waves = int(pwave.size - 1)
         self.n_g_all = [int(b.size) for b in buckets]
         self.n_big = int(rest.size)
         self.n_g = self.n_g_all if schedule else [0] * len(BUCKETS)

@@ -105,8 +105,7 @@ struct LaneDict {
     uint8_t dirty;   // D_* bits of the fields an op changed
     int pos;         // cached dict position (-1 absent), valid while pos_ok
     bool pos_ok;
-    int last;        // group lane of the last dict key (largest rank), valid while pos_ok
-    bool has_last;   // the dict has a key (valid while pos_ok)
+    int last;        // group lane of the last dict key (largest rank), valid while last_ok
     bool last_ok;
 };
 
@@ -561,8 +560,8 @@ __device__ __forceinline__ bool node_fields(NodeCtx<G>& c, const gtf_graph& g, c
     c.same_layer_ok = false;
     c.same_x = 0;
     c.same_x_ok = false;
-    c.tse = LaneDict{-1, 0.0, 0.0, 0, -1, false, 0, false, false};
-    c.uts = LaneDict{-1, 0.0, 0.0, 0, -1, false, 0, false, false};
+    c.tse = LaneDict{-1, 0.0, 0.0, 0, -1, false, 0, false};
+    c.uts = LaneDict{-1, 0.0, 0.0, 0, -1, false, 0, false};
     c.lik = 0; c.lr = 0; c.x0 = 0; c.edge_mw = 0; c.side = -1; c.fresh = 0;
     c.uts_dirty_lr = false; c.edge_mw_dirty = false; c.degree = 0; c.degree_set = false;
     // only what an op reads: mw of the TSE dict, lr and side are written, never read

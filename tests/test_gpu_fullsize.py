@@ -68,7 +68,9 @@ def _run(g, how, p):
         d.cluster("uts", p.cluster_chi2, p.cluster_kl, p)
     elif how == "interpreter":
         d.message_passing(p)
-        d.node_ops(["priors_uts", "reweight_uts", "priors_uts", "reweight_uts", "degree", "prune", "priors_tse",
+        # "fresh" and "ranks" again: both are idempotent right after message passing, and this
+        # runs the interpreter's own OP_FRESH / OP_RANKS code
+        d.node_ops(["fresh", "ranks", "priors_uts", "reweight_uts", "priors_uts", "reweight_uts", "degree", "prune", "priors_tse",
                     "priors_uts", "reweight_uts"], p)
         d.node_ops(["cluster_uts", "degree", "mw_uts", "priors_uts"], p, p.cluster_chi2, p.cluster_kl)
     d.torch.cuda.synchronize()

@@ -9,7 +9,9 @@ device-to-device restore of the arrays the pass mutates (activation mask,
 state-dict ranks, merged states) so every step processes the same input; the
 restore is inside the timed region. Default workload "c4" = BASELINE.json
 configs[3], a pileup-200-shaped event (~180k hits, ~1.0M directed edges),
-the config the north-star 1-GPU target is quoted on; it fits one GPU.
+the config the north-star 1-GPU target is quoted on; it fits one GPU. The event
+is uploaded with its nodes renumbered into the node kernel's schedule order
+(--layout schedule, the default; --layout natural keeps the host order).
 
 The K steps are timed twice, each run bracketed by barrier + synchronize: first
 as a caller runs them (value, ms_per_step), then with HIP events recorded before,
@@ -140,7 +142,7 @@ def bench_sharded(workload, rank, world, dev, steps, warmup, params):
 # the fused node kernel: priors, side norm, reweights, update and KL clustering of every
 # receiver in one launch (gtf_pass.hip run_pass)
 NODE_KERNEL = "k_node_multi<update+cluster> (KL-distance kernel)"
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_v8", "pmc_c4.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_v9", "pmc_c4.json")
 
 
 def committed_traffic(workload, kernel):
@@ -168,7 +170,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-c5", action="store_true", help="skip the config-5 parabolic-KL section")
     ap.add_argument("--no-sharded", action="store_true", help="skip the single-event sharded section (N > 1)")
-    ap.add_argument("--layout", default="natural", choices=["natural", "schedule"],
+    ap.add_argument("--layout", default="schedule", choices=["schedule", "natural"],
                     help="device node order (DeviceGraph layout)")
     args = ap.parse_args()
 
@@ -193,8 +195,9 @@ def main():
 
     p = Params()
     g = synth.workload(args.workload, seed=1000 * rank)
-    # --layout schedule renumbers the nodes into schedule order (same results bit for bit;
-    # contiguous node-kernel loads, but the sender/receiver gathers lose their locality)
+    # nodes renumbered into schedule order on upload (DeviceGraph layout "schedule", the
+    # default): each wavefront of the node kernel reads one contiguous run of slots; the
+    # pass's results are the same bit for bit (tests/test_gpu_fullsize.py)
     d = DeviceGraph(g, dev, layout=args.layout)
     snap = d.snapshot(DeviceGraph.PASS_INPUTS)
     K, W = args.steps, args.warmup

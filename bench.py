@@ -10,8 +10,9 @@ state-dict ranks, merged states) so every step processes the same input; the
 restore is inside the timed region. Default workload "c4" = BASELINE.json
 configs[3], a pileup-200-shaped event (~180k hits, ~1.0M directed edges),
 the config the north-star 1-GPU target is quoted on; it fits one GPU. The event
-is uploaded with its nodes renumbered into the node kernel's schedule order
-(--layout schedule, the default; --layout natural keeps the host order).
+is uploaded with its nodes renumbered into the node kernel's schedule order tile
+by tile (--layout tiled, the default; "schedule" without tiles, "natural" keeps
+the host order).
 
 The K steps are timed twice, each run bracketed by barrier + synchronize: first
 as a caller runs them (value, ms_per_step), then with HIP events recorded before,
@@ -142,7 +143,7 @@ def bench_sharded(workload, rank, world, dev, steps, warmup, params):
 # the fused node kernel: priors, side norm, reweights, update and KL clustering of every
 # receiver in one launch (gtf_pass.hip run_pass)
 NODE_KERNEL = "k_node_multi<update+cluster> (KL-distance kernel)"
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_v9", "pmc_c4.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_v10", "pmc_c4.json")
 
 
 def committed_traffic(workload, kernel):
@@ -170,8 +171,9 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-c5", action="store_true", help="skip the config-5 parabolic-KL section")
     ap.add_argument("--no-sharded", action="store_true", help="skip the single-event sharded section (N > 1)")
-    ap.add_argument("--layout", default="schedule", choices=["schedule", "natural"],
+    ap.add_argument("--layout", default="tiled", choices=["tiled", "schedule", "natural"],
                     help="device node order (DeviceGraph layout)")
+    ap.add_argument("--tile", type=int, default=4096, help="nodes per tile of --layout tiled")
     args = ap.parse_args()
 
     import torch
@@ -195,10 +197,12 @@ def main():
 
     p = Params()
     g = synth.workload(args.workload, seed=1000 * rank)
-    # nodes renumbered into schedule order on upload (DeviceGraph layout "schedule", the
-    # default): each wavefront of the node kernel reads one contiguous run of slots; the
-    # pass's results are the same bit for bit (tests/test_gpu_fullsize.py)
-    d = DeviceGraph(g, dev, layout=args.layout)
+    # nodes renumbered on upload (DeviceGraph layout "tiled", the default): inside every
+    # run of 4096 nodes, bucketed by slot count, so each wavefront of the node kernel
+    # reads one contiguous run of slots while neighbouring hits stay close for the sender
+    # and extrapolation gathers; the results are the same bit for bit
+    # (tests/test_gpu_fullsize.py)
+    d = DeviceGraph(g, dev, layout=args.layout, tile=args.tile)
     snap = d.snapshot(DeviceGraph.PASS_INPUTS)
     K, W = args.steps, args.warmup
     NE = 5

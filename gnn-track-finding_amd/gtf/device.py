@@ -78,12 +78,21 @@ def _torch():
     return torch
 
 
-def schedule_order(slot_ptr):
+def schedule_order(slot_ptr, tile=0):
     """node indices bucketed by slot count as the node-kernel schedule takes them
-    (BUCKETS, then the nodes beyond 64 slots), node order inside a bucket"""
+    (BUCKETS, then the nodes beyond 64 slots), node order inside a bucket. tile > 0:
+    the same inside every run of `tile` consecutive nodes, tile after tile, so a bucket's
+    nodes stay contiguous within a tile and spatially close nodes stay close"""
     deg = np.diff(np.asarray(slot_ptr, dtype=np.int64))
     idx = np.arange(deg.size, dtype=np.int64)
-    return np.concatenate([idx[(deg >= lo) & (deg <= hi)] for lo, hi in BUCKETS] + [idx[deg > 64]])
+    bucket = np.full(deg.size, len(BUCKETS), np.int64)
+    for q, (lo, hi) in reversed(list(enumerate(BUCKETS))):
+        bucket[(deg >= lo) & (deg <= hi)] = q
+    t = idx // tile if tile > 0 else np.zeros_like(idx)
+    return np.lexsort((idx, bucket, t))
+
+
+TILE = 4096   # nodes per tile of the "tiled" layout
 
 
 class DeviceGraph:
@@ -97,15 +106,15 @@ class DeviceGraph:
     stage methods are layout-independent (the pass is equivariant under renumber)."""
 
     def __init__(self, g: TrackGraph, device: str = "cuda", schedule: bool = True, layout: str = "natural",
-                 pack: bool = False):
+                 pack: bool = False, tile: int = TILE):
         torch = _torch()
         self.layout = layout
         self.order = self.slot_perm = None
-        if layout == "schedule":
-            self.order = schedule_order(g.slot_ptr)
+        if layout in ("schedule", "tiled"):
+            self.order = schedule_order(g.slot_ptr, tile if layout == "tiled" else 0)
             g, self.slot_perm = renumber(g, self.order)
         elif layout != "natural":
-            raise ValueError("layout must be 'natural' or 'schedule'")
+            raise ValueError("layout must be 'natural', 'schedule' or 'tiled'")
         self.slot_ptr_host = g.slot_ptr
         self.torch = torch
         self.device = torch.device(device)

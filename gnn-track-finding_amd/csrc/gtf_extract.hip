@@ -523,7 +523,8 @@ size_t gtf_extract_workspace_bytes(int32_t n_nodes, int32_t n_sub) {
 
 int gtf_extract_candidates(const gtf_graph* g, const gtf_edges* e, const gtf_extract_io* io,
                            const gtf_extract_params* p, void* workspace, gtf_stream_t stream) {
-    if (!g || !e || !io || !p || !workspace) { gtf::set_error("gtf_extract_candidates: null argument"); return -2; }
+    if (int rc = gtf::check_abi(g, "gtf_extract_candidates")) return rc;
+    if (!e || !io || !p || !workspace) { gtf::set_error("gtf_extract_candidates: null argument"); return -2; }
     const int n = g->n_nodes;
     if (n <= 0) return 0;
     if (!io->xyzr || !io->vivl || !io->sub_id || !io->sub_ptr || !io->gnn || !io->label || !io->status ||

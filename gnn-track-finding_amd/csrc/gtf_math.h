@@ -10,8 +10,32 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 #include <stdint.h>
+#include <stdio.h>
+
+#include "../../include/gtf.h"
 
 namespace gtf {
+
+void set_error(const char* msg);   // gtf_last_error() text (gtf_pass.hip)
+
+// A gtf_graph built against another layout of include/gtf.h: refused with status -3
+// instead of read with shifted fields. Host side, every entry point taking a gtf_graph.
+inline int check_abi(const gtf_graph* g, const char* who) {
+    if (!g) {
+        char m[160];
+        snprintf(m, sizeof(m), "%s: null graph", who);
+        set_error(m);
+        return -2;
+    }
+    if (g->struct_size != (uint32_t)sizeof(gtf_graph) || g->abi_version != GTF_ABI_VERSION) {
+        char m[200];
+        snprintf(m, sizeof(m), "%s: gtf_graph ABI mismatch (caller struct_size %u, abi_version %u; library %u, %u)",
+                 who, g->struct_size, g->abi_version, (unsigned)sizeof(gtf_graph), (unsigned)GTF_ABI_VERSION);
+        set_error(m);
+        return -3;
+    }
+    return 0;
+}
 
 // XCD-aware block index. MI355X deals workgroups round-robin over its 8 XCDs, each with
 // its own 4 MiB L2 (MI355X_MICROARCH.md, workgroup dispatch), so consecutive blocks --

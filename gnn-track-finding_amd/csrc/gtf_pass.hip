@@ -629,7 +629,7 @@ int fail(const char* what, hipError_t e) {
 }
 
 int check_graph(const gtf_graph* g) {
-    if (!g) { snprintf(g_err, sizeof(g_err), "null graph"); return -2; }
+    if (int rc = check_abi(g, "gtf_pass")) return rc;
     if (g->n_nodes < 0 || g->n_slots < 0 || g->n_edges < 0) {
         snprintf(g_err, sizeof(g_err), "negative sizes"); return -2;
     }

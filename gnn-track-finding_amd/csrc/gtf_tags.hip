@@ -61,6 +61,7 @@ extern "C" {
 
 int gtf_tag_prepare(const gtf_graph* g, const double* radius, uint8_t* keep, uint8_t* processed,
                     int32_t* n_processed, gtf_stream_t stream) {
+    if (int rc = gtf::check_abi(g, "gtf_tag_prepare")) return rc;
     hipStream_t st = (hipStream_t)stream;
     if (hipMemsetAsync(n_processed, 0, sizeof(int32_t), st) != hipSuccess) return -1;
     if (g->n_nodes > 0)
@@ -71,6 +72,7 @@ int gtf_tag_prepare(const gtf_graph* g, const double* radius, uint8_t* keep, uin
 
 int gtf_tag_sweep(const gtf_graph* g, const uint8_t* keep, const uint8_t* processed, const int64_t* tags_in,
                   int64_t* tags_out, int32_t* flips, gtf_stream_t stream) {
+    if (int rc = gtf::check_abi(g, "gtf_tag_sweep")) return rc;
     hipStream_t st = (hipStream_t)stream;
     if (hipMemsetAsync(flips, 0, sizeof(int32_t), st) != hipSuccess) return -1;
     if (g->n_nodes > 0)

@@ -285,7 +285,8 @@ __global__ void __launch_bounds__(BLOCK) k_tse(gtf_graph g, gtf_states tse, gtf_
 
 extern "C" int gtf_track_state_estimates(const gtf_graph* g, gtf_states* tse, const gtf_tse_extra* x,
                                          const gtf_params* p, gtf_stream_t stream) {
-    if (!g || !tse || !x || !p) { gtf::set_error("gtf_track_state_estimates: null argument"); return -2; }
+    if (int rc = gtf::check_abi(g, "gtf_track_state_estimates")) return rc;
+    if (!tse || !x || !p) { gtf::set_error("gtf_track_state_estimates: null argument"); return -2; }
     if (g->n_nodes < 0 || g->n_slots < 0) { gtf::set_error("gtf_track_state_estimates: negative sizes"); return -2; }
     if (g->n_nodes == 0) return 0;
     if (!g->sched || !g->slot_ptr || !g->slot_src || !g->gnn || !tse->rank || !tse->sv || !tse->tau || !tse->cov ||

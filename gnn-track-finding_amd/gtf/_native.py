@@ -15,8 +15,14 @@ I32 = ctypes.c_int32
 F64 = ctypes.c_double
 
 
+U32 = ctypes.c_uint32
+ABI_VERSION = 2   # GTF_ABI_VERSION of include/gtf.h
+
+
 class GtfGraph(ctypes.Structure):
-    _fields_ = [("n_nodes", I32), ("n_slots", I32), ("n_edges", I32), ("n_big", I32),
+    """gtf_graph; keyword construction only -- struct_size / abi_version are filled in,
+    and the library refuses a struct of another layout (status -3)"""
+    _fields_ = [("struct_size", U32), ("abi_version", U32), ("n_nodes", I32), ("n_slots", I32), ("n_edges", I32), ("n_big", I32),
                 ("slot_ptr", P), ("slot_src", P), ("slot_dst", P), ("out_ptr", P), ("out_slot", P),
                 ("slot_outpos", P),
                 ("is_edge", P), ("rev_edge", P), ("solo", P), ("gnn", P), ("xyzr", P), ("layer", P),
@@ -24,6 +30,11 @@ class GtfGraph(ctypes.Structure):
                 ("slot_layer", P), ("n_g4", I32), ("sched_seg", P),
                 ("out_sched", P), ("n_o4", I32), ("n_o8", I32), ("n_o16", I32), ("n_g2", I32),
                 ("pack_ent", P), ("pack_wave", P), ("n_pack_waves", I32)]
+
+    def __init__(self, **fields):
+        super().__init__(**fields)
+        self.struct_size = ctypes.sizeof(GtfGraph)
+        self.abi_version = ABI_VERSION
 
 
 class GtfNodes(ctypes.Structure):
@@ -83,6 +94,10 @@ class GtfKlGraph(ctypes.Structure):
                 ("pair_ptr", P), ("list", P * 4), ("count", I32 * 4)]
 
 
+class GtfPairOut(ctypes.Structure):
+    _fields_ = [("chi2", P), ("avg_tau", P), ("avg_theta", P), ("delta_theta", P), ("truth", P), ("err", P)]
+
+
 class GtfKlOut(ctypes.Structure):
     _fields_ = [("kl", P), ("truth", P), ("emp_var", P), ("emp_mean", P), ("sv", P), ("cov", P), ("err", P)]
 
@@ -98,6 +113,9 @@ ERR_FLAGS = {
     32: "ValueError: NaN KL distance (clustering.py:117)",
     64: "KeyError: node has no state dict (remove_state_metadata.py:39)",
     128: "LinAlgError: singular parabola matrix H (learn_KL_parabolic_model utils.py:277)",
+    256: "pair_ptr disagrees with the updated_track_states dicts (caller error)",
+    512: "KeyError: neighbour not in the subgraph (calculate_distance_between_updated_track_states.py:182-183)",
+    1024: "a node holds more than 2048 updated track states (not processed)",
 }
 
 # exported symbols (must match include/gtf.h; tests check the .so exports all of them)
@@ -106,6 +124,7 @@ SYMBOLS = ["gtf_workspace_bytes", "gtf_clear_errors", "gtf_read_errors", "gtf_ex
            "gtf_cluster", "gtf_pass", "gtf_pass_ev", "gtf_tag_prepare", "gtf_tag_sweep", "gtf_parabolic_kl", "gtf_track_state_estimates", "gtf_pass_shard",
            "gtf_shard_chunk_bytes", "gtf_shard_pack", "gtf_shard_unpack", "gtf_extract_workspace_bytes",
            "gtf_extract_candidates", "gtf_build_event_csr", "gtf_candidate_order",
+           "gtf_updated_state_pair_counts", "gtf_updated_state_distances",
            "gtf_last_error",
            "gtf_version"]
 
@@ -156,13 +175,15 @@ def lib():
     L.gtf_parabolic_kl.argtypes = [ctypes.POINTER(GtfKlGraph), I32, ctypes.POINTER(GtfKlOut), P]
     L.gtf_build_event_csr.argtypes = [ctypes.POINTER(GtfEventCsr)]
     L.gtf_candidate_order.argtypes = [ctypes.POINTER(GtfCandidateGraph), P]
+    L.gtf_updated_state_pair_counts.argtypes = [G, N, S, E, P, P]
+    L.gtf_updated_state_distances.argtypes = [G, N, S, E, P, P, ctypes.POINTER(GtfPairOut), P]
     L.gtf_last_error.restype = ctypes.c_char_p
     L.gtf_version.restype = ctypes.c_char_p
     for fn in ("gtf_clear_errors", "gtf_read_errors", "gtf_extrapolate", "gtf_update", "gtf_cluster", "gtf_pass",
                "gtf_pass_ev", "gtf_message_passing", "gtf_node_ops",
                "gtf_tag_prepare", "gtf_tag_sweep", "gtf_parabolic_kl", "gtf_track_state_estimates", "gtf_pass_shard", "gtf_shard_pack",
                "gtf_shard_unpack", "gtf_extract_candidates", "gtf_build_event_csr",
-               "gtf_candidate_order"):
+               "gtf_candidate_order", "gtf_updated_state_pair_counts", "gtf_updated_state_distances"):
         getattr(L, fn).restype = ctypes.c_int
     _lib = L
     return L

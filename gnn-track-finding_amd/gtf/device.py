@@ -207,22 +207,24 @@ class DeviceGraph:
 
     def _build_structs(self, pack=True):
         p = self.ptr
-        self.cg = nat.GtfGraph(self.n_nodes, self.n_slots, self.n_edges, self.n_big if self.use_sched else 0,
-                               p("slot_ptr"), p("slot_src"),
-                               p("slot_dst"), p("out_ptr"), p("out_slot"), p("slot_outpos"), p("is_edge"), p("rev_edge"), p("solo"),
-                               p("gnn"), p("xyzr"), p("layer"),
-                               p("sched") if self.use_sched else ctypes.c_void_p(0), *self.n_g[1:], p("out_dst"),
-                               p("slot_layer"), self.n_g[0], p("sched_seg") if self.use_sched else ctypes.c_void_p(0),
-                               p("out_sched") if self.use_sched else ctypes.c_void_p(0), *self.n_o,
-                               self.n_g2 if self.use_sched else 0,
-                               *((p("pack_ent"), p("pack_wave"), self.n_pack_waves) if self.use_sched and pack
-                                 else (ctypes.c_void_p(0), ctypes.c_void_p(0), 0)))
-        self.cg_sched = nat.GtfGraph(self.n_nodes, self.n_slots, self.n_edges, self.n_big, p("slot_ptr"),
-                                     p("slot_src"),
-                                     p("slot_dst"), p("out_ptr"), p("out_slot"), p("slot_outpos"), p("is_edge"),
-                                     p("rev_edge"), p("solo"), p("gnn"), p("xyzr"), p("layer"), p("sched"),
-                                     *self.n_g_all[1:], p("out_dst"), p("slot_layer"), self.n_g_all[0],
-                                     p("sched_seg"), p("out_sched"), *self.n_o, self.n_g2)
+        base = dict(n_nodes=self.n_nodes, n_slots=self.n_slots, n_edges=self.n_edges,
+                    slot_ptr=p("slot_ptr"), slot_src=p("slot_src"), slot_dst=p("slot_dst"), out_ptr=p("out_ptr"),
+                    out_slot=p("out_slot"), slot_outpos=p("slot_outpos"), is_edge=p("is_edge"),
+                    rev_edge=p("rev_edge"), solo=p("solo"), gnn=p("gnn"), xyzr=p("xyzr"), layer=p("layer"),
+                    out_dst=p("out_dst"), slot_layer=p("slot_layer"))
+        # with the node schedule (lane groups) and the sender schedule
+        sched = dict(n_big=self.n_big, sched=p("sched"), n_g4=self.n_g_all[0], n_g8=self.n_g_all[1],
+                     n_g16=self.n_g_all[2], n_g32=self.n_g_all[3], n_g64=self.n_g_all[4], sched_seg=p("sched_seg"),
+                     out_sched=p("out_sched"), n_o4=self.n_o[0], n_o8=self.n_o[1], n_o16=self.n_o[2],
+                     n_g2=self.n_g2)
+        if not self.use_sched:   # thread per node, 8-lane sender scan
+            self.cg = nat.GtfGraph(**base)
+        elif pack and self.n_pack_waves:
+            self.cg = nat.GtfGraph(**base, **sched, pack_ent=p("pack_ent"), pack_wave=p("pack_wave"),
+                                   n_pack_waves=self.n_pack_waves)
+        else:
+            self.cg = nat.GtfGraph(**base, **sched)
+        self.cg_sched = nat.GtfGraph(**base, **sched)
         self.cn = nat.GtfNodes(*[p(f) for f in MUTABLE_NODE])
         self.cuts = nat.GtfStates(p("uts_rank"), p("uts_sv"), p("uts_tau"), p("uts_cov"), p("uts_xyzr"),
                                   p("uts_lik"), p("uts_mw"), p("uts_prior"), p("uts_lr"), p("uts_side"),
@@ -324,6 +326,46 @@ class DeviceGraph:
         nat.check(self.lib.gtf_track_state_estimates(ctypes.byref(self.cg_sched), ctypes.byref(self.ctse),
                                                      ctypes.byref(ex), ctypes.byref(cp), self.stream))
         return x
+
+    # ------------------------------------------ a15: distances between updated states
+    def updated_state_distances(self, truth=None):
+        """calculate_distance_between_updated_track_states.py (:27-104 over the pair loop
+        :134-195) on the current updated_track_states: every pair i > j of the dict entries
+        of each node with the dict and more than one active in-edge. Returns (pair_ptr [N+1]
+        int64, {"chi2", "avg_tau", "avg_theta", "delta_theta"[, "truth"]}) as device
+        tensors, pairs of node v at [pair_ptr[v], pair_ptr[v+1]) in the reference's loop
+        order. truth: [N] truth_particle per node (host or device), or None."""
+        self._natural_only("updated_state_distances")
+        torch = self.torch
+        dev = self.device
+        N = self.n_nodes
+        vp = lambda t: ctypes.c_void_p(t.data_ptr() if t is not None and t.numel() else 0)  # noqa: E731
+        counts = torch.zeros(max(N, 1), dtype=torch.int64, device=dev)
+        nat.check(self.lib.gtf_updated_state_pair_counts(ctypes.byref(self.cg_sched), ctypes.byref(self.cn),
+                                                         ctypes.byref(self.cuts), ctypes.byref(self.ce), vp(counts),
+                                                         self.stream))
+        pair_ptr = torch.zeros(N + 1, dtype=torch.int64, device=dev)
+        if N:
+            torch.cumsum(counts[:N], 0, out=pair_ptr[1:])
+        P = int(pair_ptr[-1].item())
+        out = {k: torch.empty(max(P, 1), dtype=torch.float64, device=dev)
+               for k in ("chi2", "avg_tau", "avg_theta", "delta_theta")}
+        tr = None
+        if truth is not None:
+            tr = torch.as_tensor(np.asarray(truth, dtype=np.int64) if not torch.is_tensor(truth) else truth,
+                                 device=dev).to(torch.int64).contiguous()
+            out["truth"] = torch.empty(max(P, 1), dtype=torch.int8, device=dev)
+        err = torch.zeros(1, dtype=torch.int32, device=dev)
+        po = nat.GtfPairOut(vp(out["chi2"]), vp(out["avg_tau"]), vp(out["avg_theta"]), vp(out["delta_theta"]),
+                            vp(out.get("truth")), vp(err))
+        nat.check(self.lib.gtf_updated_state_distances(ctypes.byref(self.cg_sched), ctypes.byref(self.cn),
+                                                       ctypes.byref(self.cuts), ctypes.byref(self.ce), vp(tr),
+                                                       vp(pair_ptr), ctypes.byref(po), self.stream))
+        f = int(err.item())
+        if f:
+            raise ValueError("updated-state distances: " +
+                             "; ".join(m for b, m in nat.ERR_FLAGS.items() if f & b))
+        return pair_ptr, {k: v[:P] for k, v in out.items()}
 
     # ------------------------------------------------------- tag propagation
     def tag_propagation(self, tags, radius, threshold=0.1, max_sweeps=100000):

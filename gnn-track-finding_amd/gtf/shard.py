@@ -107,10 +107,13 @@ class ShardedDeviceGraph:
         self.ranges = up(self.plan.ranges())
         p = d.ptr
         vp = lambda t: ctypes.c_void_p(t.data_ptr() if t.numel() else 0)  # noqa: E731
-        self.cg = nat.GtfGraph(d.n_nodes, d.n_slots, d.n_edges, n_big, p("slot_ptr"), p("slot_src"), p("slot_dst"),
-                               p("out_ptr"), p("out_slot"), p("slot_outpos"), p("is_edge"), p("rev_edge"),
-                               p("solo"), p("gnn"), p("xyzr"), p("layer"), vp(self.sched), *n_g[1:], p("out_dst"),
-                               p("slot_layer"), n_g[0], vp(self.sched_seg))
+        self.cg = nat.GtfGraph(n_nodes=d.n_nodes, n_slots=d.n_slots, n_edges=d.n_edges, n_big=n_big,
+                               slot_ptr=p("slot_ptr"), slot_src=p("slot_src"), slot_dst=p("slot_dst"),
+                               out_ptr=p("out_ptr"), out_slot=p("out_slot"), slot_outpos=p("slot_outpos"),
+                               is_edge=p("is_edge"), rev_edge=p("rev_edge"), solo=p("solo"), gnn=p("gnn"),
+                               xyzr=p("xyzr"), layer=p("layer"), sched=vp(self.sched), n_g4=n_g[0], n_g8=n_g[1],
+                               n_g16=n_g[2], n_g32=n_g[3], n_g64=n_g[4], out_dst=p("out_dst"),
+                               slot_layer=p("slot_layer"), sched_seg=vp(self.sched_seg))
         pl = self.plan
         self.shard = nat.GtfShard(vp(self.senders), int(self.senders.numel()), int(pl.node_lo[rank]),
                                   int(pl.node_hi[rank]), int(pl.slot_lo[rank]), int(pl.slot_hi[rank]))

@@ -183,6 +183,42 @@ def tag_propagation(G, threshold=0.1):
 
 
 # ---------------------------------------------------------------------- I/O
+def updated_state_distances(subGraphs):
+    """calculate_distance_between_updated_track_states.py (:27-104, pair loop :134-195) on
+    the GPU: for every node with an updated_track_states dict and more than one active
+    in-edge, every pair i > j of its entries in dict order. Returns one dict per subgraph,
+    {node: rows}, rows = [(chi2, <tau>, <theta>, delta_theta, truth, neighbour_i,
+    neighbour_j), ...] in the reference's loop order (truth per :190-193 from the nodes'
+    'truth_particle')."""
+    import numpy as np
+    from .device import DeviceGraph
+    g = pack(subGraphs)
+    out = [dict() for _ in subGraphs]
+    if g.n_nodes == 0:
+        return out
+    truth = np.array([G.nodes[n].get("truth_particle", -1) for G in subGraphs for n in G.nodes()], dtype=np.int64)
+    d = DeviceGraph(g)
+    ptr, cols = d.updated_state_distances(truth)
+    ptr = ptr.cpu().numpy()
+    c = {k: v.cpu().numpy() for k, v in cols.items()}
+    S = g.slot
+    node_of = [(si, n) for si, G in enumerate(subGraphs) for n in G.nodes()]
+    for v in np.nonzero(np.diff(ptr) > 0)[0]:
+        lo, hi = int(g.slot_ptr[v]), int(g.slot_ptr[v + 1])
+        keys = sorted((k for k in range(lo, hi) if S["uts_rank"][k] >= 0), key=lambda k: S["uts_rank"][k])
+        si, n = node_of[v]
+        rows = []
+        t = int(ptr[v])
+        for i in range(len(keys)):
+            for j in range(i):
+                rows.append((float(c["chi2"][t]), float(c["avg_tau"][t]), float(c["avg_theta"][t]),
+                             float(c["delta_theta"][t]), int(c["truth"][t]), S["slot_key"][keys[i]],
+                             S["slot_key"][keys[j]]))
+                t += 1
+        out[si][n] = rows
+    return out
+
+
 def read_subgraphs(inputDir: str) -> List:
     """the stages' loader: glob order, pickled nx.DiGraph (== nx.read_gpickle)"""
     out = []

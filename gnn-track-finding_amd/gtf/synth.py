@@ -11,8 +11,8 @@ fused, C4 pileup-200 ~170k hits / ~1M edges) are synthesised:
   fake edges to hits with a nearby azimuth on the same target layer, tuned to
   the committed 800' event's E/N ~ 3.0 (SURVEY §8d);
 * per node the reference's initial state (helper.compute_track_state_estimates
-  math for its first neighbour, helper.py:238-452, vectorised) as the "full
-  load" merged state (every node extrapolates), all edges active,
+  math for its first neighbour with |dr| >= SEED_MIN_DR, helper.py:238-452,
+  vectorised) as the "full load" merged state (every node extrapolates), all edges active,
   track_state_estimates keys = all neighbours with mixture weight 1/degree
   (helper.py:76-96).
 
@@ -165,6 +165,9 @@ def event(seed: int = 0, n_tracks: int = 3300, fake_mean: float = 0.55, drop_tru
     return g
 
 
+SEED_MIN_DR = 5.0   # mm: smallest |r_node - r_neighbour| of a full-load seed pair
+
+
 def _assemble(N, src, dst, x, y, z, r, layer, p) -> TrackGraph:
     E = src.size
     # slots: receiver-major, sorted by sender index
@@ -208,11 +211,18 @@ def _assemble(N, src, dst, x, y, z, r, layer, p) -> TrackGraph:
     slot["tse_mw"] = 1.0 / deg[slot_dst]
     slot["send_mw"] = 1.0 / deg[slot_src]
     slot["tse_xyzr"] = gnn[slot_src]
-    # full load: merged state = initial state towards the node's first neighbour
-    has = deg > 0
-    first_nb = slot_src[np.minimum(slot_ptr[:-1], E - 1)]
+    # full load: merged state = initial state towards the node's first neighbour whose
+    # pair is well conditioned (|dr| >= SEED_MIN_DR): the tau Jacobian goes as 1/dr, so a
+    # near-equal-r pair (steep tracks crossing two endcap disks) gives c22 up to 1e25 and
+    # states the reference's own clustering cannot always process (NaN KL, clustering.py
+    # :116-117). A node without such a neighbour starts without a merged state.
+    ok = np.abs(r[slot_dst] - r[slot_src]) >= SEED_MIN_DR
+    cand = np.where(ok, np.arange(E), E)
+    first_ok = np.minimum.reduceat(np.append(cand, E), np.minimum(slot_ptr[:-1], E)) if E else np.zeros(N, np.int64)
+    has = (deg > 0) & (first_ok < E)
     vv = np.nonzero(has)[0]
-    sv, c5 = _initial_state(gnn[vv], gnn[first_nb[vv]], p)
+    first_nb = slot_src[first_ok[vv]]
+    sv, c5 = _initial_state(gnn[vv], gnn[first_nb], p)
     node["has_merged"][vv] = 1
     node["merged_state"][vv] = sv
     node["merged_cov"][vv] = c5

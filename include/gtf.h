@@ -22,6 +22,8 @@
  *                       (run_gnn_trackml_mod.sh:101,138,112 stage order)
  *   gtf_tag_sweep    -> tag_propagation/tag_propagation.py:137-164 (one sweep)
  *   gtf_tag_prepare  -> tag_propagation/tag_propagation.py:97-110
+ *   gtf_updated_state_distances -> calculate_distance_between_updated_states/
+ *                       calculate_distance_between_updated_track_states.py:27-104,134-195
  */
 #ifndef GTF_H
 #define GTF_H
@@ -35,8 +37,15 @@ extern "C" {
 
 typedef void* gtf_stream_t; /* a hipStream_t */
 
+/* Version of the struct layouts below. gtf_graph carries it with its own size, and every
+ * entry point taking a gtf_graph refuses a caller built against another layout
+ * (status -3, gtf_last_error() names both). Bumped on every layout change. */
+#define GTF_ABI_VERSION 2u
+
 /* ---- graph structure (read-only on the path) ------------------------------ */
 typedef struct gtf_graph {
+    uint32_t struct_size;     /* sizeof(gtf_graph) as the caller compiled it */
+    uint32_t abi_version;     /* GTF_ABI_VERSION */
     int32_t n_nodes;
     int32_t n_slots;          /* slots = (receiver, sender) pairs, receiver-major */
     int32_t n_edges;          /* directed edges = slots with is_edge == 1 */
@@ -145,7 +154,10 @@ enum {
     GTF_ERR_EMPTY_DICT_MW = 16,    /* ZeroDivisionError helper.py:90 */
     GTF_ERR_NAN_KL = 32,           /* ValueError clustering.py:117 (list.index of NaN) */
     GTF_ERR_NO_STATE_DICT = 64,    /* KeyError remove_state_metadata.py:39 */
-    GTF_ERR_SINGULAR_H = 128       /* LinAlgError learn_KL_parabolic_model/.../utils.py:277 (x_B = 0 or x_B = x_0) */
+    GTF_ERR_SINGULAR_H = 128,      /* LinAlgError learn_KL_parabolic_model/.../utils.py:277 (x_B = 0 or x_B = x_0) */
+    GTF_ERR_PAIR_COUNT = 256,      /* pair_ptr disagrees with the state dicts (caller error, a15) */
+    GTF_ERR_NEIGHBOUR_MISSING = 512, /* KeyError calculate_distance_between_updated_track_states.py:182-183 */
+    GTF_ERR_TOO_MANY_STATES = 1024 /* a15: a node with more than 2048 updated states (not processed) */
 };
 
 /* Workspace: caller allocates gtf_workspace_bytes() bytes of device memory. */
@@ -241,6 +253,34 @@ int gtf_tag_prepare(const gtf_graph* g, const double* radius, uint8_t* keep, uin
 /* one Jacobi sweep: tags_out[u] = max(tags_in[u], tags_in[kept neighbours]); flips += changes */
 int gtf_tag_sweep(const gtf_graph* g, const uint8_t* keep, const uint8_t* processed,
                   const int64_t* tags_in, int64_t* tags_out, int32_t* flips, gtf_stream_t stream);
+
+/* ---- Distances between updated track states --------------------
+ * calculate_distance_between_updated_states/calculate_distance_between_updated_track_states.py:
+ * mahalanobis_distance (:27-104) over the pair loop of :134-195. For every node with an
+ * updated_track_states dict (n->has_uts, :143) and more than one active in-edge (:139-140),
+ * every pair i > j of its dict entries in dict order (:174-176): the [a, b] Mahalanobis term
+ * plus the delta-tau term with the hard-coded sigma_z = 0.5 / sigma_r = 0.1, swapped where
+ * |x| >= 600 (:62-74); <tau>, <theta>, delta theta (:89-99); and the truth flag (:190-193).
+ * Coordinates: g->xyzr of the node and of each neighbour (:162-163, :182-183).
+ * Pairs of node v are written at [pair_ptr[v] + t], t = i (i - 1) / 2 + j (the reference's
+ * loop order). gtf_updated_state_pair_counts writes each node's pair count (0 or d(d-1)/2)
+ * for the caller's exclusive scan into pair_ptr [N+1]; a node whose pair_ptr range has
+ * another size is skipped with GTF_ERR_PAIR_COUNT. Uses g->sched when present. */
+typedef struct gtf_pair_out {
+    double* chi2;         /* [P] */
+    double* avg_tau;      /* [P] or NULL */
+    double* avg_theta;    /* [P] or NULL */
+    double* delta_theta;  /* [P] or NULL */
+    int8_t* truth;        /* [P] or NULL (needs node truth) */
+    uint32_t* err;        /* device error word (GTF_ERR_PAIR_COUNT / _NEIGHBOUR_MISSING / _TOO_MANY_STATES) or NULL */
+} gtf_pair_out;
+
+int gtf_updated_state_pair_counts(const gtf_graph* g, const gtf_nodes* n, const gtf_states* uts, const gtf_edges* e,
+                                  int64_t* counts, gtf_stream_t stream);
+/* truth: [N] truth_particle per node (device), or NULL */
+int gtf_updated_state_distances(const gtf_graph* g, const gtf_nodes* n, const gtf_states* uts, const gtf_edges* e,
+                                const int64_t* truth, const int64_t* pair_ptr, const gtf_pair_out* out,
+                                gtf_stream_t stream);
 
 /* ---- Initial track-state estimates -----------------------------
  * helper.compute_track_state_estimates (helper.py:238-452): for every key of every

@@ -412,6 +412,46 @@ def mahalanobis_distance_updated(mean1, cov1, mean2, cov2, node_coords, n1, n2):
     return distance1 + distance2, (tau1 + tau2) / 2, (theta1 + theta2) / 2, theta1 - theta2
 
 
+def updated_state_pairs(g: TrackGraph, truth=None):
+    """a15 pair loop (calculate_distance_between_updated_track_states.py:134-195): for every
+    node with an updated_track_states dict (:143) and more than one active in-edge
+    (:139-140), every pair i > j of the dict's entries in dict order (:174-176), with the
+    node's and the neighbours' node attribute xyzr (:162-163, :182-183) and the pair truth
+    flag (:190-193). Returns pair_ptr [N+1] and a dict of per-pair arrays."""
+    S = g.slot
+    sp = g.slot_ptr
+    ptr = np.zeros(g.n_nodes + 1, np.int64)
+    cols = {"chi2": [], "avg_tau": [], "avg_theta": [], "delta_theta": [], "truth": []}
+    for v in range(g.n_nodes):
+        lo, hi = sp[v], sp[v + 1]
+        nact = int(np.sum((S["is_edge"][lo:hi] == 1) & (S["act"][lo:hi] == 1)))
+        n = 0
+        if g.node["has_uts"][v] == 1 and nact > 1:
+            keys = _dict_order(g, "uts", v)
+            for i in range(len(keys)):
+                for j in range(i):
+                    ki, kj = keys[i], keys[j]
+                    ui, uj = S["slot_src"][ki], S["slot_src"][kj]
+                    if ui < 0 or uj < 0:
+                        raise ReferenceError_("KeyError: neighbour not in the subgraph (:182-183)")
+                    mi = np.array([S["uts_sv"][ki][0], S["uts_sv"][ki][1], S["uts_tau"][ki]])
+                    mj = np.array([S["uts_sv"][kj][0], S["uts_sv"][kj][1], S["uts_tau"][kj]])
+                    r = mahalanobis_distance_updated(mi, mat_from_cov5(S["uts_cov"][ki]), mj,
+                                                     mat_from_cov5(S["uts_cov"][kj]), g.node["xyzr"][v],
+                                                     g.node["xyzr"][ui], g.node["xyzr"][uj])
+                    for c, x in zip(("chi2", "avg_tau", "avg_theta", "delta_theta"), r):
+                        cols[c].append(x)
+                    t = 0
+                    if truth is not None:
+                        t = int(truth[v] == truth[ui] and truth[ui] == truth[uj] and truth[v] == truth[uj])
+                    cols["truth"].append(t)
+                    n += 1
+        ptr[v + 1] = ptr[v] + n
+    out = {k: np.array(x, np.float64) for k, x in cols.items() if k != "truth"}
+    out["truth"] = np.array(cols["truth"], np.int8)
+    return ptr, out
+
+
 def KLDistance(mean1, cov1, mean2, cov2):                                        # clustering.py:90-94
     inv1 = np.linalg.inv(cov1)
     inv2 = np.linalg.inv(cov2)

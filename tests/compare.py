@@ -4,6 +4,8 @@ Integer / flag / index outputs must match exactly (activation masks, ranks =
 dict membership and order, degree, merged flags). Floats are compared with a
 relative tolerance, only where the entry exists (rank >= 0 / has_merged).
 """
+import hashlib
+
 import numpy as np
 
 INT_NODE = ["has_merged", "has_uts", "degree"]
@@ -283,3 +285,14 @@ def compare_noise(got, ref, noise, flips, rtol=1e-6, k=100.0):
             errs.append("%s.%s: %d beyond rtol+noise, e.g. %d got %s exp %s noise %s" % (
                 kind, f, bad.size, bad[0], a[bad[0]], b[bad[0]], nz[bad[0]]))
     return errs, stats
+
+
+def input_sha(g):
+    """SHA-256 of a generated event's structure and of the inputs the pass reads (pins a
+    full-size digest to the generator output it was made from)"""
+    h = hashlib.sha256()
+    for a in (g.slot_ptr, g.out_ptr, g.out_slot, g.slot["slot_src"], g.node["gnn"], g.node["xyzr"],
+              g.node["merged_state"], g.node["merged_cov"], g.node["has_merged"], g.slot["send_mw"],
+              g.slot["tse_rank"], g.node["layer"]):
+        h.update(np.ascontiguousarray(a).tobytes())
+    return h.hexdigest()

@@ -45,7 +45,7 @@ def test_struct_layout_matches_header():
           "gtf_edges": nat.GtfEdges, "gtf_params": nat.GtfParams, "gtf_kl_graph": nat.GtfKlGraph, "gtf_tse_extra": nat.GtfTseExtra, "gtf_shard": nat.GtfShard,
           "gtf_extract_params": nat.GtfExtractParams, "gtf_extract_io": nat.GtfExtractIO,
           "gtf_kl_out": nat.GtfKlOut, "gtf_event_csr": nat.GtfEventCsr,
-          "gtf_candidate_graph": nat.GtfCandidateGraph}
+          "gtf_candidate_graph": nat.GtfCandidateGraph, "gtf_pair_out": nat.GtfPairOut}
     lines = []
     for t, cls in py.items():
         lines += ['  printf("%s.%s %%zu\\n", offsetof(%s, %s));' % (t, f, t, f) for f, _ in cls._fields_]
@@ -75,3 +75,28 @@ def test_no_fallback_without_library(monkeypatch, tmp_path):
     monkeypatch.setattr(_native, "_lib", None)
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         _native.lib()
+
+
+def test_graph_struct_carries_abi_version():
+    """gtf_graph starts with its size and GTF_ABI_VERSION; the ctypes mirror fills both"""
+    from gtf import _native as nat
+    ver = re.search(r"#define GTF_ABI_VERSION (\d+)u", open(HDR).read())
+    assert ver and int(ver.group(1)) == nat.ABI_VERSION
+    g = nat.GtfGraph(n_nodes=3)
+    assert g.struct_size == ctypes.sizeof(nat.GtfGraph) and g.abi_version == nat.ABI_VERSION
+    assert nat.GtfGraph.struct_size.offset == 0 and nat.GtfGraph.abi_version.offset == 4
+
+
+def test_abi_mismatch_is_refused_without_a_gpu():
+    """a gtf_graph of another layout is refused (-3) before any device work"""
+    from gtf import _native as nat
+    if not os.path.exists(nat.LIB_PATH):
+        pytest.skip("libgtf.so not built")
+    L = nat.lib()
+    g = nat.GtfGraph(n_nodes=0)
+    g.abi_version = nat.ABI_VERSION + 1
+    cnt = ctypes.c_int64(0)
+    z = ctypes.c_void_p(0)
+    rc = L.gtf_updated_state_pair_counts(ctypes.byref(g), ctypes.byref(nat.GtfNodes()), ctypes.byref(nat.GtfStates()),
+                                         ctypes.byref(nat.GtfEdges()), ctypes.byref(cnt), z)
+    assert rc == -3 and b"ABI mismatch" in L.gtf_last_error()

@@ -92,3 +92,20 @@ def test_track_state_estimates_full_vol7():
         assert np.allclose(a, b, rtol=RTOL, atol=0, equal_nan=True), f
     for k in ("xy_mean_var", "zr_mean_var", "angle_of_rotation", "translation"):
         assert np.allclose(node[k], extra[k], rtol=RTOL, atol=0, equal_nan=True), k
+
+
+@pytest.mark.parametrize("name", ["extrapolate_full", "pass_full"])
+def test_updated_state_pairs_a15(name):
+    """a15 (calculate_distance_between_updated_track_states.py:27-104, pair loop :134-195)
+    against the reference's own function run on the same states (make_golden_a15.py)"""
+    import os
+    from fixtures import GOLDEN
+    z = np.load(os.path.join(GOLDEN, "a15_pairs.npz"), allow_pickle=False)
+    g, out, _, _ = load(name)
+    e = expected_graph(g, out)
+    ptr, got = O.updated_state_pairs(e, z[name + "__node_truth"])
+    assert np.array_equal(ptr, z[name + "__pair_ptr"])
+    assert ptr[-1] > 1000
+    for c in ("chi2", "avg_tau", "avg_theta", "delta_theta"):
+        np.testing.assert_allclose(got[c], z[name + "__" + c], rtol=RTOL, atol=1e-300, err_msg=c)
+    assert np.array_equal(got["truth"], z[name + "__truth"])

@@ -146,16 +146,17 @@ NODE_KERNEL = "k_node_multi<update+cluster> (KL-distance kernel)"
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_v10", "pmc_c4.json")
 
 
-def committed_traffic(workload, kernel):
+def committed_traffic(workload, kernel, layout, tile):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
     (separate FETCH_SIZE / WRITE_SIZE passes, tools/gpu_profile.sh; corrections in
-    DESIGN.md), or None when no summary matches this workload/kernel."""
+    DESIGN.md), or None when no summary matches this workload / node layout / tile /
+    kernel (traffic depends on the layout: 318 vs 201 MB for the node kernel)."""
     try:
         with open(PMC_SUMMARY) as f:
             s = json.load(f)
     except OSError:
         return None
-    if s.get("workload") != workload:
+    if s.get("workload") != workload or s.get("layout") != layout or s.get("tile") != tile:
         return None
     k = s.get("kernels", {}).get(kernel)
     return None if k is None else k.get("hbm_bytes_per_launch")
@@ -251,9 +252,8 @@ def main():
     # eligible nodes of the KL clustering (3 <= |updated_track_states| <= 15), from the
     # state after a pass (clustering does not change dict membership)
     sp = d.slot_ptr_host   # device order
-    nst = np.add.reduceat((d.t["uts_rank"] >= 0).to(torch.int32).cpu().numpy(), sp[:-1]) \
-        if g.n_slots else np.zeros(0)
-    nst = np.where(np.diff(sp) > 0, nst, 0)
+    owner = np.repeat(np.arange(g.n_nodes), np.diff(sp))
+    nst = np.bincount(owner, weights=(d.t["uts_rank"] >= 0).cpu().numpy(), minlength=g.n_nodes)
     elig = (nst >= 3) & (nst <= 15) & (d.t["has_uts"].cpu().numpy() == 1)
     e_elig = int(np.diff(sp)[elig].sum())
     kern = {
@@ -270,9 +270,9 @@ def main():
     per_kernel = {k: {"ms": round(v[0], 5), "algorithmic_bytes": v[1],
                       "achieved_GBps": v[1] / (v[0] * 1e-3) / 1e9,
                       "frac": v[1] / (v[0] * 1e-3) / 1e9 / rf.HBM_PEAK_GBS,
-                      "traffic_bytes": committed_traffic(args.workload, k)} for k, v in cands.items()}
+                      "traffic_bytes": committed_traffic(args.workload, k, args.layout, args.tile)} for k, v in cands.items()}
     achieved = nbytes / (ms * 1e-3) / 1e9
-    traffic = committed_traffic(args.workload, name)
+    traffic = committed_traffic(args.workload, name, args.layout, args.tile)
 
     sharded = None
     if world > 1 and not args.no_sharded:
@@ -323,9 +323,14 @@ def main():
         }
         if cpu:
             out["speedup_vs_cpu"] = out["value"] / cpu["value"]
+        if flags:
+            # the reference raises on this input (GTF_ERR_*): the timed pass has no reference answer
+            out["invalid"] = "device_error_flags %d: the reference raises on this input" % flags
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()
+    if flags:
+        sys.exit(3)
 
 
 if __name__ == "__main__":

@@ -1,6 +1,6 @@
 """Summarise rocprofv3 FETCH_SIZE / WRITE_SIZE passes into profiles/<round>_pmc/.
 
-    python tools/pmc_summary.py PROFDIR CALIBDIR OUT.json [workload]
+    python tools/pmc_summary.py PROFDIR CALIBDIR OUT.json [workload [layout [tile]]]
 
 PROFDIR holds fetch/ and write/ counter passes of bench.py (tools/gpu_profile.sh);
 CALIBDIR the same two passes of tools/calib_fetch (kernels that stream exactly
@@ -39,6 +39,8 @@ def load(path):
 def main():
     prof, calib, out = sys.argv[1:4]
     workload = sys.argv[4] if len(sys.argv) > 4 else "c4"
+    layout = sys.argv[5] if len(sys.argv) > 5 else "tiled"
+    tile = int(sys.argv[6]) if len(sys.argv) > 6 else 4096
     cf, cw = load(calib + "/fetch/run_counter_collection.csv"), load(calib + "/write/run_counter_collection.csv")
     gib = float(1 << 30)
     read_factor = {k: gib / (cf[k] * 1024) for k in ("rd1", "rd8", "rd16") if k in cf}
@@ -53,7 +55,7 @@ def main():
     if "k_sender" in ks and "k_extrapolate" in ks:
         ks["k_sender+k_extrapolate"] = {"hbm_bytes_per_launch": ks["k_sender"]["hbm_bytes_per_launch"] +
                                         ks["k_extrapolate"]["hbm_bytes_per_launch"]}
-    res = {"workload": workload, "read_factor_applied": rf, "write_factor_applied": write_factor,
+    res = {"workload": workload, "layout": layout, "tile": tile, "read_factor_applied": rf, "write_factor_applied": write_factor,
            "calibration_bytes_per_FETCH_KiB": {k: v for k, v in read_factor.items()},
            "note": "FETCH_SIZE/WRITE_SIZE in KiB per launch (median over launches); hbm bytes = "
                    "FETCH*1024*read_factor + WRITE*1024*write_factor, factors measured by tools/calib_fetch",

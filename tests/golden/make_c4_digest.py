@@ -6,7 +6,7 @@ The oracle (oracle/gtf_oracle.py, itself pinned to the reference's own outputs b
 tests/test_oracle_golden.py) runs the fused pass -- extrapolate stage, update stage,
 clustering on updated_track_states (oracle.full_pass, run_gnn_trackml_mod.sh:101,138,112
 order) -- on the seeded C4 event (gtf.synth.workload("c4", seed=0): 179,788 hits,
-1,023,954 directed edges), and three more times with the continuous inputs scaled by
+1,027,548 directed edges), and three more times with the continuous inputs scaled by
 (1 + U(-2^-46, 2^-46)) (tests/compare.py noise_envelope). The full outputs are ~100 MB,
 so the committed file holds a digest (< 2 MB):
 

@@ -4,9 +4,9 @@ states.py:27-104 over the pair loop :134-195) against
   * the reference's own mahalanobis_distance run on the committed volume-7 states
     (tests/golden/a15_pairs.npz, tests/golden/make_golden_a15.py): pair layout and truth
     flags exact, floats within 1e-6 relative;
-  * the oracle (oracle.updated_state_pairs) on the states the HIP pass leaves on a
-    seeded synthetic event with hub nodes beyond 64 slots (the one-wavefront path):
-    same inputs, so within 1e-12.
+  * the oracle (oracle.updated_state_pairs) on the states the HIP extrapolation leaves on
+    a seeded synthetic event whose hub nodes carry > 64 dict entries (the one-wavefront
+    path): same inputs, so within 1e-12.
 """
 import os
 
@@ -15,7 +15,6 @@ import pytest
 
 import gtf_oracle as O
 from fixtures import GOLDEN, load, expected_graph
-from gtf import synth
 from gtf.params import Params
 
 pytestmark = pytest.mark.gpu
@@ -45,22 +44,52 @@ def test_a15_matches_reference_pairs(name):
     assert np.array_equal(got["truth"], z[name + "__truth"])
 
 
-def test_a15_matches_oracle_after_a_pass_with_hubs():
+def _hub_states(seed=5):
+    """a synthetic event with 4 hub hits (> 64 slots each) after the HIP extrapolation
+    stage, with every slot of each hub turned into an active edge holding an
+    updated_track_states entry (random dict order, states drawn around the event's own
+    entries, SPD covariances): > 64 dict entries per hub, so the pair kernel's
+    one-wavefront path and its dict-position map carry thousands of pairs."""
     from gtf.device import DeviceGraph
-    g = synth.event(seed=5, n_tracks=1500, fake_mean=synth.C4_FAKE)
+    from test_gpu_edges import hub_event
+    g = hub_event(seed=seed, n_tracks=1500, n_hubs=4)
     d = DeviceGraph(g)
-    d.full_pass(Params())
+    d.extrapolate(Params())
     g = d.download(g.copy())
-    deg = np.diff(g.slot_ptr)
-    assert deg.max() > 64, "the event should hold hub nodes (one-wavefront path)"
-    truth = np.random.default_rng(0).integers(0, 50, g.n_nodes)
+    rng = np.random.default_rng(seed)
+    S = g.slot
+    have = np.nonzero(S["uts_rank"] >= 0)[0]
+    hubs = np.nonzero(np.diff(g.slot_ptr) > 64)[0]
+    assert hubs.size >= 3 and have.size > 100
+    for v in hubs:
+        lo, hi = int(g.slot_ptr[v]), int(g.slot_ptr[v + 1])
+        ks = np.arange(lo, hi)[S["slot_src"][lo:hi] >= 0]
+        S["is_edge"][ks] = 1
+        S["act"][ks] = 1
+        S["uts_rank"][lo:hi] = -1
+        S["uts_rank"][ks] = rng.permutation(ks.size)
+        src = rng.choice(have, ks.size)
+        S["uts_sv"][ks] = S["uts_sv"][src] * (1 + 1e-3 * rng.standard_normal((ks.size, 3)))
+        S["uts_tau"][ks] = S["uts_tau"][src] + 1e-3 * rng.standard_normal(ks.size)
+        a, c = rng.uniform(1e-4, 1e-2, (2, ks.size))
+        b = rng.uniform(-0.5, 0.5, ks.size) * np.sqrt(a * c)
+        S["uts_cov"][ks] = np.stack([a, b, b, c, rng.uniform(1e-4, 1e-2, ks.size)], axis=1)
+        g.node["has_uts"][v] = 1
+    return g, hubs
+
+
+def test_a15_matches_oracle_with_hubs():
+    g, hubs = _hub_states()
+    truth = np.random.default_rng(0).integers(0, 3, g.n_nodes)
     ptr, got = _gpu(g, truth)
     ref_ptr, ref = O.updated_state_pairs(g, truth)
     assert np.array_equal(ptr, ref_ptr)
-    assert ptr[-1] > 10000
+    per_node = np.diff(ptr)
+    assert per_node[hubs].min() > 64 * 63 // 2 and ptr[-1] > 10000
     for c in COLS:
-        np.testing.assert_allclose(got[c], ref[c], rtol=1e-12, atol=1e-15, err_msg=c)
+        np.testing.assert_allclose(got[c], ref[c], rtol=1e-10, atol=1e-15, err_msg=c)
     assert np.array_equal(got["truth"], ref["truth"])
+    assert got["truth"].sum() > 0
 
 
 def test_a15_dropin_cli(tmp_path):

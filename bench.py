@@ -143,20 +143,22 @@ def bench_sharded(workload, rank, world, dev, steps, warmup, params):
 # the fused node kernel: priors, side norm, reweights, update and KL clustering of every
 # receiver in one launch (gtf_pass.hip run_pass)
 NODE_KERNEL = "k_node_multi<update+cluster> (KL-distance kernel)"
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_v10", "pmc_c4.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02_v0", "pmc_c4.json")
 
 
-def committed_traffic(workload, kernel, layout, tile):
+def committed_traffic(workload, kernel, layout, tile, edges, nodes):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary
     (separate FETCH_SIZE / WRITE_SIZE passes, tools/gpu_profile.sh; corrections in
     DESIGN.md), or None when no summary matches this workload / node layout / tile /
-    kernel (traffic depends on the layout: 318 vs 201 MB for the node kernel)."""
+    kernel (traffic depends on the layout: 318 vs 201 MB for the node kernel) / event size."""
     try:
         with open(PMC_SUMMARY) as f:
             s = json.load(f)
     except OSError:
         return None
     if s.get("workload") != workload or s.get("layout") != layout or s.get("tile") != tile:
+        return None
+    if s.get("edges") != edges or s.get("nodes") != nodes:   # another generator's event
         return None
     k = s.get("kernels", {}).get(kernel)
     return None if k is None else k.get("hbm_bytes_per_launch")
@@ -270,9 +272,9 @@ def main():
     per_kernel = {k: {"ms": round(v[0], 5), "algorithmic_bytes": v[1],
                       "achieved_GBps": v[1] / (v[0] * 1e-3) / 1e9,
                       "frac": v[1] / (v[0] * 1e-3) / 1e9 / rf.HBM_PEAK_GBS,
-                      "traffic_bytes": committed_traffic(args.workload, k, args.layout, args.tile)} for k, v in cands.items()}
+                      "traffic_bytes": committed_traffic(args.workload, k, args.layout, args.tile, g.n_edges, g.n_nodes)} for k, v in cands.items()}
     achieved = nbytes / (ms * 1e-3) / 1e9
-    traffic = committed_traffic(args.workload, name, args.layout, args.tile)
+    traffic = committed_traffic(args.workload, name, args.layout, args.tile, g.n_edges, g.n_nodes)
 
     sharded = None
     if world > 1 and not args.no_sharded:

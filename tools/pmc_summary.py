@@ -55,7 +55,16 @@ def main():
     if "k_sender" in ks and "k_extrapolate" in ks:
         ks["k_sender+k_extrapolate"] = {"hbm_bytes_per_launch": ks["k_sender"]["hbm_bytes_per_launch"] +
                                         ks["k_extrapolate"]["hbm_bytes_per_launch"]}
-    res = {"workload": workload, "layout": layout, "tile": tile, "read_factor_applied": rf, "write_factor_applied": write_factor,
+    # the event the counters were taken on: bench.py's own line in the trace pass
+    edges = nodes = None
+    try:
+        for ln in open(prof + "/trace.log"):
+            if ln.startswith("{"):
+                c = json.loads(ln)["config"]
+                edges, nodes = c.get("directed_edges_per_gpu"), c.get("nodes_per_gpu")
+    except (OSError, ValueError, KeyError):
+        pass
+    res = {"workload": workload, "layout": layout, "tile": tile, "edges": edges, "nodes": nodes, "read_factor_applied": rf, "write_factor_applied": write_factor,
            "calibration_bytes_per_FETCH_KiB": {k: v for k, v in read_factor.items()},
            "note": "FETCH_SIZE/WRITE_SIZE in KiB per launch (median over launches); hbm bytes = "
                    "FETCH*1024*read_factor + WRITE*1024*write_factor, factors measured by tools/calib_fetch",

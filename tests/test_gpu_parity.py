@@ -56,6 +56,14 @@ def test_cluster_tse():
     _run("cluster_tse", lambda d, p, m: d.cluster("tse", m["chi2"], m["kl"], p))
 
 
+def test_cluster_tie():
+    """the reference's own clustering on non-emptying ties (make_golden_tie.py)"""
+    got = _run("cluster_tie", lambda d, p, m: d.cluster("tse", m["chi2"], m["kl"], p))
+    _, _, extra, _ = load("cluster_tie")
+    tied = np.isin(got.node["node_id"], extra["tie_nodes"])
+    assert tied.sum() >= 20 and got.node["has_merged"][tied].sum() >= 15
+
+
 def test_cluster_uts():
     _run("cluster_uts", lambda d, p, m: d.cluster("uts", m["chi2"], m["kl"], p))
 

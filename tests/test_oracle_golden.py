@@ -51,6 +51,20 @@ def test_cluster_tse():
     assert compare(g, exp, rtol=RTOL) == []
 
 
+def test_cluster_tie():
+    """non-emptying np.where ties, made and clustered by the reference (make_golden_tie.py):
+    the merged pair is (rows[0], rows[1]) and every listed index is removed"""
+    g, out, extra, meta = load("cluster_tie")
+    exp = expected_graph(g, out)
+    assert extra["tie_nodes"].size >= 20
+    O.cluster_stage(g, "tse", meta["chi2"], meta["kl"], _params(meta))
+    assert compare(g, exp, rtol=RTOL) == []
+    ids = g.node["node_id"]
+    tied = np.isin(ids, extra["tie_nodes"])
+    # a tie whose chi2 is above the threshold (-c 1.0) merges nothing (clustering.py:228)
+    assert tied.sum() == extra["tie_nodes"].size and g.node["has_merged"][tied].sum() >= 15
+
+
 def test_cluster_uts():
     g, out, _, meta = load("cluster_uts")
     exp = expected_graph(g, out)

@@ -43,8 +43,21 @@ sys.path[:0] = [os.path.join(ROOT, "gnn-track-finding_amd"), os.path.join(ROOT, 
 import numpy as np  # noqa: E402
 
 
+def cpu_model():
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(n_tracks, params):
-    """NumPy restatement of the pass on a bounded sample (1 core)."""
+    """BASELINE.md plan item 1, the headline denominator: the NumPy restatement of the pass
+    (oracle.full_pass, the reference's own NumPy calls) on 1 core, on a bounded sample of
+    the same generator (~10 s). Its rate is per edge and roughly size independent: the
+    full C4 pass takes ~180 s (tests/golden/make_c4_digest.py)."""
     import gtf_oracle as O
     from gtf import synth
     g = synth.event(seed=12345, n_tracks=n_tracks, fake_mean=synth.C4_FAKE)
@@ -54,6 +67,100 @@ def cpu_baseline(n_tracks, params):
     return {"value": g.n_edges / dt, "unit": "edges/s", "cores": 1, "kind": "port",
             "sample": "oracle/gtf_oracle.full_pass (NumPy restatement) on one synthetic event of %d hits / "
                       "%d directed edges (pileup-200 density), %.1f s" % (g.n_nodes, g.n_edges, dt)}
+
+
+def cpu_baseline_cpp(g, params, reps=5):
+    """BASELINE.md plan item 2: the C++ fp64 restatement (oracle/cpu_ref.cpp, OpenMP over
+    senders and receivers) on the benchmark event itself, 1 core and every core of this
+    process's share (OMP_NUM_THREADS, else os.cpu_count()); warm passes, median of reps."""
+    import cpu_ref
+    if not os.path.exists(cpu_ref.LIB):
+        return {"error": "oracle/build/libcpuref.so not built"}
+    allc = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    out = {"unit": "edges/s", "kind": "port", "cpu_model": cpu_model(), "nproc": os.cpu_count(),
+           "sample": "oracle/cpu_ref.cpp full pass on the whole bench event (%d directed edges), median of %d "
+                     "warm passes" % (g.n_edges, reps)}
+    for label, th in (("1_core", 1), ("all_cores", allc)):
+        ts = []
+        for _ in range(reps + 1):
+            h = g.copy()
+            b = cpu_ref.Bound(h)
+            cp = cpu_ref.params(params)
+            import ctypes
+            t0 = time.perf_counter()
+            flags = cpu_ref.lib().cr_full_pass(ctypes.byref(b.c), ctypes.byref(cp), th)
+            ts.append(time.perf_counter() - t0)
+        dt = float(np.median(ts[1:]))
+        out[label] = {"value": g.n_edges / dt, "cores": th, "s_per_pass": dt, "flags": int(flags)}
+    return out
+
+
+def dropin_input_vol7(params):
+    """The reference-schema full-load network of the committed volume-7 134 event: the
+    event conversion (event_conversion.py:53-101: construct_graph, weakly connected
+    subgraphs, TSE, activation, priors, weights, degree) through the drop-in modules, then
+    every node's merged state = a copy of its first TSE entry (SURVEY §8d full load)."""
+    import numpy as np_
+    from gtf import io, stages as st
+    kat = os.path.join(ROOT, "tests", "golden", "kat134")
+    subs = io.build_networkx(os.path.join(kat, "event_1_filtered_graph_"), 7, 7, os.path.join(kat, "truth_vol7.csv"))
+    subs = st.compute_track_state_estimates(subs, params.sigma0xy, params.sigma0rz, params.sigma0rz2,
+                                            params.endcap_boundary)
+    for s in subs:
+        for e in s.edges:
+            s.edges[e]["activated"] = 1
+    st.compute_prior_probabilities(subs, "track_state_estimates")
+    st.compute_mixture_weights(subs, "track_state_estimates")
+    st.node_degrees(subs)
+    for s in subs:
+        for n in s.nodes:
+            tse = s.nodes[n]["track_state_estimates"]
+            if tse:
+                first = next(iter(tse.values()))
+                s.nodes[n]["merged_state"] = np_.array(first["edge_state_vector"], dtype=float).copy()
+                s.nodes[n]["merged_cov"] = np_.array(first["edge_covariance"], dtype=float).copy()
+                s.nodes[n]["merged_prior"] = first.get("prior", 1.0)
+    return subs
+
+
+def dropin_stage_wall(params, reps=3):
+    """the drop-in stage wall time, gpickle in -> gpickle out, of the
+    extrapolation stage (extrapolate_merged_states.py:521-572's main body through the
+    drop-in module: read every subgraph, message passing + priors / reweight x2 + degree
+    on the GPU, write every subgraph), in process (interpreter start excluded), on the
+    full-load volume-7 134 network (14,766 directed edges); median of reps. BASELINE.md
+    times the reference's own stage on this input at 788 edges/s as is (18.7 s) and
+    5,367 edges/s with its prints stubbed."""
+    import shutil
+    import tempfile
+    from gtf import stages as st
+    graphs = dropin_input_vol7(params)
+    tmp = tempfile.mkdtemp(prefix="gtf_dropin_")
+    try:
+        ind, outd = os.path.join(tmp, "in") + "/", os.path.join(tmp, "out") + "/"
+        os.makedirs(ind)
+        os.makedirs(outd)
+        for i, s in enumerate(graphs):
+            st.save_network(ind, i, s)
+        ts, tk = [], []
+        for _ in range(reps + 1):
+            t0 = time.perf_counter()
+            subs = st.read_subgraphs(ind)
+            t1 = time.perf_counter()
+            st.extrapolate_stage(subs, params)
+            t2 = time.perf_counter()
+            for i, s in enumerate(subs):
+                st.save_network(outd, i, s)
+            ts.append(time.perf_counter() - t0)
+            tk.append(t2 - t1)
+        edges = sum(s.number_of_edges() for s in graphs)
+        dt = float(np.median(ts[1:]))
+        return {"stage": "extrapolate (drop-in main body, in process)", "input": "vol-7 134 full load",
+                "subgraphs": len(graphs), "edges": edges, "wall_s": dt, "edges_per_s": edges / dt,
+                "stage_call_s": float(np.median(tk[1:])),
+                "reference_as_is_edges_per_s": 788, "reference_prints_stubbed_edges_per_s": 5367}
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
 
 
 def bench_c5(dev, steps, warmup, n_events=256):
@@ -173,6 +280,7 @@ def main():
     ap.add_argument("--cpu-tracks", type=int, default=4000, help="CPU-baseline sample size (tracks)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-c5", action="store_true", help="skip the config-5 parabolic-KL section")
+    ap.add_argument("--no-dropin", action="store_true", help="skip the drop-in stage wall time")
     ap.add_argument("--no-sharded", action="store_true", help="skip the single-event sharded section (N > 1)")
     ap.add_argument("--layout", default="tiled", choices=["tiled", "schedule", "natural"],
                     help="device node order (DeviceGraph layout)")
@@ -287,9 +395,12 @@ def main():
     if rank == 0 and world == 1 and not args.no_c5:
         c5 = bench_c5(dev, K, W)
 
-    cpu = None
+    cpu = cpu_cpp = dropin = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(args.cpu_tracks, p)
+        cpu_cpp = cpu_baseline_cpp(g, p)
+    if rank == 0 and world == 1 and not args.no_dropin:
+        dropin = dropin_stage_wall(p)
 
     if rank == 0:
         out = {
@@ -319,12 +430,16 @@ def main():
                          "algorithmic_bytes_per_launch": nbytes, "kernel_ms": ms,
                          "kl_eligible_nodes": int(elig.sum()), "kl_eligible_in_edges": e_elig},
             "cpu_baseline": cpu,
+            "cpu_baseline_cpp": cpu_cpp,
+            "dropin_stage": dropin,
             "device_error_flags": flags,
             "c5_parabolic_kl": c5,
             "sharded_single_event": sharded,
         }
         if cpu:
             out["speedup_vs_cpu"] = out["value"] / cpu["value"]
+        if cpu_cpp and "all_cores" in cpu_cpp:
+            out["speedup_vs_cpp_all_cores"] = out["value"] / cpu_cpp["all_cores"]["value"]
         if flags:
             # the reference raises on this input (GTF_ERR_*): the timed pass has no reference answer
             out["invalid"] = "device_error_flags %d: the reference raises on this input" % flags

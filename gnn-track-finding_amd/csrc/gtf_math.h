@@ -1,7 +1,8 @@
 // gtf_math.h -- fp64 small-matrix arithmetic of the track-finding pass, written
 // in the operation order of the reference's NumPy expressions so that results
 // track the CPU path to the last few ulps (built with -ffp-contract=off: no
-// fused multiply-add where the reference has separate roundings).
+// fused multiply-add where the reference has separate roundings, and an explicit
+// fma() exactly where numpy's BLAS / LAPACK kernels fuse, see below).
 //
 // Covariances on the path are block diagonal [[c00 c01 0][c10 c11 0][0 0 c22]]
 // (the reference zeroes row/col 2 of every stored state covariance:
@@ -75,10 +76,20 @@ struct Cov5 {
     double c00, c01, c10, c11, c22;
 };
 
+// numpy's small products go through OpenBLAS (0.3.29, x86-64 FMA kernels), whose
+// rounding the reference's values carry; these helpers reproduce it bit for bit
+// (checked against numpy on random operands, tests/test_numpy_rounding.py):
+//   x @ y (1-D, ddot)           s = x0*y0; s = fma(x1, y1, s); s = fma(x2, y2, s) ...
+//   A @ x (gemv_n, 3x3)         s = A_i1*x1; s = fma(A_i0, x0, s); s = fma(A_i2, x2, s)
+//   x @ A (gemv_t)              s = x0*A_0j; s = fma(x1, A_1j, s); s = fma(x2, A_2j, s)
+//   A @ B, A @ B.T (gemm, 3x3)  s = A_i0*B_0j; s = fma(A_i1, B_1j, s); s = fma(A_i2, B_2j, s)
+// Exact zeros of block-diagonal operands add exact zeros and are skipped.
+
 // 2x2 inverse the way np.linalg.inv gets it from OpenBLAS (dgesv = getf2 LU with
-// partial pivoting, then triangular solves): the pivot and u22 are inverted once
-// and multiplied (getf2 scales by 1/pivot, the trsm kernels store the inverted
-// diagonal), so each inverse costs two divisions.
+// partial pivoting, then triangular solves): the pivot and u22 are inverted once and
+// multiplied (getf2 scales by 1/pivot, the trsm kernels store the inverted diagonal),
+// and the back substitution's update is one fused multiply-add (trsm kernel
+// c -= b * a), so each inverse costs two divisions.
 __device__ __forceinline__ void inv2(double a, double b, double c, double d, double& i00, double& i01,
                                      double& i10, double& i11) {
     const bool sw = fabs(c) > fabs(a);
@@ -90,9 +101,9 @@ __device__ __forceinline__ void inv2(double a, double b, double c, double d, dou
     const double ru = 1.0 / u22;
     // columns of P*I: e0 -> (sw ? (0,1) : (1,0)), e1 -> (sw ? (1,0) : (0,1))
     const double y0a = sw ? 0.0 : 1.0, y1a = (sw ? 1.0 : 0.0) - l * y0a;
-    const double x1a = y1a * ru, x0a = (y0a - p1 * x1a) * rp;
+    const double x1a = y1a * ru, x0a = fma(-x1a, p1, y0a) * rp;
     const double y0b = sw ? 1.0 : 0.0, y1b = (sw ? 0.0 : 1.0) - l * y0b;
-    const double x1b = y1b * ru, x0b = (y0b - p1 * x1b) * rp;
+    const double x1b = y1b * ru, x0b = fma(-x1b, p1, y0b) * rp;
     i00 = x0a; i10 = x1a; i01 = x0b; i11 = x1b;
 }
 
@@ -107,10 +118,10 @@ __device__ __forceinline__ Cov5 add_cov5(const Cov5& a, const Cov5& b) {
     return Cov5{a.c00 + b.c00, a.c01 + b.c01, a.c10 + b.c10, a.c11 + b.c11, a.c22 + b.c22};
 }
 
-// y = M x for a block-diagonal M (zeros contribute exact zeros)
+// y = M x (numpy gemv_n) for a block-diagonal M (zeros contribute exact zeros)
 __device__ __forceinline__ void mv_cov5(const Cov5& m, const double x[3], double y[3]) {
-    y[0] = m.c00 * x[0] + m.c01 * x[1];
-    y[1] = m.c10 * x[0] + m.c11 * x[1];
+    y[0] = fma(m.c00, x[0], m.c01 * x[1]);
+    y[1] = fma(m.c10, x[0], m.c11 * x[1]);
     y[2] = m.c22 * x[2];
 }
 
@@ -144,11 +155,12 @@ __device__ __forceinline__ double kl_with_inv(const double m1[3], const Cov5& c1
     tr = tr + (c1.c22 - c2.c22) * (i2.c22 - i1.c22);
     const Cov5 s = add_cov5(i1, i2);
     const double d0 = m1[0] - m2[0], d1 = m1[1] - m2[1], d2 = m1[2] - m2[2];
-    const double w0 = d0 * s.c00 + d1 * s.c10;
-    const double w1 = d0 * s.c01 + d1 * s.c11;
+    // dm @ (I1 + I2) (gemv_t), then @ dm (ddot)
+    const double w0 = fma(d1, s.c10, d0 * s.c00);
+    const double w1 = fma(d1, s.c11, d0 * s.c01);
     const double w2 = d2 * s.c22;
-    double q = w0 * d0 + w1 * d1;
-    q = q + w2 * d2;
+    double q = fma(w1, d1, w0 * d0);
+    q = fma(w2, d2, q);
     return tr + q;
 }
 
@@ -188,19 +200,21 @@ __device__ __forceinline__ double mahalanobis_geo(double a1, double b1, const Co
     const double r0 = a1 - a2, r1 = b1 - b2;
     double i00, i01, i10, i11;
     inv2(c1.c00 + c2.c00, c1.c01 + c2.c01, c1.c10 + c2.c10, c1.c11 + c2.c11, i00, i01, i10, i11);
-    const double t0 = r0 * i00 + r1 * i10;
-    const double t1 = r0 * i01 + r1 * i11;
-    const double d1 = t0 * r0 + t1 * r1;
+    // residual @ inv (gemv_t), then @ residual (ddot)
+    const double t0 = fma(r1, i10, r0 * i00);
+    const double t1 = fma(r1, i11, r0 * i01);
+    const double d1 = fma(t1, r1, t0 * r0);
     const double j2 = gb.q, j3 = -gc.q;
     const double j1 = -j3 - j2;
     const double j5 = -gb.w, j6 = gc.w;
     const double j4 = -j5 - j6;
+    // J @ diag(S) (exact products), then @ J (ddot)
     double cdt = (j1 * sza2) * j1;
-    cdt = cdt + (j2 * gb.sz2) * j2;
-    cdt = cdt + (j3 * gc.sz2) * j3;
-    cdt = cdt + (j4 * sra2) * j4;
-    cdt = cdt + (j5 * gb.sr2) * j5;
-    cdt = cdt + (j6 * gc.sr2) * j6;
+    cdt = fma(j2 * gb.sz2, j2, cdt);
+    cdt = fma(j3 * gc.sz2, j3, cdt);
+    cdt = fma(j4 * sra2, j4, cdt);
+    cdt = fma(j5 * gb.sr2, j5, cdt);
+    cdt = fma(j6 * gc.sr2, j6, cdt);
     const double res = gb.tau - gc.tau;
     const double d2 = (res * res) * (1.0 / cdt);
     return d1 + d2;
@@ -222,6 +236,7 @@ struct Mat3 {
     double m[3][3];
 };
 
+// A @ B (numpy gemm)
 __device__ __forceinline__ Mat3 mm3(const Mat3& A, const Mat3& B) {
     Mat3 C;
 #pragma unroll
@@ -229,14 +244,14 @@ __device__ __forceinline__ Mat3 mm3(const Mat3& A, const Mat3& B) {
 #pragma unroll
         for (int j = 0; j < 3; j++) {
             double s = A.m[i][0] * B.m[0][j];
-            s = s + A.m[i][1] * B.m[1][j];
-            s = s + A.m[i][2] * B.m[2][j];
+            s = fma(A.m[i][1], B.m[1][j], s);
+            s = fma(A.m[i][2], B.m[2][j], s);
             C.m[i][j] = s;
         }
     return C;
 }
 
-// A * B^T
+// A @ B.T (numpy gemm)
 __device__ __forceinline__ Mat3 mm3t(const Mat3& A, const Mat3& B) {
     Mat3 C;
 #pragma unroll
@@ -244,32 +259,33 @@ __device__ __forceinline__ Mat3 mm3t(const Mat3& A, const Mat3& B) {
 #pragma unroll
         for (int j = 0; j < 3; j++) {
             double s = A.m[i][0] * B.m[j][0];
-            s = s + A.m[i][1] * B.m[j][1];
-            s = s + A.m[i][2] * B.m[j][2];
+            s = fma(A.m[i][1], B.m[j][1], s);
+            s = fma(A.m[i][2], B.m[j][2], s);
             C.m[i][j] = s;
         }
     return C;
 }
 
-// A * C for a block-diagonal C ([[c00 c01 0] [c10 c11 0] [0 0 c22]]): the products with
+// A @ C for a block-diagonal C ([[c00 c01 0] [c10 c11 0] [0 0 c22]]): the products with
 // C's exact zeros, which add nothing to the reference's sums, are skipped
 __device__ __forceinline__ Mat3 mul_block(const Mat3& A, const Mat3& C) {
     Mat3 R;
 #pragma unroll
     for (int i = 0; i < 3; i++) {
-        R.m[i][0] = A.m[i][0] * C.m[0][0] + A.m[i][1] * C.m[1][0];
-        R.m[i][1] = A.m[i][0] * C.m[0][1] + A.m[i][1] * C.m[1][1];
+        R.m[i][0] = fma(A.m[i][1], C.m[1][0], A.m[i][0] * C.m[0][0]);
+        R.m[i][1] = fma(A.m[i][1], C.m[1][1], A.m[i][0] * C.m[0][1]);
         R.m[i][2] = A.m[i][2] * C.m[2][2];
     }
     return R;
 }
 
+// A @ x (numpy gemv_n: column 1 first, then 0, then 2)
 __device__ __forceinline__ void mv3(const Mat3& A, const double x[3], double y[3]) {
 #pragma unroll
     for (int i = 0; i < 3; i++) {
-        double s = A.m[i][0] * x[0];
-        s = s + A.m[i][1] * x[1];
-        s = s + A.m[i][2] * x[2];
+        double s = A.m[i][1] * x[1];
+        s = fma(A.m[i][0], x[0], s);
+        s = fma(A.m[i][2], x[2], s);
         y[i] = s;
     }
 }

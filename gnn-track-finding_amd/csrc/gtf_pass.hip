@@ -259,16 +259,17 @@ __global__ void __launch_bounds__(BLOCK) k_extrapolate(gtf_graph g, gtf_nodes n,
     // A = (I - K H) Pp, rows 0 and 1 (the only ones the aliased [a, b] block reads); the
     // identity's exact zero / one entries contribute nothing to the reference's sums
     Mat3 A;
+    // (numpy gemm: the 1 * P0j and 0 * P1j terms are exact, the last one is fused)
 #pragma unroll
     for (int j = 0; j < 3; j++) {
-        A.m[0][j] = Pp.m[0][j] + IKH.m[0][2] * Pp.m[2][j];
-        A.m[1][j] = Pp.m[1][j] + IKH.m[1][2] * Pp.m[2][j];
+        A.m[0][j] = fma(IKH.m[0][2], Pp.m[2][j], Pp.m[0][j]);
+        A.m[1][j] = fma(IKH.m[1][2], Pp.m[2][j], Pp.m[1][j]);
     }
     // P = A IKH^T + (K R) K^T, only the [a,b] block survives the aliasing (:362-365)
-    double P00 = A.m[0][0] + A.m[0][2] * IKH.m[0][2];
-    double P01 = A.m[0][1] + A.m[0][2] * IKH.m[1][2];
-    double P10 = A.m[1][0] + A.m[1][2] * IKH.m[0][2];
-    double P11 = A.m[1][1] + A.m[1][2] * IKH.m[1][2];
+    double P00 = fma(A.m[0][2], IKH.m[0][2], A.m[0][0]);
+    double P01 = fma(A.m[0][2], IKH.m[1][2], A.m[0][1]);
+    double P10 = fma(A.m[1][2], IKH.m[0][2], A.m[1][0]);
+    double P11 = fma(A.m[1][2], IKH.m[1][2], A.m[1][1]);
     P00 = P00 + (K0 * sig2) * K0;
     P01 = P01 + (K0 * sig2) * K1;
     P10 = P10 + (K1 * sig2) * K0;
@@ -283,10 +284,10 @@ __global__ void __launch_bounds__(BLOCK) k_extrapolate(gtf_graph g, gtf_nodes n,
     double sigma_rn = p.sigma0rz, sigma_zn = p.sigma0rz2;
     if (fabs(nbz) >= p.endcap_boundary) { sigma_zn = p.sigma0rz; sigma_rn = p.sigma0rz2; }
     const double J0 = 1.0 / dr, J1 = -1.0 / dr, J2 = (-dz) / (dr * dr), J3 = dz / (dr * dr);
-    double vt = (J0 * (sigma_z * sigma_z)) * J0;
-    vt = vt + (J1 * (sigma_zn * sigma_zn)) * J1;
-    vt = vt + (J2 * (sigma_r * sigma_r)) * J2;
-    vt = vt + (J3 * (sigma_rn * sigma_rn)) * J3;
+    double vt = (J0 * (sigma_z * sigma_z)) * J0;      // J @ S2 @ J.T (numpy ddot)
+    vt = fma(J1 * (sigma_zn * sigma_zn), J1, vt);
+    vt = fma(J2 * (sigma_r * sigma_r), J2, vt);
+    vt = fma(J3 * (sigma_rn * sigma_rn), J3, vt);
 
     if (isnan(smw)) raise_flag(w.err, GTF_ERR_SEND_MW_MISSING);
     uts.sv[3 * (int64_t)k + 0] = xu0;

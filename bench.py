@@ -20,16 +20,18 @@ between and after the pass's kernels on their stream (kernel_ms, the roofline of
 the dominant kernel, instrumented_ms_per_step) -- every event record costs a few
 microseconds of GPU timeline, so it stays out of the headline.
 
-Multi-GPU (torchrun, one process per GPU): every rank processes its own event
-(seed differs per rank) -- events are independent, so there is no data-path
-collective ("scaling": "weak"); the barrier and max-over-ranks timing bracket
-the timed steps. value = edges of all ranks x steps / max elapsed. At N > 1 the
-line also carries "sharded_single_event": one C4 event edge-sharded across the N
-ranks with the per-pass RCCL exchange (gtf/shard.py), total work fixed ("strong").
+Multi-GPU (torchrun, one process per GPU): the headline is the north star's config 4,
+ONE C4 event edge-sharded across the N ranks (gtf/shard.py: azimuthal wedges, each rank
+owns the receivers of its wedge, one halo all-to-all over RCCL per pass), total work
+fixed ("scaling": "strong"; at N = 1 the same event on one GPU). value = the event's
+edges x steps / max elapsed over ranks, with the barrier + synchronize bracket. The
+line also carries "event_replicas": every rank running its own C4 event (independent
+events, no collective, "weak").
 
-The CPU baseline (rank 0, N = 1 only) times the repository's NumPy restatement
-of the same pass (oracle/gtf_oracle.py, kind "port", 1 core) on a bounded
-sample event of the same generator.
+CPU baselines (rank 0, N = 1 only): the repository's NumPy restatement of the pass
+(oracle/gtf_oracle.py, kind "port", 1 core) on a bounded sample event of the same
+generator, the C++ restatement (oracle/cpu_ref.cpp) on the bench event on 1 core and
+all cores, and the drop-in stage wall time (gpickle in -> gpickle out).
 """
 import argparse
 import json
@@ -213,38 +215,62 @@ def bench_c5(dev, steps, warmup, n_events=256):
     return res
 
 
-def bench_sharded(workload, rank, world, dev, steps, warmup, params):
+def reduce_scalar(x, op, dev, backend):
+    """all-reduce one number across ranks (device tensor over RCCL, host tensor over gloo)"""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+    dist.all_reduce(t, op=op)
+    return float(t.item())
+
+
+def bench_sharded(workload, rank, world, dev, steps, warmup, params, backend="nccl"):
     """Config 4 as the north star states it: ONE pileup-200 event edge-sharded across
-    the ranks (receiver ranges balanced by slot count), one exchange of the owned merged
-    states and activations per pass (all-gather over RCCL; gtf/shard.py). Total work is
-    fixed as N grows ("strong"). Every rank runs the same event (seed 0)."""
+    the ranks (azimuthal wedges balanced by slots; gtf/shard.py), one halo exchange per
+    pass (all-to-all over RCCL). Total work is fixed as N grows ("strong"). Every rank
+    builds the same event (seed 0). Times K steps of restore + pass + exchange, and the
+    same K steps without the exchange (pass_ms: the compute share)."""
     import torch
     import torch.distributed as dist
     from gtf import synth
     from gtf.device import DeviceGraph
     from gtf.shard import ShardedDeviceGraph
     g = synth.workload(workload, seed=0)
-    sd = ShardedDeviceGraph(g, rank, world, dev, backend="nccl")
+    sd = ShardedDeviceGraph(g, rank, world, dev, backend=backend)
     snap = sd.d.snapshot(DeviceGraph.PASS_INPUTS)
+    sd.d.clear_errors()
     for _ in range(warmup):
         sd.d.restore(snap)
         sd.step(params)
-    torch.cuda.synchronize()
-    dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        sd.d.restore(snap)
-        sd.step(params)
-    torch.cuda.synchronize()
-    dist.barrier()
-    torch.cuda.synchronize()
-    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    el = float(t.item())
-    return {"scaling": "strong", "n_gpus": world, "edges": g.n_edges, "ms_per_step": el / steps * 1e3,
-            "edges_per_s": g.n_edges * steps / el, "exchange_chunk_bytes_per_rank": sd.chunk_bytes,
-            "owned_slots_max": sd.plan.cap_slots, "collective": "all_gather_into_tensor (RCCL)"}
+
+    def run(exchange):
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            sd.d.restore(snap)
+            if exchange:
+                sd.step(params)
+            else:
+                sd.pass_(params)
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        return reduce_scalar(time.perf_counter() - t0, dist.ReduceOp.MAX, dev, backend)
+
+    el = run(True)
+    el_pass = run(False)
+    flags = int(reduce_scalar(sd.d.errors(), dist.ReduceOp.MAX, dev, backend))
+    hb = int(reduce_scalar(sd.halo_bytes, dist.ReduceOp.MAX, dev, backend))
+    pl = sd.plan
+    return {"scaling": "strong", "n_gpus": world, "edges": g.n_edges, "nodes": g.n_nodes,
+            "ms_per_step": el / steps * 1e3, "edges_per_s": g.n_edges * steps / el,
+            "pass_ms_no_exchange": el_pass / steps * 1e3,
+            "halo_bytes_per_rank_max": hb, "owned_slots_max": pl.cap_slots,
+            "owned_slots_min": int((pl.slot_hi - pl.slot_lo).min()),
+            "collective": "all_to_all_single of per-destination halo segments (RCCL over xGMI)",
+            "node_order": "azimuthal wedges, tiled slot-count buckets inside each", "device_error_flags": flags, "backend": backend}
 
 
 # the fused node kernel: priors, side norm, reweights, update and KL clustering of every
@@ -281,10 +307,11 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-c5", action="store_true", help="skip the config-5 parabolic-KL section")
     ap.add_argument("--no-dropin", action="store_true", help="skip the drop-in stage wall time")
-    ap.add_argument("--no-sharded", action="store_true", help="skip the single-event sharded section (N > 1)")
     ap.add_argument("--layout", default="tiled", choices=["tiled", "schedule", "natural"],
                     help="device node order (DeviceGraph layout)")
     ap.add_argument("--tile", type=int, default=4096, help="nodes per tile of --layout tiled")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="torch.distributed backend for N > 1 (gloo: rehearsal with several ranks on one GPU)")
     args = ap.parse_args()
 
     import torch
@@ -297,10 +324,15 @@ def main():
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
+    if args.backend == "gloo":   # rehearsal: ranks may share the GPU
+        local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = "cuda:%d" % local
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device(dev))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(dev))
+        else:   # rehearsal of the N > 1 path with several ranks on one GPU (RCCL needs one GPU per rank)
+            dist.init_process_group("gloo")
 
     def barrier():
         if world > 1:
@@ -348,13 +380,10 @@ def main():
     elapsed_ev = timed(True)      # the same K passes with per-kernel events (kernel_ms, roofline)
     flags = d.errors()
 
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    edges = torch.tensor([float(g.n_edges)], dtype=torch.float64, device=dev)
+    total_edges = float(g.n_edges)
     if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dist.all_reduce(edges, op=dist.ReduceOp.SUM)
-    elapsed = float(t.item())
-    total_edges = float(edges.item())
+        elapsed = reduce_scalar(elapsed, dist.ReduceOp.MAX, dev, args.backend)
+        total_edges = reduce_scalar(total_edges, dist.ReduceOp.SUM, dev, args.backend)
 
     def avg(a, b):
         return float(np.mean([evs[i][a].elapsed_time(evs[i][b]) for i in range(K)]))
@@ -385,10 +414,10 @@ def main():
     traffic = committed_traffic(args.workload, name, args.layout, args.tile, g.n_edges, g.n_nodes)
 
     sharded = None
-    if world > 1 and not args.no_sharded:
+    if world > 1:
         try:
-            sharded = bench_sharded(args.workload, rank, world, dev, K, W, p)
-        except Exception as ex:   # reported, never fatal: the headline line above stands
+            sharded = bench_sharded(args.workload, rank, world, dev, K, W, p, args.backend)
+        except Exception as ex:   # reported; the line then carries the replicas only and is marked
             sharded = {"error": repr(ex)[:300]}
 
     c5 = None
@@ -413,7 +442,7 @@ def main():
             "ms_per_step": elapsed / K * 1e3,
             "instrumented_ms_per_step": elapsed_ev / K * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (seeded TrackML-shaped generator, gtf/synth.py)",
@@ -434,8 +463,24 @@ def main():
             "dropin_stage": dropin,
             "device_error_flags": flags,
             "c5_parabolic_kl": c5,
-            "sharded_single_event": sharded,
         }
+        if world > 1:
+            replicas = {"value": out["value"], "ms_per_step": out["ms_per_step"], "scaling": "weak",
+                        "parallelism": "event-parallel x%d (each rank its own C4 event, no collective)" % world,
+                        "seed_per_rank": "1000 * rank"}
+            out["event_replicas"] = replicas
+            if sharded and "error" not in sharded:
+                out["value"] = sharded["edges_per_s"]
+                out["ms_per_step"] = sharded["ms_per_step"]
+                out["config"]["parallelism"] = "edge-sharded x%d (one event, azimuthal wedges, halo all-to-all)" % world
+                out["config"]["workload"] = "one pileup-200 TrackML-shaped event (configs[3]) across all GPUs"
+                out["sharded_single_event"] = sharded
+                if sharded["device_error_flags"]:
+                    out["invalid"] = "sharded pass device_error_flags %d" % sharded["device_error_flags"]
+            else:
+                out["scaling"] = "weak"
+                out["config"]["parallelism"] = replicas["parallelism"]
+                out["sharded_error"] = (sharded or {}).get("error")
         if cpu:
             out["speedup_vs_cpu"] = out["value"] / cpu["value"]
         if cpu_cpp and "all_cores" in cpu_cpp:

@@ -651,7 +651,7 @@ int launch_extrap_edges(const gtf_graph* g, gtf_nodes* n, gtf_states* uts, gtf_e
     const int slot_lo = sh ? sh->slot_lo : 0, slot_hi = sh ? sh->slot_hi : g->n_slots;
     if (events) (void)hipEventRecord((hipEvent_t)events[0], st);
     if (g->n_slots > 0 && count > 0) {
-        if (!sh && g->out_sched) {
+        if (g->out_sched) {   // (a shard's graph view carries its own senders' schedule)
             SendBuckets sb;
             const int cnt[3] = {g->n_o4, g->n_o8, g->n_o16}, gs[3] = {4, 8, 16};
             const int4* l = reinterpret_cast<const int4*>(g->out_sched);

@@ -8,6 +8,8 @@
 // fixed layout; an all-gather of equal-size chunks over RCCL puts every chunk on every
 // GPU; one unpack launch scatters the other ranks' chunks into the replicated arrays.
 // Values travel as bytes, so the replicas are bit-identical to the owner's arrays.
+// The halo exchange (gtf_halo_pack / gtf_halo_unpack) moves only the records another
+// rank's next pass reads, through per-destination segments of one all-to-all.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -79,9 +81,79 @@ __global__ void __launch_bounds__(BLOCK) k_unpack(gtf_nodes n, gtf_edges e, cons
     if (t < slot_hi - slot_lo) e.act[slot_lo + t] = (uint8_t)chunk[L.act + t];
 }
 
+// halo records: thread t < n_nodes packs / unpacks node record t, the others activation
+// bytes (one launch covers both lists)
+__global__ void __launch_bounds__(BLOCK) k_halo_pack(gtf_nodes n, gtf_edges e, gtf_halo h, char* buf) {
+    const int64_t t = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (t < h.n_nodes) {
+        const int64_t v = h.node_idx[t];
+        uint64_t* rec = (uint64_t*)(buf + h.node_off[t]);
+        rec[0] = n.has_merged[v];
+        const uint64_t* ms = (const uint64_t*)(n.merged_state + 3 * v);
+        const uint64_t* mc = (const uint64_t*)(n.merged_cov + 5 * v);
+        for (int i = 0; i < 3; i++) rec[1 + i] = ms[i];
+        for (int i = 0; i < 5; i++) rec[4 + i] = mc[i];
+        rec[9] = *(const uint64_t*)(n.merged_prior + v);
+    } else if (t < (int64_t)h.n_nodes + h.n_slots) {
+        const int64_t j = t - h.n_nodes;
+        buf[h.slot_off[j]] = (char)e.act[h.slot_idx[j]];
+    }
+}
+
+__global__ void __launch_bounds__(BLOCK) k_halo_unpack(gtf_nodes n, gtf_edges e, gtf_halo h, const char* buf) {
+    const int64_t t = (int64_t)blockIdx.x * BLOCK + threadIdx.x;
+    if (t < h.n_nodes) {
+        const int64_t v = h.node_idx[t];
+        const uint64_t* rec = (const uint64_t*)(buf + h.node_off[t]);
+        n.has_merged[v] = (uint8_t)rec[0];
+        uint64_t* ms = (uint64_t*)(n.merged_state + 3 * v);
+        uint64_t* mc = (uint64_t*)(n.merged_cov + 5 * v);
+        for (int i = 0; i < 3; i++) ms[i] = rec[1 + i];
+        for (int i = 0; i < 5; i++) mc[i] = rec[4 + i];
+        *(uint64_t*)(n.merged_prior + v) = rec[9];
+    } else if (t < (int64_t)h.n_nodes + h.n_slots) {
+        const int64_t j = t - h.n_nodes;
+        e.act[h.slot_idx[j]] = (uint8_t)buf[h.slot_off[j]];
+    }
+}
+
+bool halo_ok(const gtf_halo* h) {
+    return h && h->n_nodes >= 0 && h->n_slots >= 0 && (h->n_nodes == 0 || (h->node_idx && h->node_off)) &&
+           (h->n_slots == 0 || (h->slot_idx && h->slot_off));
+}
+
 }  // namespace
 
 extern "C" {
+
+int gtf_halo_pack(const gtf_nodes* n, const gtf_edges* e, const gtf_halo* h, void* buf, gtf_stream_t stream) {
+    if (!n || !e || !halo_ok(h) || (!buf && h->n_nodes + h->n_slots > 0)) {
+        gtf::set_error("gtf_halo_pack: bad arguments");
+        return -2;
+    }
+    const int64_t m = (int64_t)h->n_nodes + h->n_slots;
+    if (m > 0)
+        hipLaunchKernelGGL(k_halo_pack, dim3((unsigned)((m + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, (hipStream_t)stream,
+                           *n, *e, *h, (char*)buf);
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) { gtf::set_error(hipGetErrorString(err)); return -1; }
+    return 0;
+}
+
+int gtf_halo_unpack(gtf_nodes* n, gtf_edges* e, const gtf_halo* h, const void* buf, gtf_stream_t stream) {
+    if (!n || !e || !halo_ok(h) || (!buf && h->n_nodes + h->n_slots > 0)) {
+        gtf::set_error("gtf_halo_unpack: bad arguments");
+        return -2;
+    }
+    const int64_t m = (int64_t)h->n_nodes + h->n_slots;
+    if (m > 0)
+        hipLaunchKernelGGL(k_halo_unpack, dim3((unsigned)((m + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0,
+                           (hipStream_t)stream, *n, *e, *h, (const char*)buf);
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) { gtf::set_error(hipGetErrorString(err)); return -1; }
+    return 0;
+}
+
 
 size_t gtf_shard_chunk_bytes(int32_t cap_nodes, int32_t cap_slots) {
     return layout(cap_nodes > 0 ? cap_nodes : 0, cap_slots > 0 ? cap_slots : 0).bytes;

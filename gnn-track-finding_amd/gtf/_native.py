@@ -61,6 +61,14 @@ class GtfShard(ctypes.Structure):
                 ("slot_hi", I32)]
 
 
+class GtfHalo(ctypes.Structure):
+    _fields_ = [("node_idx", P), ("node_off", P), ("n_nodes", I32), ("pad_", I32), ("slot_idx", P), ("slot_off", P),
+                ("n_slots", I32), ("pad2_", I32)]
+
+
+HALO_NODE_BYTES = 80   # GTF_HALO_NODE_BYTES
+
+
 class GtfTseExtra(ctypes.Structure):
     _fields_ = [("theta", P), ("var_ms", P), ("xy_mean_var", P), ("zr_mean_var", P), ("angle", P),
                 ("translation", P)]
@@ -122,7 +130,8 @@ ERR_FLAGS = {
 SYMBOLS = ["gtf_workspace_bytes", "gtf_clear_errors", "gtf_read_errors", "gtf_extrapolate", "gtf_update",
            "gtf_message_passing", "gtf_node_ops",
            "gtf_cluster", "gtf_pass", "gtf_pass_ev", "gtf_tag_prepare", "gtf_tag_sweep", "gtf_parabolic_kl", "gtf_track_state_estimates", "gtf_pass_shard",
-           "gtf_shard_chunk_bytes", "gtf_shard_pack", "gtf_shard_unpack", "gtf_extract_workspace_bytes",
+           "gtf_shard_chunk_bytes", "gtf_shard_pack", "gtf_shard_unpack", "gtf_halo_pack", "gtf_halo_unpack",
+           "gtf_extract_workspace_bytes",
            "gtf_extract_candidates", "gtf_build_event_csr", "gtf_candidate_order",
            "gtf_updated_state_pair_counts", "gtf_updated_state_distances",
            "gtf_last_error",
@@ -171,6 +180,9 @@ def lib():
     L.gtf_shard_chunk_bytes.argtypes = [I32, I32]
     L.gtf_shard_pack.argtypes = [N, E, SH, I32, I32, P, P]
     L.gtf_shard_unpack.argtypes = [N, E, P, I32, I32, P, I32, I32, P]
+    HA = ctypes.POINTER(GtfHalo)
+    L.gtf_halo_pack.argtypes = [N, E, HA, P, P]
+    L.gtf_halo_unpack.argtypes = [N, E, HA, P, P]
     L.gtf_track_state_estimates.argtypes = [G, S, ctypes.POINTER(GtfTseExtra), PR, P]
     L.gtf_parabolic_kl.argtypes = [ctypes.POINTER(GtfKlGraph), I32, ctypes.POINTER(GtfKlOut), P]
     L.gtf_build_event_csr.argtypes = [ctypes.POINTER(GtfEventCsr)]
@@ -182,7 +194,7 @@ def lib():
     for fn in ("gtf_clear_errors", "gtf_read_errors", "gtf_extrapolate", "gtf_update", "gtf_cluster", "gtf_pass",
                "gtf_pass_ev", "gtf_message_passing", "gtf_node_ops",
                "gtf_tag_prepare", "gtf_tag_sweep", "gtf_parabolic_kl", "gtf_track_state_estimates", "gtf_pass_shard", "gtf_shard_pack",
-               "gtf_shard_unpack", "gtf_extract_candidates", "gtf_build_event_csr",
+               "gtf_shard_unpack", "gtf_halo_pack", "gtf_halo_unpack", "gtf_extract_candidates", "gtf_build_event_csr",
                "gtf_candidate_order", "gtf_updated_state_pair_counts", "gtf_updated_state_distances"):
         getattr(L, fn).restype = ctypes.c_int
     _lib = L

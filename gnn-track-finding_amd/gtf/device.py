@@ -35,14 +35,15 @@ def sched_segments(slot_ptr, sched):
     return np.stack([sp[v], sp[v + 1]], axis=1).astype(np.int32).reshape(-1)
 
 
-def sender_schedule(out_ptr):
+def sender_schedule(out_ptr, nodes=None):
     """gtf_graph.out_sched: (sender, out begin, out end, 0) of every node with an
-    out-edge, bucketed by out-degree 1..4 / 5..8 / more; returns (array, counts)"""
+    out-edge (or of the given nodes: a shard's senders), bucketed by out-degree 1..4 /
+    5..8 / more; returns (array, counts)"""
     op = np.asarray(out_ptr, dtype=np.int64)
-    od = np.diff(op)
-    idx = np.arange(od.size, dtype=np.int64)
+    idx = np.arange(op.size - 1, dtype=np.int64) if nodes is None else np.asarray(nodes, dtype=np.int64)
+    od = op[idx + 1] - op[idx]
     parts = [idx[(od >= 1) & (od <= 4)], idx[(od >= 5) & (od <= 8)], idx[od > 8]]
-    u = np.concatenate(parts)
+    u = np.concatenate(parts).astype(np.int64)
     q = np.stack([u, op[u], op[u + 1], np.zeros_like(u)], axis=1).astype(np.int32).reshape(-1)
     return q, [int(x.size) for x in parts]
 

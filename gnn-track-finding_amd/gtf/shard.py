@@ -1,21 +1,34 @@
-"""One event sharded across GPUs: receiver ranges, per-pass state exchange.
+"""One event sharded across GPUs: receiver ranges, per-pass halo exchange.
 
 Every stage after message passing reduces over one receiver's in-slot segment, so
 cutting the receiver-major slot array at node boundaries keeps all of that work
-local. Rank r owns receivers [node_lo, node_hi) -- chosen so every rank holds about
-S / P slots -- and every rank keeps a replica of the whole graph (a pileup-200 event
-is ~0.35 GB; HBM holds hundreds). Per pass, rank r:
+local. Rank r owns receivers [node_lo, node_hi) and every rank keeps a replica of the
+whole graph (a pileup-200 event is ~0.35 GB; HBM holds hundreds).
+
+Node order. With more than one rank the event is renumbered before upload so that the
+contiguous ranges are azimuthal wedges (``sector_order``: φ cut at slot-weighted
+quantiles, original (layer, φ) order inside a wedge): tracks are nearly radial and an
+edge spans at most ~0.06 rad, so few edges cross a wedge boundary. Inside every rank's
+range the nodes are then bucketed by slot count tile by tile (the 1-GPU "tiled" layout,
+``gtf.device.schedule_order``); the pass is equivariant under renumbering, and
+``download`` maps results back to the host order.
+
+Per pass, rank r (``gtf_pass_shard``):
 
 1. scans the out-edges of its ``senders`` (every sender with an edge into an owned
-   receiver, plus its own senders, whose cumulative merged_cov[1,1] it publishes);
-2. extrapolates its owned slots and runs the node kernels on its owned receivers
-   (``gtf_pass_shard``);
-3. publishes its owned nodes' merged state and its owned slots' activation:
-   ``gtf_shard_pack`` -> one all-gather of equal-size chunks (RCCL over xGMI, or gloo
-   through host memory) -> ``gtf_shard_unpack``. The bytes travel unchanged, so the
-   replicas stay bit-identical and the sharded pass equals the one-GPU pass exactly.
+   receiver, plus its own senders) on an out-degree-bucketed schedule (``out_sched``,
+   as the 1-GPU pass);
+2. extrapolates its owned slots and runs the fused node kernel on its owned receivers
+   (their slot-count schedule, 2-lane groups included);
+3. exchanges the halo (:class:`HaloPlan`): each rank sends every other rank the merged
+   states of that rank's senders it owns and the activations of those senders'
+   out-edges whose receivers it owns -- exactly what the other rank's next sender scan
+   reads -- through per-destination segments of ONE all-to-all (RCCL over xGMI; gloo
+   through host memory on CPU). Values travel as bytes, so the pass equals the one-GPU
+   pass bit for bit.
 
-The plan (ranges, sender lists, schedules) is host logic (:class:`ShardPlan`).
+``sync`` makes every replica complete (all-gather of every owned state, the round-1
+exchange) before results are read back.
 """
 from __future__ import annotations
 
@@ -24,20 +37,62 @@ import ctypes
 import numpy as np
 
 from . import _native as nat
-from .graph import BUCKETS, TrackGraph
+from .graph import BUCKETS, TrackGraph, renumber
+
+
+def sector_order(g: TrackGraph, world: int):
+    """(order, cuts): node order with each of `world` azimuthal wedges contiguous (wedges
+    balanced by slots + nodes, original order inside a wedge) and the wedges' node
+    boundaries (cuts[r]..cuts[r+1] is wedge r)."""
+    N = g.n_nodes
+    if world <= 1 or N == 0:
+        return np.arange(N, dtype=np.int64), np.array([0, N], np.int64)
+    phi = np.arctan2(g.node["gnn"][:, 1], g.node["gnn"][:, 0])
+    w = np.diff(g.slot_ptr.astype(np.int64)) + 1
+    o = np.argsort(phi, kind="stable")
+    cw = np.cumsum(w[o])
+    tot = cw[-1]
+    k = np.searchsorted(cw, [tot * r / world for r in range(1, world)], side="left")
+    cuts_phi = phi[o[np.minimum(k, N - 1)]]
+    sector = np.searchsorted(cuts_phi, phi, side="right")
+    order = np.lexsort((np.arange(N), sector))
+    cuts = np.concatenate([[0], np.cumsum(np.bincount(sector, minlength=world))]).astype(np.int64)
+    return order.astype(np.int64), cuts
+
+
+def shard_layout(g: TrackGraph, world: int, tile: int):
+    """The device node order of a sharded event and its rank cuts: wedges (world > 1),
+    then the tiled slot-count bucketing inside each rank's range. Returns
+    (device graph, order, slot_perm, cuts); device node i is host node order[i]."""
+    from .device import schedule_order
+    o1, cuts = sector_order(g, world)
+    g1, sp1 = renumber(g, o1)
+    sp = g1.slot_ptr.astype(np.int64)
+    parts = []
+    for r in range(len(cuts) - 1):
+        lo, hi = int(cuts[r]), int(cuts[r + 1])
+        parts.append(lo + schedule_order(sp[lo:hi + 1] - sp[lo], tile))
+    o2 = np.concatenate(parts) if parts else np.zeros(0, np.int64)
+    g2, sp2 = renumber(g1, o2)
+    return g2, o1[o2], sp1[sp2], cuts
 
 
 class ShardPlan:
-    """Receiver ranges balanced by slot count, and each rank's sender list and schedule."""
+    """Receiver ranges (given cuts, or balanced by slot count), and each rank's sender
+    list and schedules."""
 
-    def __init__(self, g: TrackGraph, world: int):
+    def __init__(self, g: TrackGraph, world: int, cuts=None):
         if world < 1:
             raise ValueError("world must be >= 1")
         sp = g.slot_ptr.astype(np.int64)
         S = int(sp[-1])
-        targets = [(r * S + world // 2) // world for r in range(world + 1)]
-        cuts = [0] + [int(np.searchsorted(sp, t, side="left")) for t in targets[1:-1]] + [g.n_nodes]
-        cuts = np.maximum.accumulate(np.minimum(np.asarray(cuts, np.int64), g.n_nodes))
+        if cuts is None:
+            targets = [(r * S + world // 2) // world for r in range(world + 1)]
+            cuts = [0] + [int(np.searchsorted(sp, t, side="left")) for t in targets[1:-1]] + [g.n_nodes]
+            cuts = np.maximum.accumulate(np.minimum(np.asarray(cuts, np.int64), g.n_nodes))
+        cuts = np.asarray(cuts, np.int64)
+        if cuts.size != world + 1 or cuts[0] != 0 or cuts[-1] != g.n_nodes or (np.diff(cuts) < 0).any():
+            raise ValueError("cuts must be world + 1 non-decreasing node boundaries from 0 to n_nodes")
         self.world = world
         self.node_lo = cuts[:-1].astype(np.int32)
         self.node_hi = cuts[1:].astype(np.int32)
@@ -51,6 +106,9 @@ class ShardPlan:
         """int32 [4 * world]: node_lo, node_hi, slot_lo, slot_hi per rank"""
         return np.stack([self.node_lo, self.node_hi, self.slot_lo, self.slot_hi], 1).reshape(-1).astype(np.int32)
 
+    def owner_of_nodes(self) -> np.ndarray:
+        return np.repeat(np.arange(self.world, dtype=np.int32), self.node_hi - self.node_lo)
+
     def senders(self, r: int) -> np.ndarray:
         g = self._g
         lo, hi = int(self.slot_lo[r]), int(self.slot_hi[r])
@@ -62,13 +120,84 @@ class ShardPlan:
         return np.unique(np.concatenate([halo.astype(np.int64), own])).astype(np.int32)
 
     def schedule(self, r: int):
-        """(sched, [n_g4, n_g8, n_g16, n_g32, n_g64], n_big) of the owned receivers"""
+        """(sched, [n_g4, n_g8, n_g16, n_g32, n_g64], n_big, n_g2) of the owned receivers:
+        slot-count buckets in node order, the <= 2-slot nodes first in the <= 4 bucket"""
         deg = np.diff(self._g.slot_ptr.astype(np.int64))
         idx = np.arange(self.node_lo[r], self.node_hi[r], dtype=np.int32)
         d = deg[idx]
         buckets = [idx[(d >= lo) & (d <= hi)] for lo, hi in BUCKETS]
+        d0 = deg[buckets[0]]
+        buckets[0] = np.concatenate([buckets[0][d0 <= 2], buckets[0][d0 > 2]])
         big = idx[d > 64]
-        return np.concatenate(buckets + [big]).astype(np.int32), [int(b.size) for b in buckets], int(big.size)
+        return (np.concatenate(buckets + [big]).astype(np.int32), [int(b.size) for b in buckets], int(big.size),
+                int((d0 <= 2).sum()))
+
+    def sender_schedule(self, r: int):
+        """the rank's senders as (u, out_ptr[u], out_ptr[u+1], 0) quadruples bucketed by
+        out-degree (gtf_graph.out_sched) and the bucket sizes [n_o4, n_o8, n_o16]"""
+        from .device import sender_schedule
+        g = self._g
+        u = self.senders(r).astype(np.int64)
+        op = g.out_ptr.astype(np.int64)
+        return sender_schedule(op, u)
+
+
+class HaloPlan:
+    """What each rank's next pass reads from the others: for rank r, the merged states
+    of its senders owned elsewhere and the activations of its senders' out-edges whose
+    receivers are owned elsewhere. A message q -> r is one segment
+    [node records (GTF_HALO_NODE_BYTES each) | activation bytes], padded to 8 bytes."""
+
+    def __init__(self, plan: ShardPlan):
+        g = plan._g
+        W = plan.world
+        self.world = W
+        on = plan.owner_of_nodes()
+        slot_dst = g.slot_dst() if g.n_slots else np.zeros(0, np.int64)
+        os_ = on[slot_dst] if g.n_slots else np.zeros(0, np.int32)
+        op = g.out_ptr.astype(np.int64)
+        self.need_nodes, self.need_slots = [], []
+        for r in range(W):
+            s = plan.senders(r).astype(np.int64)
+            self.need_nodes.append(np.sort(s[on[s] != r]).astype(np.int32))
+            cnt = op[s + 1] - op[s]
+            first = np.repeat(op[s], cnt)
+            pos = np.arange(int(cnt.sum()), dtype=np.int64) - np.repeat(np.cumsum(cnt) - cnt, cnt)
+            sl = g.out_slot.astype(np.int64)[first + pos] if cnt.sum() else np.zeros(0, np.int64)
+            self.need_slots.append(np.unique(sl[os_[sl] != r]).astype(np.int32))
+        self._on, self._os = on, os_
+
+    @staticmethod
+    def _seg_bytes(n_nodes, n_slots):
+        return (nat.HALO_NODE_BYTES * n_nodes + n_slots + 7) // 8 * 8
+
+    def message(self, q: int, r: int):
+        """(nodes, slots) rank q sends rank r"""
+        nn, ns = self.need_nodes[r], self.need_slots[r]
+        return nn[self._on[nn] == q], ns[self._os[ns] == q]
+
+    def lists(self, rank: int, send: bool):
+        """node / slot indices with their byte offsets in this rank's send (or receive)
+        buffer, and the per-peer segment sizes (all_to_all split sizes)"""
+        idx_n, off_n, idx_s, off_s, sizes = [], [], [], [], []
+        base = 0
+        for peer in range(self.world):
+            if peer == rank:
+                sizes.append(0)
+                continue
+            nodes, slots = self.message(rank, peer) if send else self.message(peer, rank)
+            idx_n.append(nodes)
+            off_n.append(base + nat.HALO_NODE_BYTES * np.arange(nodes.size, dtype=np.int64))
+            idx_s.append(slots)
+            off_s.append(base + nat.HALO_NODE_BYTES * nodes.size + np.arange(slots.size, dtype=np.int64))
+            b = self._seg_bytes(nodes.size, slots.size)
+            sizes.append(b)
+            base += b
+        cat = lambda xs, dt: np.concatenate(xs).astype(dt) if xs else np.zeros(0, dt)  # noqa: E731
+        return cat(idx_n, np.int32), cat(off_n, np.int64), cat(idx_s, np.int32), cat(off_s, np.int64), sizes
+
+    def bytes_sent(self, rank: int) -> int:
+        return int(sum(self.lists(rank, True)[4]))
 
 
 def allgather_bytes(chunk, out, backend: str, group=None):
@@ -86,40 +215,83 @@ def allgather_bytes(chunk, out, backend: str, group=None):
     return out
 
 
-class ShardedDeviceGraph:
-    """A DeviceGraph replica on this rank's GPU that runs the pass for its receivers
-    and exchanges the published state with the other ranks after each pass."""
+def alltoall_bytes(send, recv, send_sizes, recv_sizes, backend: str, group=None):
+    """one all-to-all of variable-size uint8 segments (split sizes in bytes). RCCL moves
+    device buffers over xGMI; gloo stages through host memory."""
+    import torch.distributed as dist
+    if backend == "nccl":
+        dist.all_to_all_single(recv, send, recv_sizes, send_sizes, group=group)
+        return recv
+    h = recv.cpu()
+    dist.all_to_all_single(h, send.cpu(), recv_sizes, send_sizes, group=group)
+    recv.copy_(h.to(recv.device))
+    return recv
 
-    def __init__(self, g: TrackGraph, rank: int, world: int, device="cuda", backend="nccl", group=None):
+
+class ShardedDeviceGraph:
+    """A DeviceGraph replica on this rank's GPU (wedge + tiled node order) that runs the
+    pass for its receivers and exchanges the halo with the other ranks after each pass."""
+
+    def __init__(self, g: TrackGraph, rank: int, world: int, device="cuda", backend="nccl", group=None,
+                 tile: int = None):
         import torch
-        from .device import DeviceGraph, sched_segments
+        from .device import DeviceGraph, TILE, sched_segments
         self.torch = torch
         self.rank, self.world, self.backend, self.group = rank, world, backend, group
-        self.plan = ShardPlan(g, world)
-        self.d = DeviceGraph(g, device)
+        gd, order, slot_perm, cuts = shard_layout(g, world, TILE if tile is None else tile)
+        self.plan = ShardPlan(gd, world, cuts)
+        self.halo = HaloPlan(self.plan)
+        self.d = DeviceGraph(gd, device)
         d = self.d
+        d.order, d.slot_perm, d.layout = order, slot_perm, "sharded"   # download() maps back to host order
         dev = d.device
         up = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
-        self.senders = up(self.plan.senders(rank))
-        sched, n_g, n_big = self.plan.schedule(rank)
-        self.sched = up(sched)
-        self.sched_seg = up(sched_segments(g.slot_ptr, sched))
-        self.ranges = up(self.plan.ranges())
-        p = d.ptr
         vp = lambda t: ctypes.c_void_p(t.data_ptr() if t.numel() else 0)  # noqa: E731
+        pl = self.plan
+        self.senders = up(pl.senders(rank))
+        sched, n_g, n_big, n_g2 = pl.schedule(rank)
+        self.sched = up(sched)
+        self.sched_seg = up(sched_segments(gd.slot_ptr, sched))
+        osched, n_o = pl.sender_schedule(rank)
+        self.out_sched = up(osched)
+        self.ranges = up(pl.ranges())
+        p = d.ptr
         self.cg = nat.GtfGraph(n_nodes=d.n_nodes, n_slots=d.n_slots, n_edges=d.n_edges, n_big=n_big,
                                slot_ptr=p("slot_ptr"), slot_src=p("slot_src"), slot_dst=p("slot_dst"),
                                out_ptr=p("out_ptr"), out_slot=p("out_slot"), slot_outpos=p("slot_outpos"),
                                is_edge=p("is_edge"), rev_edge=p("rev_edge"), solo=p("solo"), gnn=p("gnn"),
                                xyzr=p("xyzr"), layer=p("layer"), sched=vp(self.sched), n_g4=n_g[0], n_g8=n_g[1],
                                n_g16=n_g[2], n_g32=n_g[3], n_g64=n_g[4], out_dst=p("out_dst"),
-                               slot_layer=p("slot_layer"), sched_seg=vp(self.sched_seg))
-        pl = self.plan
+                               slot_layer=p("slot_layer"), sched_seg=vp(self.sched_seg),
+                               out_sched=vp(self.out_sched), n_o4=n_o[0], n_o8=n_o[1], n_o16=n_o[2], n_g2=n_g2)
         self.shard = nat.GtfShard(vp(self.senders), int(self.senders.numel()), int(pl.node_lo[rank]),
                                   int(pl.node_hi[rank]), int(pl.slot_lo[rank]), int(pl.slot_hi[rank]))
+        # halo exchange buffers and lists (fixed per plan)
+        self._halo_t = {}
+        self.halo_send, self.halo_recv = self._halo(True), self._halo(False)
+        self.send_buf = torch.zeros(max(sum(self.send_sizes), 8), dtype=torch.uint8, device=dev)
+        self.recv_buf = torch.zeros(max(sum(self.recv_sizes), 8), dtype=torch.uint8, device=dev)
+        # full sync (every owned state, all-gather) before results are read back
         self.chunk_bytes = int(d.lib.gtf_shard_chunk_bytes(pl.cap_nodes, pl.cap_slots))
         self.chunk = torch.zeros(self.chunk_bytes, dtype=torch.uint8, device=dev)
         self.gathered = torch.zeros(self.chunk_bytes * world, dtype=torch.uint8, device=dev)
+
+    def _halo(self, send):
+        torch = self.torch
+        idx_n, off_n, idx_s, off_s, sizes = self.halo.lists(self.rank, send)
+        ts = [torch.from_numpy(a).to(self.d.device) for a in (idx_n, off_n, idx_s, off_s)]
+        self._halo_t[send] = ts     # keep the device lists alive
+        if send:
+            self.send_sizes = sizes
+        else:
+            self.recv_sizes = sizes
+        vp = lambda t: ctypes.c_void_p(t.data_ptr() if t.numel() else 0)  # noqa: E731
+        return nat.GtfHalo(vp(ts[0]), vp(ts[1]), int(idx_n.size), 0, vp(ts[2]), vp(ts[3]), int(idx_s.size), 0)
+
+    @property
+    def halo_bytes(self) -> int:
+        """bytes this rank sends per pass"""
+        return int(sum(self.send_sizes))
 
     def pass_(self, p, events=None):
         """the pass for the owned receivers (events: optional 5 hipEvent_t handles)"""
@@ -131,7 +303,20 @@ class ShardedDeviceGraph:
                                        ctypes.byref(self.shard), d.ptr("ws"), d.stream, ev))
 
     def exchange(self):
-        """publish the owned merged states and activations; take the other ranks'"""
+        """the halo: what the other ranks' next pass reads, one all-to-all"""
+        if self.world == 1:
+            return
+        d = self.d
+        nat.check(d.lib.gtf_halo_pack(ctypes.byref(d.cn), ctypes.byref(d.ce), ctypes.byref(self.halo_send),
+                                      ctypes.c_void_p(self.send_buf.data_ptr()), d.stream))
+        alltoall_bytes(self.send_buf[:sum(self.send_sizes)], self.recv_buf[:sum(self.recv_sizes)], self.send_sizes,
+                       self.recv_sizes, self.backend, self.group)
+        nat.check(d.lib.gtf_halo_unpack(ctypes.byref(d.cn), ctypes.byref(d.ce), ctypes.byref(self.halo_recv),
+                                        ctypes.c_void_p(self.recv_buf.data_ptr()), d.stream))
+
+    def sync(self):
+        """every owned merged state and activation to every replica (all-gather), so the
+        whole graph can be read back from any rank"""
         d = self.d
         pl = self.plan
         nat.check(d.lib.gtf_shard_pack(ctypes.byref(d.cn), ctypes.byref(d.ce), ctypes.byref(self.shard),
@@ -146,3 +331,12 @@ class ShardedDeviceGraph:
     def step(self, p, events=None):
         self.pass_(p, events)
         self.exchange()
+
+    def owned_host_nodes(self) -> np.ndarray:
+        """host indices of this rank's receivers (their results are final on this rank)"""
+        r = self.rank
+        return self.d.order[self.plan.node_lo[r]:self.plan.node_hi[r]]
+
+    def owned_host_slots(self) -> np.ndarray:
+        r = self.rank
+        return self.d.slot_perm[self.plan.slot_lo[r]:self.plan.slot_hi[r]]

@@ -221,9 +221,11 @@ int gtf_pass_ev(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* u
  * (every sender with an out-edge into an owned receiver, plus the owned senders whose
  * merged_cov write-back the rank publishes), extrapolation of the owned slots, and the
  * node kernels over the owned receivers (pass `g` with sched, n_g8..n_g64 and n_big describing the
- * owned receivers only). Between passes each rank publishes its owned merged states and
- * slot activations (gtf_shard_pack -> an all-gather of equal-size chunks over RCCL ->
- * gtf_shard_unpack), the only cross-rank data the next pass reads. */
+ * owned receivers only; with g->out_sched set, the scan runs on that out-degree-bucketed
+ * schedule of the shard's senders). Between passes the ranks exchange what the next pass
+ * reads: the halo (gtf_halo_pack -> all-to-all -> gtf_halo_unpack, below), or every owned
+ * state (gtf_shard_pack -> an all-gather of equal-size chunks -> gtf_shard_unpack: full
+ * replicas, used before reading results back). */
 typedef struct gtf_shard {
     const int32_t* senders;   /* [n_senders] device */
     int32_t n_senders;
@@ -244,6 +246,30 @@ int gtf_shard_pack(const gtf_nodes* n, const gtf_edges* e, const gtf_shard* shar
  * ranges: device int32 [4 * nranks] = node_lo, node_hi, slot_lo, slot_hi per rank */
 int gtf_shard_unpack(gtf_nodes* n, gtf_edges* e, const void* gathered, int32_t nranks, int32_t self,
                      const int32_t* ranges, int32_t cap_nodes, int32_t cap_slots, gtf_stream_t stream);
+
+/* Halo exchange (the per-pass exchange of gtf/shard.py): only what the other ranks' next
+ * pass reads -- the merged state of their halo senders owned here, and the activation
+ * of the out-edges of their senders whose receivers are owned here -- instead of every
+ * owned state. The lists are built once per plan (host); per pass a rank packs one
+ * buffer of per-destination segments, exchanges it with one all-to-all (RCCL over
+ * xGMI), and scatters what it received. A node record is GTF_HALO_NODE_BYTES: has_merged
+ * as a 64-bit integer, merged_state[3], merged_cov[5], merged_prior (raw fp64 bits);
+ * an activation is one byte. Offsets of node records must be multiples of 8. */
+#define GTF_HALO_NODE_BYTES 80
+typedef struct gtf_halo {
+    const int32_t* node_idx;  /* [n_nodes] device: node of each record */
+    const int64_t* node_off;  /* [n_nodes] device: byte offset of each record in the buffer */
+    int32_t n_nodes;
+    int32_t pad_;
+    const int32_t* slot_idx;  /* [n_slots] device: slot of each activation byte */
+    const int64_t* slot_off;  /* [n_slots] device: byte offset of each activation byte */
+    int32_t n_slots;
+    int32_t pad2_;
+} gtf_halo;
+/* gather the listed node states and activations into buf (device) */
+int gtf_halo_pack(const gtf_nodes* n, const gtf_edges* e, const gtf_halo* h, void* buf, gtf_stream_t stream);
+/* scatter buf (device) into the listed node states and activations */
+int gtf_halo_unpack(gtf_nodes* n, gtf_edges* e, const gtf_halo* h, const void* buf, gtf_stream_t stream);
 
 /* Tag propagation. radius: [N] node radius (attr 'zr'[1]); keep: [E] output mask of
  * kept inward neighbours per out-edge (u8, indexed by out-edge position);

@@ -42,7 +42,7 @@ def test_struct_layout_matches_header():
     against the header and compare with the ctypes mirrors"""
     from gtf import _native as nat
     py = {"gtf_graph": nat.GtfGraph, "gtf_nodes": nat.GtfNodes, "gtf_states": nat.GtfStates,
-          "gtf_edges": nat.GtfEdges, "gtf_params": nat.GtfParams, "gtf_kl_graph": nat.GtfKlGraph, "gtf_tse_extra": nat.GtfTseExtra, "gtf_shard": nat.GtfShard,
+          "gtf_edges": nat.GtfEdges, "gtf_params": nat.GtfParams, "gtf_kl_graph": nat.GtfKlGraph, "gtf_tse_extra": nat.GtfTseExtra, "gtf_shard": nat.GtfShard, "gtf_halo": nat.GtfHalo,
           "gtf_extract_params": nat.GtfExtractParams, "gtf_extract_io": nat.GtfExtractIO,
           "gtf_kl_out": nat.GtfKlOut, "gtf_event_csr": nat.GtfEventCsr,
           "gtf_candidate_graph": nat.GtfCandidateGraph, "gtf_pair_out": nat.GtfPairOut}

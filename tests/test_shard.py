@@ -1,6 +1,7 @@
-"""Single-event sharding (§8e): the host plan on CPU, the exchange protocol over gloo
-with world size 2 on CPU, and the sharded pass on the GPU (two ranks on one GPU over
-gloo) against the one-GPU pass, bit for bit."""
+"""Single-event sharding (§8e): the host plan (ranges, wedge node order, schedules, halo
+lists) on CPU, the exchange collectives over gloo with world size 2 on CPU, and the
+sharded pass on the GPU (two ranks on one GPU over gloo; one rank over RCCL) against the
+one-GPU pass, bit for bit."""
 import os
 import socket
 
@@ -27,15 +28,73 @@ def test_plan_partitions_receivers_and_slots(world):
     owner = np.repeat(np.arange(world), pl.node_hi - pl.node_lo)
     dst = g.slot_dst()
     for r in range(world):
-        sched, n_g, n_big = pl.schedule(r)
+        sched, n_g, n_big, n_g2 = pl.schedule(r)
         assert sorted(sched.tolist()) == list(range(pl.node_lo[r], pl.node_hi[r]))
-        assert sum(n_g) + n_big == sched.size
+        assert sum(n_g) + n_big == sched.size and 0 <= n_g2 <= n_g[0]
+        deg = np.diff(g.slot_ptr)
+        assert (deg[sched[:n_g2]] <= 2).all() and (deg[sched[n_g2:n_g[0]]] > 2).all()
         snd = set(pl.senders(r).tolist())
         # every sender of an owned edge, and every owned node with out-edges, is scanned
         e = g.slot["is_edge"].astype(bool) & (owner[dst] == r)
         assert set(g.slot["slot_src"][e].tolist()) <= snd
         outdeg = np.diff(g.out_ptr)
         assert {v for v in range(pl.node_lo[r], pl.node_hi[r]) if outdeg[v] > 0} <= snd
+        osched, n_o = pl.sender_schedule(r)
+        q = osched.reshape(-1, 4)
+        assert sorted(q[:, 0].tolist()) == sorted(snd) and sum(n_o) == len(snd)
+        assert (q[:, 1] == g.out_ptr[q[:, 0]]).all() and (q[:, 2] == g.out_ptr[q[:, 0] + 1]).all()
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_wedge_layout_is_a_permutation_with_small_halo(world):
+    from gtf.graph import check_layout
+    from gtf.shard import HaloPlan, shard_layout
+    g = synth.event(seed=4, n_tracks=3000, fake_mean=synth.C4_FAKE)
+    gd, order, slot_perm, cuts = shard_layout(g, world, 512)
+    check_layout(gd)
+    assert sorted(order.tolist()) == list(range(g.n_nodes))
+    assert sorted(slot_perm.tolist()) == list(range(g.n_slots))
+    assert np.array_equal(gd.node["gnn"], g.node["gnn"][order])
+    assert np.array_equal(gd.slot["slot_key"], g.slot["slot_key"][slot_perm])
+    pl = ShardPlan(gd, world, cuts)
+    sizes = pl.slot_hi - pl.slot_lo
+    assert sizes.max() <= 1.1 * g.n_slots / world + 64          # wedges balanced by slots
+    h = HaloPlan(pl)
+    halo = sum(x.size for x in h.need_nodes)
+    assert halo < 0.1 * g.n_nodes, halo                            # azimuthal wedges: a thin halo
+    # against layer-range cuts of the host order, the round-1 partition
+    h0 = HaloPlan(ShardPlan(g, world))
+    assert halo < 0.5 * sum(x.size for x in h0.need_nodes)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_halo_plan_is_what_the_next_pass_reads(world):
+    """rank r needs exactly: the merged state of every sender it scans that another rank
+    owns, and the activation of every out-edge of those senders (and of its own) whose
+    receiver another rank owns; each item comes from its owner, once"""
+    from gtf.shard import HaloPlan
+    g = _event()
+    pl = ShardPlan(g, world)
+    h = HaloPlan(pl)
+    on = pl.owner_of_nodes()
+    dst = g.slot_dst()
+    for r in range(world):
+        snd = pl.senders(r)
+        exp_n = sorted(u for u in snd.tolist() if on[u] != r)
+        exp_s = sorted(int(g.out_slot[e]) for u in snd.tolist() for e in range(g.out_ptr[u], g.out_ptr[u + 1])
+                       if on[dst[g.out_slot[e]]] != r)
+        assert h.need_nodes[r].tolist() == exp_n and h.need_slots[r].tolist() == exp_s
+        got_n, got_s = [], []
+        for q in range(world):
+            nodes, slots = h.message(q, r)
+            assert (on[nodes] == q).all() and (on[dst[slots]] == q).all()
+            got_n += nodes.tolist()
+            got_s += slots.tolist()
+        assert sorted(got_n) == exp_n and sorted(got_s) == exp_s
+        # send / receive layouts agree pairwise
+        for q in range(world):
+            if q != r:
+                assert h.lists(q, True)[4][r] == h.lists(r, False)[4][q]
 
 
 def _free_port():
@@ -75,6 +134,39 @@ def test_exchange_allgather_gloo_world2():
         assert (res[r] == exp).all()
 
 
+def _gloo_alltoall_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    from gtf.shard import alltoall_bytes
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # rank r sends (r + 1) * (d + 1) bytes of value 10 r + d to rank d
+    send_sizes = [(rank + 1) * (d + 1) for d in range(world)]
+    send = torch.cat([torch.full((n,), 10 * rank + d, dtype=torch.uint8) for d, n in enumerate(send_sizes)])
+    recv_sizes = [(s + 1) * (rank + 1) for s in range(world)]
+    recv = torch.zeros(sum(recv_sizes), dtype=torch.uint8)
+    alltoall_bytes(send, recv, send_sizes, recv_sizes, "gloo")
+    q.put((rank, recv.numpy().copy(), recv_sizes))
+    dist.destroy_process_group()
+
+
+def test_exchange_alltoall_gloo_world2():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_gloo_alltoall_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = {r: (a, sz) for r, a, sz in (q.get(timeout=120) for _ in ps)}
+    for p in ps:
+        p.join(60)
+    for r in range(2):
+        a, sz = res[r]
+        exp = np.concatenate([np.full(n, 10 * s + r, np.uint8) for s, n in enumerate(sz)])
+        assert (a == exp).all()
+
+
 # ---------------------------------------------------------------- GPU (2 ranks, 1 GPU)
 PASSES = 2
 OUT_NODE = ("has_merged", "merged_state", "merged_cov", "merged_prior", "has_uts", "degree")
@@ -94,23 +186,27 @@ def _shard_worker(rank, world, port, q, backend="gloo"):
     else:
         dist.init_process_group("gloo", rank=rank, world_size=world)
     g = _event()
-    sd = ShardedDeviceGraph(g, rank, world, "cuda:0", backend=backend)
-    if backend == "nccl":   # the device all-gather itself (exchange() skips it at world 1)
-        from gtf.shard import allgather_bytes
+    sd = ShardedDeviceGraph(g, rank, world, "cuda:0", backend=backend, tile=256)
+    if backend == "nccl":   # the device collectives themselves (exchange() skips them at world 1)
+        from gtf.shard import allgather_bytes, alltoall_bytes
         c = torch.arange(4096, device="cuda:0").to(torch.uint8)
         o = torch.zeros(4096 * world, dtype=torch.uint8, device="cuda:0")
         allgather_bytes(c, o, "nccl")
         assert torch.equal(o[4096 * rank:4096 * (rank + 1)], c)
+        o2 = torch.zeros(4096, dtype=torch.uint8, device="cuda:0")
+        alltoall_bytes(c, o2, [4096], [4096], "nccl")
+        assert torch.equal(o2, c)
     p = Params()
     for _ in range(PASSES):
         sd.step(p)
+    sd.sync()
     torch.cuda.synchronize()
     h = sd.d.download(g.copy())
-    pl = sd.plan
-    nl, nh, sl, sh = (int(x[rank]) for x in (pl.node_lo, pl.node_hi, pl.slot_lo, pl.slot_hi))
-    out = {"node": {f: h.node[f][nl:nh] for f in OUT_NODE}, "slot": {f: h.slot[f][sl:sh] for f in OUT_SLOT},
+    nodes, slots = sd.owned_host_nodes(), sd.owned_host_slots()
+    out = {"nodes": nodes, "slots": slots, "node": {f: h.node[f][nodes] for f in OUT_NODE},
+           "slot": {f: h.slot[f][slots] for f in OUT_SLOT},
            "replica": {f: h.node[f] for f in ("has_merged", "merged_state", "merged_cov")}, "act": h.slot["act"],
-           "flags": sd.d.errors()}
+           "flags": sd.d.errors(), "halo_bytes": sd.halo_bytes}
     q.put((rank, out))
     dist.barrier()
     dist.destroy_process_group()
@@ -138,11 +234,13 @@ def test_sharded_path_over_rccl_world1():
     _, res = q.get(timeout=300)
     p.join(60)
     assert p.exitcode == 0
+    nodes, slots = res["nodes"], res["slots"]
+    assert nodes.size == g.n_nodes and slots.size == g.n_slots
     for f in OUT_SLOT:
         a = res["slot"][f]
-        assert np.array_equal(a, ref.slot[f], equal_nan=a.dtype.kind == "f"), f
+        assert np.array_equal(a, ref.slot[f][slots], equal_nan=a.dtype.kind == "f"), f
     for f in OUT_NODE:
-        assert np.array_equal(res["node"][f], ref.node[f], equal_nan=True), f
+        assert np.array_equal(res["node"][f], ref.node[f][nodes], equal_nan=True), f
 
 
 @pytest.mark.gpu
@@ -160,15 +258,16 @@ def test_sharded_pass_equals_single_gpu_pass():
     for p in ps:
         p.join(60)
         assert p.exitcode == 0
-    pl = ShardPlan(g, world)
+    assert sorted(np.concatenate([res[r]["nodes"] for r in range(world)]).tolist()) == list(range(g.n_nodes))
     for r in range(world):
-        nl, nh, sl, sh = (int(x[r]) for x in (pl.node_lo, pl.node_hi, pl.slot_lo, pl.slot_hi))
+        nodes, slots = res[r]["nodes"], res[r]["slots"]
+        assert res[r]["flags"] == 0 and 0 < res[r]["halo_bytes"]
         for f in OUT_NODE:
-            assert np.array_equal(res[r]["node"][f], ref.node[f][nl:nh], equal_nan=True), (r, f)
+            assert np.array_equal(res[r]["node"][f], ref.node[f][nodes], equal_nan=True), (r, f)
         for f in OUT_SLOT:
-            a, b = res[r]["slot"][f], ref.slot[f][sl:sh]
+            a, b = res[r]["slot"][f], ref.slot[f][slots]
             assert np.array_equal(a, b, equal_nan=a.dtype.kind == "f"), (r, f)
-        # after the exchange every replica holds every rank's published state
+        # after sync() every replica holds every rank's published state
         for f in ("has_merged", "merged_state", "merged_cov"):
             assert np.array_equal(res[r]["replica"][f], ref.node[f], equal_nan=True), (r, f)
         assert np.array_equal(res[r]["act"], ref.slot["act"]), r

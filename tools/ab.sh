@@ -6,7 +6,7 @@ set -e
 mkdir -p gpurun_out/ab
 for r in 1 2; do
   for lib in "$@"; do
-    GTF_LIB=$PWD/gnn-track-finding_amd/gtf/$lib timeout -k 10 120 python -u bench.py --no-cpu --no-c5 --steps 50 --warmup 5 \
+    GTF_LIB=$PWD/gnn-track-finding_amd/gtf/$lib timeout -k 10 120 python -u bench.py --no-cpu --no-c5 --no-dropin --steps 50 --warmup 5 \
       > gpurun_out/ab/$lib.$r.json 2> gpurun_out/ab/$lib.$r.err
     python -c "import json,sys; d=json.load(open(sys.argv[1])); print(sys.argv[2], d['ms_per_step'], d['kernel_ms'])" gpurun_out/ab/$lib.$r.json $lib
   done

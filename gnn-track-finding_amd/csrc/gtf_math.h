@@ -72,6 +72,19 @@ __device__ __forceinline__ void pair_ij(int t, int& i, int& j) {
     j = t - r * (r - 1) / 2;
 }
 
+// x / d given r = 1.0 / d (correctly rounded): one product and two fused corrections give
+// the correctly rounded quotient, the same bits as x / d (Markstein's theorem: r = RN(1/d),
+// q = RN(x r), e = x - d q exactly, RN(q + e r) = RN(x / d); quotients near the ends of
+// the exponent range, zeros and non-finite operands take the division; checked on random,
+// adversarial and special operands in tests/test_numpy_rounding.py). A divisor
+// used k times then costs one division and k * 3 instructions instead of k divisions.
+__device__ __forceinline__ double qdiv(double x, double d, double r) {
+    const double q = x * r;
+    const double m = fabs(q);
+    if (m >= 0x1p-960 && m <= 0x1p+1000) return fma(fma(-q, d, x), r, q);
+    return x / d;   // zero, subnormal, huge, inf / NaN quotients (or d = 0, inf, NaN): divide
+}
+
 struct Cov5 {
     double c00, c01, c10, c11, c22;
 };

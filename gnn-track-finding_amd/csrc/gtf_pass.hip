@@ -67,7 +67,7 @@ __device__ __forceinline__ double highland_var_ms(double a, double b, const doub
     double q = (2.0 * a * nb[0]) + b;
     const double t15 = 1.0 + q * q;
     double kappa = (2.0 * a) / (t15 * sqrt(t15));  // (1 + q^2)**1.5
-    double t = ((13.6 * 1e-3 * sqrt(0.02)) * kappa) / 0.3;
+    double t = qdiv((13.6 * 1e-3 * sqrt(0.02)) * kappa, 0.3, 1.0 / 0.3);   // (a constant reciprocal)
     double var_ms = sin_t * (t * t);
     if (fabs(ng[2]) >= boundary) {
         double tan_t = fabs(dr) / fabs(dz);
@@ -194,12 +194,16 @@ __global__ void __launch_bounds__(BLOCK) k_extrapolate(gtf_graph g, gtf_nodes n,
 
     // cos/sin of atan2(y, x) as x/h, y/h (h = |(x, y)|): the same angles as the
     // reference's atan2 -> cos/sin round trips, to a couple of ulps, without fp64 libm
+    // (divisors used more than once: one correctly rounded reciprocal, then qdiv() -- the
+    // same bits as dividing each time)
     const double rA = sqrt(node_x * node_x + node_y * node_y);
-    const double ca = rA > 0.0 ? node_x / rA : 1.0, sa = rA > 0.0 ? node_y / rA : 0.0;       // :41
+    const double irA = 1.0 / rA;
+    const double ca = rA > 0.0 ? qdiv(node_x, rA, irA) : 1.0, sa = rA > 0.0 ? qdiv(node_y, rA, irA) : 0.0;  // :41
     const double x_A = (nbx - node_x) * ca + (nby - node_y) * sa;                              // :52
     const double py = (node_x * nby) - (node_y * nbx), px = (node_x * nbx) + (node_y * nby);  // :59
     const double hp = sqrt(px * px + py * py);
-    const double sp = hp > 0.0 ? py / hp : 0.0, cp = hp > 0.0 ? px / hp : 1.0;
+    const double ihp = 1.0 / hp;
+    const double sp = hp > 0.0 ? qdiv(py, hp, ihp) : 0.0, cp = hp > 0.0 ? qdiv(px, hp, ihp) : 1.0;
     const double x_prime = x_A + (c * sp);                                        // :63
     const double Vx = cp + (b * sp);
     const double Ax = a * sp;
@@ -208,19 +212,22 @@ __global__ void __launch_bounds__(BLOCK) k_extrapolate(gtf_graph g, gtf_nodes n,
     double numer = x_A + c * sp;                                                  // :82
     double denom = cp + b * sp;
     const double d2 = denom * denom;
+    const double id2 = 1.0 / d2;
     const double ds_da = -(sp * (numer * numer)) / (d2 * denom);
-    const double ds_db = ((sp * numer) * (1.0 + ((3.0 * a * sp * numer) / d2))) / d2;
-    const double ds_dc = (-sp * (1.0 + ((2.0 * a * sp * numer) / d2))) / denom;
+    const double ds_db = qdiv((sp * numer) * (1.0 + qdiv(3.0 * a * sp * numer, d2, id2)), d2, id2);
+    const double ds_dc = (-sp * (1.0 + qdiv(2.0 * a * sp * numer, d2, id2))) / denom;
     denom = cp + ((2.0 * a + b) * sp);                                             // :89
     const double e2 = denom * denom;
     const double da_da = (1.0 / (e2 * denom)) * (1.0 - ((6.0 * a * sp) * (s_star + a * ds_da) / denom));
-    const double da_db = (-3.0 * a * sp * ((2.0 * a * ds_db) + 1.0)) / (e2 * e2);
-    const double da_dc = (-6.0 * sp * ds_dc * (a * a)) / (e2 * e2);
+    const double e4 = e2 * e2, ie4 = 1.0 / e4;
+    const double da_db = qdiv(-3.0 * a * sp * ((2.0 * a * ds_db) + 1.0), e4, ie4);
+    const double da_dc = qdiv(-6.0 * sp * ds_dc * (a * a), e4, ie4);
     denom = cp + ((2.0 * a * s_star + b) * sp);                                    // :95
-    double bracket = cp - ((sp * (-sp + ((2.0 * a * s_star + b) * cp))) / denom);
-    const double db_da = (2.0 * (s_star + a * ds_da) * bracket) / denom;
-    const double db_db = ((1.0 + (2.0 * a * ds_da)) * bracket) / denom;
-    const double db_dc = (2.0 * a * ds_dc * bracket) / denom;
+    const double idn = 1.0 / denom;
+    double bracket = cp - qdiv(sp * (-sp + ((2.0 * a * s_star + b) * cp)), denom, idn);
+    const double db_da = qdiv(2.0 * (s_star + a * ds_da) * bracket, denom, idn);
+    const double db_db = qdiv((1.0 + (2.0 * a * ds_da)) * bracket, denom, idn);
+    const double db_dc = qdiv(2.0 * a * ds_dc * bracket, denom, idn);
     bracket = (cp * (2.0 * a + b)) - sp;                                           // :102
     const double dc_da = (ds_da * bracket) + ((s_star * s_star) * cp);
     const double dc_db = (ds_db * bracket) + (s_star * cp);
@@ -278,12 +285,14 @@ __global__ void __launch_bounds__(BLOCK) k_extrapolate(gtf_graph g, gtf_nodes n,
     // tau and its variance (:326-358) -- NOT squared here, unlike helper.py:421
     const double dr = nbr - node_r;
     const double dz = nbz - node_z;
-    const double tau = dz / dr;
+    const double J0 = 1.0 / dr;
+    const double tau = qdiv(dz, dr, J0);
     double sigma_r = p.sigma0rz, sigma_z = p.sigma0rz2;
     if (fabs(node_z) >= p.endcap_boundary) { sigma_z = p.sigma0rz; sigma_r = p.sigma0rz2; }
     double sigma_rn = p.sigma0rz, sigma_zn = p.sigma0rz2;
     if (fabs(nbz) >= p.endcap_boundary) { sigma_zn = p.sigma0rz; sigma_rn = p.sigma0rz2; }
-    const double J0 = 1.0 / dr, J1 = -1.0 / dr, J2 = (-dz) / (dr * dr), J3 = dz / (dr * dr);
+    // -1 / dr == -(1 / dr) and (-dz) / q == -(dz / q) exactly (round to nearest is symmetric)
+    const double J1 = -J0, J3 = dz / (dr * dr), J2 = -J3;
     double vt = (J0 * (sigma_z * sigma_z)) * J0;      // J @ S2 @ J.T (numpy ddot)
     vt = fma(J1 * (sigma_zn * sigma_zn), J1, vt);
     vt = fma(J2 * (sigma_r * sigma_r), J2, vt);

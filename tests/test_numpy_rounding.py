@@ -140,3 +140,33 @@ def test_clustering_functions(rng):
         res = (zb - za) / (rb - ra) - (zc - za) / (rc_ - ra)
         got = d1 + res ** 2 * (1 / cdt)
         assert got == O.mahalanobis_distance(m1, c1, m2, c2, na, nb, nc, 0.4, 0.6, 550.0)
+
+
+def qdiv(x, d, r):
+    """csrc/gtf_math.h qdiv: x / d from r = 1.0 / d"""
+    q = x * r
+    m = abs(q)
+    if 2.0 ** -960 <= m <= 2.0 ** 1000:
+        return fma(fma(-q, d, x), r, q)
+    return x / d if d != 0 else (np.float64(x) / np.float64(d))
+
+
+def test_shared_reciprocal_division_is_exact(rng):
+    """Markstein: with r = RN(1/d), RN(q + (x - d q) r) for q = RN(x r) is RN(x / d)"""
+    xs = list(rng.normal(size=40000) * 10.0 ** rng.uniform(-40, 40, 40000))
+    ds = list(rng.normal(size=40000) * 10.0 ** rng.uniform(-40, 40, 40000))
+    # significands near 1 and near 2 (the hard cases of reciprocal-based division)
+    m1 = 1 + rng.integers(0, 2 ** 52, 20000) / 2.0 ** 52
+    m2 = 2 - rng.integers(1, 2 ** 20, 20000) / 2.0 ** 52
+    e = rng.integers(-60, 60, (2, 20000))
+    xs += list(np.ldexp(m1, e[0])) + list(np.ldexp(m2, e[0]))
+    ds += list(np.ldexp(m2, e[1])) + list(np.ldexp(m1, e[1]))
+    with np.errstate(all="ignore"):
+        for x, d in zip(xs, ds):
+            x, d = float(x), float(d)
+            assert qdiv(x, d, 1.0 / d) == x / d
+        for x, d in ((0.0, 3.0), (-0.0, 3.0), (1.0, 1e308), (1e-300, 1e10), (5e-324, 3.0), (1e308, 1e-10),
+                     (2.0, float("inf")), (float("inf"), 2.0), (float("nan"), 2.0)):
+            ref = np.float64(x) / np.float64(d)
+            got = qdiv(x, d, float(np.float64(1.0) / np.float64(d)))
+            assert got == ref or (np.isnan(got) and np.isnan(ref)), (x, d)

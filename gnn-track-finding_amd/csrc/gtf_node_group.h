@@ -19,6 +19,12 @@
 #ifndef GTF_ABLATE
 #define GTF_ABLATE 0  // diagnostics builds only (tools/ablate_build.sh)
 #endif
+#ifndef GTF_HOIST
+#define GTF_HOIST 1   // the node's own scalars (x, xyzr, solo) loaded with the slot fields
+#endif
+#ifndef GTF_EARLY_STAGE
+#define GTF_EARLY_STAGE 0   // clustering operands loaded into LDS with the slot fields
+#endif
 
 template <int G>
 struct Grp {
@@ -127,6 +133,10 @@ struct NodeCtx {
     bool uts_dirty_lr, edge_mw_dirty;
     int degree;
     bool degree_set;
+    double node_x;             // GNN_Measurement x of the node (reweight side test)
+    double xa, za, ra;         // node attribute xyzr x, z, r (clustering tau geometry)
+    uint8_t solo;              // node alone in its subgraph (mixture weights)
+    bool staged;               // clustering operands already in the group's LDS stage (slot lanes)
 };
 
 // highest set bit index of m (m != 0)
@@ -162,6 +172,9 @@ __device__ __forceinline__ int dict_pos(const NodeCtx<G>& c, LaneDict& st) {
 // sum. Lanes write their term at their dict position in a per-group LDS line and
 // every lane adds the line in order; skipped entries add +0.0, which leaves the
 // running sum unchanged (it starts from the integer 0 of helper.py:165).
+#ifndef GTF_CHUNKED_SUM
+#define GTF_CHUNKED_SUM 1
+#endif
 template <int G>
 __device__ __forceinline__ double ordered_sum(NodeCtx<G>& c, double* sval, LaneDict& st, bool take,
                                              double term) {
@@ -170,9 +183,44 @@ __device__ __forceinline__ double ordered_sum(NodeCtx<G>& c, double* sval, LaneD
     if (pos >= 0) sval[c.grp.gbase + pos] = take ? term : 0.0;
     wave_lds_sync();
     double s = 0.0;
+#if GTF_CHUNKED_SUM
+    // the line is read CH entries at a time (independent LDS reads, one wait) and added in
+    // order; entries past the last key add +0.0, which leaves the sum unchanged (it is never
+    // -0.0: it starts at +0.0 and round-to-nearest cancellation gives +0.0)
+    constexpr int CH = G == 0 ? 1 : (G < 8 ? G : 8);   // chunks stay inside the group's line
+    for (int i = 0; i < npres; i += CH) {
+        double v[CH];
+#pragma unroll
+        for (int j = 0; j < CH; j++) v[j] = sval[c.grp.gbase + i + j];
+#pragma unroll
+        for (int j = 0; j < CH; j++) s = s + ((i + j < npres) ? v[j] : 0.0);
+    }
+#else
     for (int i = 0; i < npres; i++) s = s + sval[c.grp.gbase + i];
+#endif
     wave_lds_sync();
     return s;
+}
+
+#ifndef GTF_PAIRWISE_CLASSES
+#define GTF_PAIRWISE_CLASSES 1
+#endif
+// mask of the group's valid lanes whose value equals this lane's (a NaN equals nothing;
+// the caller adds the lane itself): every lane puts its value on the group's LDS line and
+// compares with all G entries -- independent reads instead of a leader-election chain of
+// ballots and shuffles (groups of up to 16 lanes)
+template <int G>
+__device__ __forceinline__ unsigned long long equal_lanes(const NodeCtx<G>& c, double* sval, double mine) {
+    sval[c.grp.gbase + c.grp.gl] = c.valid ? mine : NAN;
+    wave_lds_sync();
+    double v[G];
+#pragma unroll
+    for (int j = 0; j < G; j++) v[j] = sval[c.grp.gbase + j];
+    unsigned long long m = 0ull;
+#pragma unroll
+    for (int j = 0; j < G; j++) m |= (v[j] == mine) ? (1ull << j) : 0ull;
+    wave_lds_sync();
+    return c.valid ? m : 0ull;
 }
 
 template <int G>
@@ -184,7 +232,15 @@ __device__ __forceinline__ bool lane_active(const NodeCtx<G>& c, int rank) {
 // shares this key's layer. The same-layer masks are built once per node, one
 // iteration per distinct layer value (leader election with a ballot).
 template <int G>
-__device__ __forceinline__ void g_priors(NodeCtx<G>& c, LaneDict& st) {
+__device__ __forceinline__ void g_priors(NodeCtx<G>& c, LaneDict& st, double* sval) {
+#if GTF_PAIRWISE_CLASSES
+    if constexpr (G > 0 && G <= 16) {
+        if (!c.same_layer_ok) {
+            c.same_layer = equal_lanes(c, sval, c.layer) | (c.valid ? (1ull << c.grp.gl) : 0ull);
+            c.same_layer_ok = true;
+        }
+    }
+#endif
     if (!c.same_layer_ok) {
         bool done = !c.valid || c.layer != c.layer;  // NaN layers (orphans) never match
         c.same_layer = c.valid ? (1ull << c.grp.gl) : 0ull;
@@ -211,6 +267,7 @@ __device__ __forceinline__ void g_priors(NodeCtx<G>& c, LaneDict& st) {
 template <int G>
 __device__ __forceinline__ void g_reweight(NodeCtx<G>& c, double* sval, const double* gnn, double thr,
                                            uint32_t* err) {
+    (void)gnn;
     LaneDict& st = c.uts;
     const bool act = lane_active(c, st.rank);
     // last dict key = the present key with the largest rank (stale loop variable, :131,138);
@@ -224,12 +281,24 @@ __device__ __forceinline__ void g_reweight(NodeCtx<G>& c, double* sval, const do
     const int last = st.last;
     const int last_is_edge = c.grp.shfl((int)c.is_edge, last);
     const int last_act = c.grp.shfl((int)c.act, last);
+#if GTF_HOIST
+    const double node_x = c.node_x;
+#else
     const double node_x = gnn[4 * (int64_t)c.v];
+#endif
     const bool left = c.x0 < node_x;
     // distinct x values per side (len(set(coords))): the classes of equal stored x are
     // built once per node (one iteration per distinct value; a NaN is only equal to
     // itself, as set() keeps every NaN object); a key counts if it is the first active
     // key of its class -- equal x, same side
+#if GTF_PAIRWISE_CLASSES
+    if constexpr (G > 0 && G <= 16) {
+        if (!c.same_x_ok) {
+            c.same_x = equal_lanes(c, sval, c.x0) | (c.valid ? (1ull << c.grp.gl) : 0ull);
+            c.same_x_ok = true;
+        }
+    }
+#endif
     if (!c.same_x_ok) {
         bool done = !c.valid || c.x0 != c.x0;
         c.same_x = c.valid ? (1ull << c.grp.gl) : 0ull;
@@ -339,14 +408,32 @@ __device__ __forceinline__ void g_ranks(NodeCtx<G>& c) {
 // covariance and inverse (computed once per state: np.linalg.inv of a state's
 // covariance is the same value every time the reference recomputes it), and the
 // per-neighbour tau geometry of the pairwise chi2
+// Entries sit at the state's SLOT lane (its lane in the group), ord[dict position] maps a
+// dict position to it: the operands can then be staged before the ops have settled
+// which keys are present and in what order (GTF_EARLY_STAGE).
 template <int CAP>
 struct StageT {
     double a[CAP], b[CAP], c[CAP], tau[CAP];
     double c00[CAP], c01[CAP], c10[CAP], c11[CAP], c22[CAP];
     double i00[CAP], i01[CAP], i10[CAP], i11[CAP], i22[CAP];
-    double q[CAP], w[CAP], tg[CAP], prior[CAP];
+    double q[CAP], w[CAP], tg[CAP], prior[CAP];   // (early staging parks x, z, r in q, w, tg)
     uint8_t ec[CAP];  // neighbour in the endcap (|x| >= boundary): picks its sigma_z / sigma_r pair
+    uint8_t ord[CAP]; // slot lane of the state at each dict position
 };
+
+// the clustering operands of this lane's state, raw, at its slot lane
+template <typename Stage>
+__device__ __forceinline__ void stage_raw(Stage* stg, int li, const gtf_states& S, int64_t k) {
+    stg->a[li] = S.sv[3 * k];
+    stg->b[li] = S.sv[3 * k + 1];
+    stg->c[li] = S.sv[3 * k + 2];
+    stg->tau[li] = S.tau[k];
+    const double* cv = S.cov + 5 * k;
+    stg->c00[li] = cv[0]; stg->c01[li] = cv[1]; stg->c10[li] = cv[2]; stg->c11[li] = cv[3]; stg->c22[li] = cv[4];
+    stg->q[li] = S.xyzr[4 * k];
+    stg->w[li] = S.xyzr[4 * k + 2];
+    stg->tg[li] = S.xyzr[4 * k + 3];
+}
 
 template <typename Stage>
 __device__ __forceinline__ Cov5 stage_cov(const Stage* s, int i) {
@@ -383,25 +470,25 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
     if (d <= 2 || d >= 16) return;                                                 // :207
     const int pos = dict_pos(c, st);
     const int sb = c.grp.stage_base();   // this group's first entry in the stage arrays
+    const int me_l = sb + c.grp.gl;      // this lane's entry (its slot lane)
+#if GTF_HOIST
+    (void)xyzr_node;
+    const double xa = c.xa, za = c.za, ra = c.ra;
+#else
     const double xa = xyzr_node[0], za = xyzr_node[2], ra = xyzr_node[3];
+#endif
     if (pres) {
-        const int64_t k = c.k;
-        stg->a[sb + pos] = S.sv[3 * k];
-        stg->b[sb + pos] = S.sv[3 * k + 1];
-        stg->c[sb + pos] = S.sv[3 * k + 2];
-        stg->tau[sb + pos] = S.tau[k];
-        const double* cv = S.cov + 5 * k;
-        const Cov5 C{cv[0], cv[1], cv[2], cv[3], cv[4]};
+        if (!c.staged) stage_raw(stg, me_l, S, c.k);
+        const Cov5 C = stage_cov(stg, me_l);
+        const double x = stg->q[me_l], z = stg->w[me_l], r = stg->tg[me_l];
         const Cov5 I = inv_cov5(C);
-        stg->c00[sb + pos] = C.c00; stg->c01[sb + pos] = C.c01; stg->c10[sb + pos] = C.c10; stg->c11[sb + pos] = C.c11;
-        stg->c22[sb + pos] = C.c22;
-        stg->i00[sb + pos] = I.c00; stg->i01[sb + pos] = I.c01; stg->i10[sb + pos] = I.c10; stg->i11[sb + pos] = I.c11;
-        stg->i22[sb + pos] = I.c22;
-        const TauGeo t = tau_geo(S.xyzr[4 * k], S.xyzr[4 * k + 2], S.xyzr[4 * k + 3], za, ra, p.sigma0rz2, p.sigma0rz,
-                                 p.sigma0rz, p.sigma0rz2, p.endcap_boundary);
-        stg->q[sb + pos] = t.q; stg->w[sb + pos] = t.w; stg->tg[sb + pos] = t.tau;
-        stg->ec[sb + pos] = fabs(S.xyzr[4 * k]) >= p.endcap_boundary;
-        stg->prior[sb + pos] = st.prior;
+        stg->i00[me_l] = I.c00; stg->i01[me_l] = I.c01; stg->i10[me_l] = I.c10; stg->i11[me_l] = I.c11;
+        stg->i22[me_l] = I.c22;
+        const TauGeo t = tau_geo(x, z, r, za, ra, p.sigma0rz2, p.sigma0rz, p.sigma0rz, p.sigma0rz2, p.endcap_boundary);
+        stg->q[me_l] = t.q; stg->w[me_l] = t.w; stg->tg[me_l] = t.tau;
+        stg->ec[me_l] = fabs(x) >= p.endcap_boundary;
+        stg->prior[me_l] = st.prior;
+        stg->ord[sb + pos] = (uint8_t)c.grp.gl;
     }
     wave_lds_sync();
     const double szb2 = p.sigma0rz2 * p.sigma0rz2, srb2 = p.sigma0rz * p.sigma0rz;   // barrel sigma_z^2, sigma_r^2
@@ -416,9 +503,10 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
     for (int t = c.grp.gl; t < npairs; t += c.grp.size()) {
         int i, j;
         pair_ij(t, i, j);
-        const double D = mahalanobis_geo(stg->a[sb + i], stg->b[sb + i], stage_cov(stg, sb + i), stg->a[sb + j], stg->b[sb + j],
-                                         stage_cov(stg, sb + j), sza2, sra2, stage_geo(stg, sb + i, szb2, srb2),
-                                         stage_geo(stg, sb + j, szb2, srb2));
+        const int li = sb + stg->ord[sb + i], lj = sb + stg->ord[sb + j];
+        const double D = mahalanobis_geo(stg->a[li], stg->b[li], stage_cov(stg, li), stg->a[lj], stg->b[lj],
+                                         stage_cov(stg, lj), sza2, sra2, stage_geo(stg, li, szb2, srb2),
+                                         stage_geo(stg, lj, szb2, srb2));
         if (D == 0.0) continue;  // zeros are excluded (np.nonzero)
         lnz = true;
         if (D != D) { lnan = true; continue; }
@@ -450,17 +538,18 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
     const int p0 = ti0, p1 = (t1 < (1 << 20)) ? ti1 : tj0;
     double pm[3], jm[3];
     Cov5 mc;
+    const int l0 = sb + stg->ord[sb + p0], l1 = sb + stg->ord[sb + p1];
     {
-        const Cov5 i0 = stage_inv(stg, sb + p0), i1 = stage_inv(stg, sb + p1);
+        const Cov5 i0 = stage_inv(stg, l0), i1 = stage_inv(stg, l1);
         mc = inv_cov5(add_cov5(i0, i1));
-        const double ps0[3] = {stg->a[sb + p0], stg->b[sb + p0], stg->c[sb + p0]};
-        const double ps1[3] = {stg->a[sb + p1], stg->b[sb + p1], stg->c[sb + p1]};
-        const double js0[3] = {ps0[0], ps0[1], stg->tau[sb + p0]};
-        const double js1[3] = {ps1[0], ps1[1], stg->tau[sb + p1]};
+        const double ps0[3] = {stg->a[l0], stg->b[l0], stg->c[l0]};
+        const double ps1[3] = {stg->a[l1], stg->b[l1], stg->c[l1]};
+        const double js0[3] = {ps0[0], ps0[1], stg->tau[l0]};
+        const double js1[3] = {ps1[0], ps1[1], stg->tau[l1]};
         merge_with_inv(ps0, i0, ps1, i1, mc, pm);
         merge_with_inv(js0, i0, js1, i1, mc, jm);
     }
-    double mprior = stg->prior[sb + p0] + stg->prior[sb + p1];
+    double mprior = stg->prior[l0] + stg->prior[l1];
     unsigned alive = ((1u << d) - 1u) & ~tiemask;
     if (alive == 0) {
         if (c.grp.gl == 0) atomicOr(err, (uint32_t)GTF_ERR_TIE_EMPTIED);
@@ -471,8 +560,8 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
             double D = INFINITY;
             bool dn = false;
             if (me) {
-                const double js_me[3] = {stg->a[sb + pos], stg->b[sb + pos], stg->tau[sb + pos]};
-                D = kl_with_inv(js_me, stage_cov(stg, sb + pos), stage_inv(stg, sb + pos), jm, mc, im);
+                const double js_me[3] = {stg->a[me_l], stg->b[me_l], stg->tau[me_l]};
+                D = kl_with_inv(js_me, stage_cov(stg, me_l), stage_inv(stg, me_l), jm, mc, im);
                 if (D != D) { dn = true; D = INFINITY; }
             }
             if (c.grp.any(dn)) {
@@ -482,17 +571,18 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
             const double mind = c.grp.min_d(D);
             if (!(mind < kl_thr)) break;
             const int m = c.grp.min_i((me && D == mind) ? pos : 99);  // first minimum (list.index)
-            const Cov5 ii = stage_inv(stg, sb + m);
+            const int lm = sb + stg->ord[sb + m];
+            const Cov5 ii = stage_inv(stg, lm);
             const Cov5 nmc = inv_cov5(add_cov5(ii, im));
-            const double ps[3] = {stg->a[sb + m], stg->b[sb + m], stg->c[sb + m]};
-            const double js[3] = {ps[0], ps[1], stg->tau[sb + m]};
+            const double ps[3] = {stg->a[lm], stg->b[lm], stg->c[lm]};
+            const double js[3] = {ps[0], ps[1], stg->tau[lm]};
             double npm[3], njm[3];
             merge_with_inv(ps, ii, pm, im, nmc, npm);
             merge_with_inv(js, ii, jm, im, nmc, njm);
             pm[0] = npm[0]; pm[1] = npm[1]; pm[2] = npm[2];
             jm[0] = njm[0]; jm[1] = njm[1]; jm[2] = njm[2];
             mc = nmc;
-            mprior = stg->prior[sb + m] + mprior;
+            mprior = stg->prior[lm] + mprior;
             alive &= ~(1u << m);
             if (alive == 0) break;
         }
@@ -515,6 +605,7 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
 // the per-slot fields an op sequence reads from memory (the others it only writes)
 struct Need {
     bool tse_rank, tse_prior, uts_rank, uts_mw, uts_prior, uts_lik, uts_x0, uts_fresh, send_mw;
+    bool node_x, node_xyzr, solo;   // the node's own scalars an op reads
 };
 
 template <int G>
@@ -564,6 +655,17 @@ __device__ __forceinline__ bool node_fields(NodeCtx<G>& c, const gtf_graph& g, c
     c.uts = LaneDict{-1, 0.0, 0.0, 0, -1, false, 0, false};
     c.lik = 0; c.lr = 0; c.x0 = 0; c.edge_mw = 0; c.side = -1; c.fresh = 0;
     c.uts_dirty_lr = false; c.edge_mw_dirty = false; c.degree = 0; c.degree_set = false;
+    c.staged = false;
+#if GTF_HOIST
+    // the node's own scalars, in the same round of loads as the slot fields (loaded inside
+    // an op, after its LDS fences, each one's latency would add to every wave's life)
+    if (nd.node_x) c.node_x = g.gnn[4 * (int64_t)c.v];
+    if (nd.node_xyzr) {
+        const double* xn = g.xyzr + 4 * (int64_t)c.v;
+        c.xa = xn[0]; c.za = xn[2]; c.ra = xn[3];
+    }
+    if (nd.solo) c.solo = g.solo[c.v];
+#endif
     // only what an op reads: mw of the TSE dict, lr and side are written, never read
     // (the reweight sets lr / side of every key it weighs before using them)
     if (c.valid) {
@@ -609,13 +711,18 @@ __device__ __forceinline__ void node_op(NodeCtx<G>& c, const gtf_graph& g, gtf_n
                                         bool has_uts) {
     if constexpr (OP == OP_FRESH) g_fresh(c);
     if constexpr (OP == OP_RANKS) g_ranks(c);
-    if constexpr (OP == OP_PRIORS_TSE) { if (has_tse) g_priors(c, c.tse); }
-    if constexpr (OP == OP_PRIORS_UTS) { if (has_uts) g_priors(c, c.uts); }
+    if constexpr (OP == OP_PRIORS_TSE) { if (has_tse) g_priors(c, c.tse, sval); }
+    if constexpr (OP == OP_PRIORS_UTS) { if (has_uts) g_priors(c, c.uts, sval); }
     if constexpr (OP == OP_REWEIGHT_UTS) { if (has_uts) g_reweight(c, sval, g.gnn, p.reweight_threshold, w.err); }
     if constexpr (OP == OP_DEGREE) g_degree(c);
     if constexpr (OP == OP_PRUNE) g_prune(c, has_tse, has_uts, w.err);
+#if GTF_HOIST
+    if constexpr (OP == OP_MW_TSE) { if (has_tse) g_mixture_weights(c, c.tse, c.solo, w.err); }
+    if constexpr (OP == OP_MW_UTS) { if (has_uts) g_mixture_weights(c, c.uts, c.solo, w.err); }
+#else
     if constexpr (OP == OP_MW_TSE) { if (has_tse) g_mixture_weights(c, c.tse, g.solo[c.v], w.err); }
     if constexpr (OP == OP_MW_UTS) { if (has_uts) g_mixture_weights(c, c.uts, g.solo[c.v], w.err); }
+#endif
     if constexpr (OP == OP_CLUSTER_TSE) {
         if (has_tse) g_cluster(c, n, tse, c.tse, stg, g.xyzr + 4 * (int64_t)c.v, chi2_thr, kl_thr, p, w.err);
     }
@@ -633,9 +740,11 @@ struct OpSeq {
     static constexpr bool cluster = ((OPS == OP_CLUSTER_TSE || OPS == OP_CLUSTER_UTS) || ...);
     static constexpr bool reweight = ((OPS == OP_REWEIGHT_UTS) || ...);
     static constexpr bool fresh = ((OPS == OP_FRESH) || ...);
+    static constexpr bool cluster_uts = ((OPS == OP_CLUSTER_UTS) || ...);
     static constexpr Need need{uses_tse, ((OPS == OP_CLUSTER_TSE) || ...), uses_uts, reweight,
-                               reweight || ((OPS == OP_CLUSTER_UTS) || ...), reweight, reweight,
-                               ((OPS == OP_RANKS) || ...) || fresh, fresh};
+                               reweight || cluster_uts, reweight, reweight,
+                               ((OPS == OP_RANKS) || ...) || fresh, fresh,
+                               reweight, cluster, ((OPS == OP_MW_TSE || OPS == OP_MW_UTS) || ...)};
 };
 
 // has_uts of the node; where the sequence finishes message passing (OP_FRESH) a node that
@@ -665,12 +774,25 @@ __device__ __forceinline__ void node_seq_body(const gtf_graph& g, gtf_nodes& n, 
                                               double kl_thr, const int32_t* list, const int32_t* seg, int count,
                                               int bid, char* smem) {
     using Q = OpSeq<OPS...>;
-    using Stage = StageT<(G < 16 ? G : 16)>;
+    using Stage = StageT<G>;
     NodeCtx<G> c;
     const int gi = (bid * BLOCK + (int)threadIdx.x) / G;
     if (!node_load(c, g, n, tse, uts, e, list, seg, count, gi, Q::need)) return;
     double* sval = (double*)smem + (threadIdx.x & ~63);
     Stage* stg = (Stage*)(smem + BLOCK * sizeof(double)) + (Q::cluster ? (int)threadIdx.x / G : 0);
+#if GTF_EARLY_STAGE
+    // the clustering operands of every slot of a node that may cluster (>= 3 slots), read
+    // with the slot fields and parked in the group's LDS stage at the slot lane
+    if constexpr (Q::cluster && G > 2) {
+        c.staged = c.d >= 3;   // group-uniform
+#if GTF_EARLY_STAGE == 2
+        const bool maybe = c.valid && (Q::cluster_uts ? (c.uts.rank >= 0 || c.fresh) : c.tse.rank >= 0);
+#else
+        const bool maybe = c.valid;
+#endif
+        if (c.staged && maybe) stage_raw(stg, c.grp.gl, Q::cluster_uts ? uts : tse, c.k);
+    }
+#endif
     const bool has_tse = n.has_tse[c.v];
     const bool has_uts = fresh_has_uts(c, n, Q::fresh);
 #if GTF_ABLATE == 4
@@ -690,7 +812,7 @@ struct Buckets {
 };
 
 template <int G>
-constexpr size_t stage_bytes() { return (size_t)(BLOCK / G) * sizeof(StageT<(G < 16 ? G : 16)>); }
+constexpr size_t stage_bytes() { return (size_t)(BLOCK / G) * sizeof(StageT<G>); }
 constexpr size_t node_smem_bytes() {
     size_t m = stage_bytes<2>();
     m = stage_bytes<4>() > m ? stage_bytes<4>() : m;
@@ -799,14 +921,14 @@ __global__ void __launch_bounds__(BLOCK) k_node_group(gtf_graph g, gtf_nodes n, 
                                                       gtf_edges e, gtf_params p, Ws w, NodeOps ops,
                                                       double chi2_thr, double kl_thr, const int32_t* list,
                                                       const int32_t* seg, int count) {
-    using Stage = StageT<(G < 16 ? G : 16)>;
+    using Stage = StageT<G>;
     __shared__ double s_val[BLOCK];
     __shared__ Stage s_stage[BLOCK / G];
     NodeCtx<G> c;
     const int gi = (blockIdx.x * BLOCK + (int)threadIdx.x) / G;
     const Need nd{(bool)ops.uses_tse, (bool)ops.uses_tse, (bool)ops.uses_uts, (bool)ops.uses_uts,
                   (bool)ops.uses_uts, (bool)ops.uses_uts, (bool)ops.uses_uts, (bool)ops.uses_uts,
-                  (bool)ops.uses_uts};
+                  (bool)ops.uses_uts, true, true, true};
     if (!node_load(c, g, n, tse, uts, e, list, seg, count, gi, nd)) return;
     double* sval = s_val + (threadIdx.x & ~63);
     Stage* stg = s_stage + (int)threadIdx.x / G;

@@ -203,8 +203,9 @@ __device__ __forceinline__ double ordered_sum(NodeCtx<G>& c, double* sval, LaneD
 }
 
 #ifndef GTF_PAIRWISE_CLASSES
-#define GTF_PAIRWISE_CLASSES 1
+#define GTF_PAIRWISE_CLASSES 1   // 1: groups of up to 16 lanes, 2: every group size
 #endif
+constexpr int PAIRWISE_MAX_G = GTF_PAIRWISE_CLASSES >= 2 ? 64 : 16;
 // mask of the group's valid lanes whose value equals this lane's (a NaN equals nothing;
 // the caller adds the lane itself): every lane puts its value on the group's LDS line and
 // compares with all G entries -- independent reads instead of a leader-election chain of
@@ -213,12 +214,16 @@ template <int G>
 __device__ __forceinline__ unsigned long long equal_lanes(const NodeCtx<G>& c, double* sval, double mine) {
     sval[c.grp.gbase + c.grp.gl] = c.valid ? mine : NAN;
     wave_lds_sync();
-    double v[G];
-#pragma unroll
-    for (int j = 0; j < G; j++) v[j] = sval[c.grp.gbase + j];
     unsigned long long m = 0ull;
+    constexpr int CH = G < 16 ? G : 16;
 #pragma unroll
-    for (int j = 0; j < G; j++) m |= (v[j] == mine) ? (1ull << j) : 0ull;
+    for (int i = 0; i < G; i += CH) {
+        double v[CH];
+#pragma unroll
+        for (int j = 0; j < CH; j++) v[j] = sval[c.grp.gbase + i + j];
+#pragma unroll
+        for (int j = 0; j < CH; j++) m |= (v[j] == mine) ? (1ull << (i + j)) : 0ull;
+    }
     wave_lds_sync();
     return c.valid ? m : 0ull;
 }
@@ -234,7 +239,7 @@ __device__ __forceinline__ bool lane_active(const NodeCtx<G>& c, int rank) {
 template <int G>
 __device__ __forceinline__ void g_priors(NodeCtx<G>& c, LaneDict& st, double* sval) {
 #if GTF_PAIRWISE_CLASSES
-    if constexpr (G > 0 && G <= 16) {
+    if constexpr (G > 0 && G <= PAIRWISE_MAX_G) {
         if (!c.same_layer_ok) {
             c.same_layer = equal_lanes(c, sval, c.layer) | (c.valid ? (1ull << c.grp.gl) : 0ull);
             c.same_layer_ok = true;
@@ -292,7 +297,7 @@ __device__ __forceinline__ void g_reweight(NodeCtx<G>& c, double* sval, const do
     // itself, as set() keeps every NaN object); a key counts if it is the first active
     // key of its class -- equal x, same side
 #if GTF_PAIRWISE_CLASSES
-    if constexpr (G > 0 && G <= 16) {
+    if constexpr (G > 0 && G <= PAIRWISE_MAX_G) {
         if (!c.same_x_ok) {
             c.same_x = equal_lanes(c, sval, c.x0) | (c.valid ? (1ull << c.grp.gl) : 0ull);
             c.same_x_ok = true;

@@ -124,6 +124,35 @@ __device__ __forceinline__ void sender_scan(const gtf_graph& g, gtf_nodes& n, co
     if (gl == 0) n.merged_cov[5 * (int64_t)u + 3] = carry;
 }
 
+// one sender u whose out-edges fit the group (<= G), lane gl holding out-edge slot k
+// (-1 past the end) with receiver v from gtf_graph.out_lanes: every load of the scan
+// is issued in one round, beside the sender's own fields
+template <int G>
+__device__ __forceinline__ void sender_scan_lane(const gtf_graph& g, gtf_nodes& n, const gtf_edges& e,
+                                                 const gtf_params& p, const Ws& w, int u, int k, int v, int gl) {
+    const uint8_t hm = n.has_merged[u];
+    const double a = n.merged_state[3 * (int64_t)u + 0];
+    const double b = n.merged_state[3 * (int64_t)u + 1];
+    const double ng[4] = {g.gnn[4 * (int64_t)u], g.gnn[4 * (int64_t)u + 1], g.gnn[4 * (int64_t)u + 2],
+                          g.gnn[4 * (int64_t)u + 3]};
+    const double carry = n.merged_cov[5 * (int64_t)u + 3];
+    const int kk = k >= 0 ? k : 0;
+    const double nb[4] = {g.gnn[4 * (int64_t)v], g.gnn[4 * (int64_t)v + 1], g.gnn[4 * (int64_t)v + 2],
+                          g.gnn[4 * (int64_t)v + 3]};
+    const uint8_t act = e.act[kk];
+    if (!hm) return;   // group-uniform
+    double vm = -1.0;
+    if (k >= 0 && act == 1) vm = highland_var_ms(a, b, ng, nb, p.endcap_boundary);
+    double c = carry;
+    for (int m = 0; m < G; m++) {
+        const double vmm = __shfl(vm, m, G);
+        if (m <= gl && vmm != -1.0) c = c + vmm;
+    }
+    if (vm != -1.0) w.vc[k] = make_double2(vm, c);
+    const double fin = __shfl(c, G - 1, G);   // the last lane has every active edge's term
+    if (gl == 0) n.merged_cov[5 * (int64_t)u + 3] = fin;
+}
+
 // every node (list NULL) or a list of senders (a shard's), 8 lanes per sender
 constexpr int SG = 8;
 __global__ void __launch_bounds__(BLOCK) k_sender(gtf_graph g, gtf_nodes n, gtf_edges e, gtf_params p, Ws w,
@@ -142,6 +171,7 @@ struct SendBuckets {
     const int4* list[3];
     int32_t count[3];
     int32_t blocks[3];  // padded to multiples of 8
+    const int2* lanes[2];  // gtf_graph.out_lanes of the 4- and 8-lane buckets, or NULL
 };
 
 template <int G>
@@ -154,12 +184,32 @@ __device__ __forceinline__ void sender_bucket(const gtf_graph& g, gtf_nodes& n, 
     sender_scan<G>(g, n, e, p, w, en.x, en.y, en.z, threadIdx.x & (G - 1));
 }
 
+template <int G>
+__device__ __forceinline__ void sender_bucket_lanes(const gtf_graph& g, gtf_nodes& n, const gtf_edges& e,
+                                                    const gtf_params& p, const Ws& w, const int4* list,
+                                                    const int2* lanes, int count, int b, int nb) {
+    const int t = xcd_local(b, nb) * BLOCK + (int)threadIdx.x;
+    const int gi = t / G;
+    if (gi >= count) return;  // group-uniform
+    const int u = list[gi].x;
+    const int2 kv = lanes[t];  // lane t of the bucket = lane (t % G) of entry gi
+    sender_scan_lane<G>(g, n, e, p, w, u, kv.x, kv.y, t & (G - 1));
+}
+
 __global__ void __launch_bounds__(BLOCK) k_sender_sched(gtf_graph g, gtf_nodes n, gtf_edges e, gtf_params p, Ws w,
                                                         SendBuckets sb) {
     int b = blockIdx.x;
-    if (b < sb.blocks[0]) { sender_bucket<4>(g, n, e, p, w, sb.list[0], sb.count[0], b, sb.blocks[0]); return; }
+    if (b < sb.blocks[0]) {
+        if (sb.lanes[0]) sender_bucket_lanes<4>(g, n, e, p, w, sb.list[0], sb.lanes[0], sb.count[0], b, sb.blocks[0]);
+        else sender_bucket<4>(g, n, e, p, w, sb.list[0], sb.count[0], b, sb.blocks[0]);
+        return;
+    }
     b -= sb.blocks[0];
-    if (b < sb.blocks[1]) { sender_bucket<8>(g, n, e, p, w, sb.list[1], sb.count[1], b, sb.blocks[1]); return; }
+    if (b < sb.blocks[1]) {
+        if (sb.lanes[1]) sender_bucket_lanes<8>(g, n, e, p, w, sb.list[1], sb.lanes[1], sb.count[1], b, sb.blocks[1]);
+        else sender_bucket<8>(g, n, e, p, w, sb.list[1], sb.count[1], b, sb.blocks[1]);
+        return;
+    }
     b -= sb.blocks[1];
     sender_bucket<16>(g, n, e, p, w, sb.list[2], sb.count[2], b, sb.blocks[2]);
 }
@@ -665,6 +715,13 @@ int launch_extrap_edges(const gtf_graph* g, gtf_nodes* n, gtf_states* uts, gtf_e
             const int cnt[3] = {g->n_o4, g->n_o8, g->n_o16}, gs[3] = {4, 8, 16};
             const int4* l = reinterpret_cast<const int4*>(g->out_sched);
             int total = 0;
+#ifdef GTF_NO_OUT_LANES   // diagnostics build: the scan without the per-lane table
+            const int2* ln = nullptr;
+#else
+            const int2* ln = reinterpret_cast<const int2*>(g->out_lanes);
+#endif
+            sb.lanes[0] = ln;
+            sb.lanes[1] = ln ? ln + 4 * g->n_o4 : nullptr;
             for (int q = 0; q < 3; q++) {
                 sb.list[q] = l;
                 l += cnt[q];

@@ -16,7 +16,7 @@ F64 = ctypes.c_double
 
 
 U32 = ctypes.c_uint32
-ABI_VERSION = 2   # GTF_ABI_VERSION of include/gtf.h
+ABI_VERSION = 3   # GTF_ABI_VERSION of include/gtf.h
 
 
 class GtfGraph(ctypes.Structure):
@@ -29,7 +29,7 @@ class GtfGraph(ctypes.Structure):
                 ("sched", P), ("n_g8", I32), ("n_g16", I32), ("n_g32", I32), ("n_g64", I32), ("out_dst", P),
                 ("slot_layer", P), ("n_g4", I32), ("sched_seg", P),
                 ("out_sched", P), ("n_o4", I32), ("n_o8", I32), ("n_o16", I32), ("n_g2", I32),
-                ("pack_ent", P), ("pack_wave", P), ("n_pack_waves", I32)]
+                ("pack_ent", P), ("pack_wave", P), ("n_pack_waves", I32), ("out_lanes", P)]
 
     def __init__(self, **fields):
         super().__init__(**fields)

@@ -48,6 +48,25 @@ def sender_schedule(out_ptr, nodes=None):
     return q, [int(x.size) for x in parts]
 
 
+def sender_lanes(out_slot, out_dst, q, counts):
+    """gtf_graph.out_lanes: for every lane of the 4- and 8-lane entries of the sender
+    schedule `q` (sender_schedule), (slot, receiver) of the lane's out-edge or (-1, 0)"""
+    q = np.asarray(q, dtype=np.int64).reshape(-1, 4)
+    os_ = np.asarray(out_slot, dtype=np.int64)
+    od = np.asarray(out_dst, dtype=np.int64)
+    parts, at = [], 0
+    for G, n in ((4, counts[0]), (8, counts[1])):
+        e = q[at:at + n]
+        at += n
+        idx = e[:, 1:2] + np.arange(G)[None, :]
+        ok = idx < e[:, 2:3]
+        safe = np.minimum(idx, max(os_.size - 1, 0))
+        k = np.where(ok, os_[safe] if os_.size else -1, -1)
+        v = np.where(ok, od[safe] if od.size else 0, 0)
+        parts.append(np.stack([k, v], axis=2).reshape(-1))
+    return np.concatenate(parts).astype(np.int32) if parts else np.zeros(0, np.int32)
+
+
 def pack_schedule(slot_ptr):
     """gtf_graph.pack_ent / pack_wave: the nodes with <= 64 slots, largest first, packed
     greedily into wavefronts of 64 lanes (one lane per slot, one for a slot-free node);
@@ -156,6 +175,7 @@ class DeviceGraph:
         up("sched_seg", sched_segments(g.slot_ptr, sched))
         osched, self.n_o = sender_schedule(g.out_ptr)
         up("out_sched", osched)
+        up("out_lanes", sender_lanes(g.out_slot, self.t["out_dst"].cpu().numpy(), osched, self.n_o))
         self.n_pack_waves = 0
         if pack:   # the packed lane segments are built only when asked for
             pent, pwave = pack_schedule(g.slot_ptr)
@@ -217,7 +237,7 @@ class DeviceGraph:
         sched = dict(n_big=self.n_big, sched=p("sched"), n_g4=self.n_g_all[0], n_g8=self.n_g_all[1],
                      n_g16=self.n_g_all[2], n_g32=self.n_g_all[3], n_g64=self.n_g_all[4], sched_seg=p("sched_seg"),
                      out_sched=p("out_sched"), n_o4=self.n_o[0], n_o8=self.n_o[1], n_o16=self.n_o[2],
-                     n_g2=self.n_g2)
+                     n_g2=self.n_g2, out_lanes=p("out_lanes"))
         if not self.use_sched:   # thread per node, 8-lane sender scan
             self.cg = nat.GtfGraph(**base)
         elif pack and self.n_pack_waves:
@@ -439,3 +459,37 @@ class DeviceGraph:
             return
         for k, v in snap.items():
             self.t[k].copy_(v, non_blocking=True)
+
+    # ------------------------------------------------ staged copies of the pass input
+    def stage_inputs(self, k: int):
+        """k device copies of the pass-input arena (PASS_INPUTS), each with its own C structs,
+        for a benchmark whose steps each run one pass over a resident, identical input without
+        a restore copy between them: use_inputs(i) points every stage method at copy i
+        (None: the arrays of this graph). The arrays outside the arena (state values,
+        degree) are shared: a pass overwrites every value it reads back."""
+        self._resident = (self.cn, self.cuts, self.ctse, self.ce)
+        lo = self.arena.data_ptr()
+        hi = lo + self.arena.numel()
+
+        def rebase(st, off):
+            vals = []
+            for name, typ in st._fields_:
+                v = getattr(st, name)
+                if typ is ctypes.c_void_p and v is not None and lo <= v < hi:
+                    v = v + off
+                vals.append(v)
+            return type(st)(*vals)
+
+        self._staged = []
+        for _ in range(k):
+            a = self.torch.empty_like(self.arena)
+            off = a.data_ptr() - lo
+            self._staged.append((a, tuple(rebase(s, off) for s in self._resident)))
+
+    def fill_inputs(self, snap):
+        """copy the pass-input snapshot into every staged copy"""
+        for a, _ in self._staged:
+            a.copy_(snap["__arena__"], non_blocking=True)
+
+    def use_inputs(self, i):
+        self.cn, self.cuts, self.ctse, self.ce = self._resident if i is None else self._staged[i][1]

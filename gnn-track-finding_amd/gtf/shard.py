@@ -235,7 +235,7 @@ class ShardedDeviceGraph:
     def __init__(self, g: TrackGraph, rank: int, world: int, device="cuda", backend="nccl", group=None,
                  tile: int = None):
         import torch
-        from .device import DeviceGraph, TILE, sched_segments
+        from .device import DeviceGraph, TILE, sched_segments, sender_lanes
         self.torch = torch
         self.rank, self.world, self.backend, self.group = rank, world, backend, group
         gd, order, slot_perm, cuts = shard_layout(g, world, TILE if tile is None else tile)
@@ -254,6 +254,7 @@ class ShardedDeviceGraph:
         self.sched_seg = up(sched_segments(gd.slot_ptr, sched))
         osched, n_o = pl.sender_schedule(rank)
         self.out_sched = up(osched)
+        self.out_lanes = up(sender_lanes(d.t["out_slot"].cpu().numpy(), d.t["out_dst"].cpu().numpy(), osched, n_o))
         self.ranges = up(pl.ranges())
         p = d.ptr
         self.cg = nat.GtfGraph(n_nodes=d.n_nodes, n_slots=d.n_slots, n_edges=d.n_edges, n_big=n_big,
@@ -263,7 +264,8 @@ class ShardedDeviceGraph:
                                xyzr=p("xyzr"), layer=p("layer"), sched=vp(self.sched), n_g4=n_g[0], n_g8=n_g[1],
                                n_g16=n_g[2], n_g32=n_g[3], n_g64=n_g[4], out_dst=p("out_dst"),
                                slot_layer=p("slot_layer"), sched_seg=vp(self.sched_seg),
-                               out_sched=vp(self.out_sched), n_o4=n_o[0], n_o8=n_o[1], n_o16=n_o[2], n_g2=n_g2)
+                               out_sched=vp(self.out_sched), n_o4=n_o[0], n_o8=n_o[1], n_o16=n_o[2], n_g2=n_g2,
+                               out_lanes=vp(self.out_lanes))
         self.shard = nat.GtfShard(vp(self.senders), int(self.senders.numel()), int(pl.node_lo[rank]),
                                   int(pl.node_hi[rank]), int(pl.slot_lo[rank]), int(pl.slot_hi[rank]))
         # halo exchange buffers and lists (fixed per plan)

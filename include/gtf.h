@@ -40,7 +40,7 @@ typedef void* gtf_stream_t; /* a hipStream_t */
 /* Version of the struct layouts below. gtf_graph carries it with its own size, and every
  * entry point taking a gtf_graph refuses a caller built against another layout
  * (status -3, gtf_last_error() names both). Bumped on every layout change. */
-#define GTF_ABI_VERSION 2u
+#define GTF_ABI_VERSION 3u
 
 /* ---- graph structure (read-only on the path) ------------------------------ */
 typedef struct gtf_graph {
@@ -99,6 +99,12 @@ typedef struct gtf_graph {
     const int32_t* pack_ent;  /* [4*n_entries] */
     const int32_t* pack_wave; /* [n_pack_waves+1] */
     int32_t n_pack_waves;
+    /* optional per-lane view of out_sched's 4- and 8-lane buckets (v3): for lane l of entry e
+     * of those buckets, (out_slot[o], receiver of o) with o = out_ptr[sender] + l, or (-1, 0)
+     * past the sender's last out-edge, as int32 pairs -- the scan then reads each lane's edge
+     * beside the schedule entry instead of after it (one dependent round of loads fewer).
+     * [2 * (4 * n_o4 + 8 * n_o8)], or NULL. */
+    const int32_t* out_lanes;
 } gtf_graph;
 
 /* ---- per-node mutable state ------------------------------------------------ */

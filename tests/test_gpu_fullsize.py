@@ -99,3 +99,25 @@ def test_pass_is_deterministic_and_only_deactivates(c4):
     d.full_pass(p)
     _same(_state(d), first, "second run")
     assert np.all(first["act"] <= act0), "an edge was re-activated"
+
+
+def test_staged_input_copies_equal_the_resident_pass(c4):
+    """bench.py's steps run on staged copies of the pass-input arena (DeviceGraph.stage_inputs):
+    a pass on copy i leaves copy i exactly as a pass on the resident arrays leaves them,
+    and the other copies untouched"""
+    from gtf.device import DeviceGraph
+    p = Params()
+    d = DeviceGraph(c4, layout="tiled")
+    snap = d.snapshot(DeviceGraph.PASS_INPUTS)
+    d.stage_inputs(3)
+    d.fill_inputs(snap)
+    d.clear_errors()
+    d.use_inputs(1)
+    d.full_pass(p)
+    d.use_inputs(None)
+    d.full_pass(p)
+    assert d.errors() == 0
+    import torch
+    assert torch.equal(d._staged[1][0], d.arena)
+    assert torch.equal(d._staged[0][0], snap["__arena__"]) and torch.equal(d._staged[2][0], snap["__arena__"])
+    assert not torch.equal(d.arena, snap["__arena__"])

@@ -313,7 +313,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-c5", action="store_true", help="skip the config-5 parabolic-KL section")
     ap.add_argument("--no-dropin", action="store_true", help="skip the drop-in stage wall time")
-    ap.add_argument("--layout", default="tiled", choices=["tiled", "schedule", "natural"],
+    ap.add_argument("--layout", default="tiled", choices=["tiled", "padded", "schedule", "natural"],
                     help="device node order (DeviceGraph layout)")
     ap.add_argument("--tile", type=int, default=4096, help="nodes per tile of --layout tiled")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
@@ -406,10 +406,11 @@ def main():
 
     # eligible nodes of the KL clustering (3 <= |updated_track_states| <= 15), from the
     # state after a pass (clustering does not change dict membership)
-    sp = d.slot_ptr_host   # device order
+    gh = d.download(g.copy())   # host order (any device layout)
+    sp = g.slot_ptr
     owner = np.repeat(np.arange(g.n_nodes), np.diff(sp))
-    nst = np.bincount(owner, weights=(d.t["uts_rank"] >= 0).cpu().numpy(), minlength=g.n_nodes)
-    elig = (nst >= 3) & (nst <= 15) & (d.t["has_uts"].cpu().numpy() == 1)
+    nst = np.bincount(owner, weights=(gh.slot["uts_rank"] >= 0), minlength=g.n_nodes)
+    elig = (nst >= 3) & (nst <= 15) & (gh.node["has_uts"] == 1)
     e_elig = int(np.diff(sp)[elig].sum())
     kern = {
         "k_sender": (avg(0, 1), None),

@@ -617,12 +617,24 @@ template <int G>
 __device__ __forceinline__ bool node_fields(NodeCtx<G>& c, const gtf_graph& g, const gtf_states& tse,
                                             const gtf_states& uts, const gtf_edges& e, const Need& nd);
 
+// the padded tile layout (gtf_graph.pad_*) of one lane-group size: c nodes per tile
+struct Arith {
+    int32_t c, node_off, slot_off, tn, ts;
+};
+
 template <int G>
 __device__ __forceinline__ bool node_load(NodeCtx<G>& c, const gtf_graph& g, const gtf_nodes& n,
                                           const gtf_states& tse, const gtf_states& uts, const gtf_edges& e,
                                           const int32_t* list, const int32_t* seg, int count, int gi,
-                                          const Need& nd) {
+                                          const Need& nd, const Arith ar = Arith{0, 0, 0, 0, 0}) {
     if (gi >= count) return false;  // group-uniform
+    if (G > 0 && ar.c > 0) {   // padded tiles: node and slots by arithmetic, no schedule loads
+        const int t = gi / ar.c, i = gi - t * ar.c;
+        c.v = t * ar.tn + ar.node_off + i;
+        c.lo = t * ar.ts + ar.slot_off + i * G;
+        c.d = G;
+        return node_fields(c, g, tse, uts, e, nd);
+    }
     c.v = list[gi];
     if (seg) {  // the slot segment stored beside the schedule entry: no dependent slot_ptr gather
         const int2 sg = reinterpret_cast<const int2*>(seg)[gi];
@@ -777,12 +789,12 @@ template <int G, int... OPS>
 __device__ __forceinline__ void node_seq_body(const gtf_graph& g, gtf_nodes& n, gtf_states& tse, gtf_states& uts,
                                               gtf_edges& e, const gtf_params& p, const Ws& w, double chi2_thr,
                                               double kl_thr, const int32_t* list, const int32_t* seg, int count,
-                                              int bid, char* smem) {
+                                              int bid, char* smem, const Arith ar) {
     using Q = OpSeq<OPS...>;
     using Stage = StageT<G>;
     NodeCtx<G> c;
     const int gi = (bid * BLOCK + (int)threadIdx.x) / G;
-    if (!node_load(c, g, n, tse, uts, e, list, seg, count, gi, Q::need)) return;
+    if (!node_load(c, g, n, tse, uts, e, list, seg, count, gi, Q::need, ar)) return;
     double* sval = (double*)smem + (threadIdx.x & ~63);
     Stage* stg = (Stage*)(smem + BLOCK * sizeof(double)) + (Q::cluster ? (int)threadIdx.x / G : 0);
 #if GTF_EARLY_STAGE
@@ -814,6 +826,7 @@ struct Buckets {
     const int32_t* seg[6];   // their slot segments (gtf_graph.sched_seg) or NULL
     int32_t count[6];
     int32_t blocks[6];
+    Arith ar[6];             // padded tile layout (ar[q].c > 0: addresses by arithmetic)
 };
 
 template <int G>
@@ -843,34 +856,36 @@ __global__ void __launch_bounds__(BLOCK) k_node_multi(gtf_graph g, gtf_nodes n, 
     int b = blockIdx.x;
     if (b < bk.blocks[0]) {
         node_seq_body<64, OPS...>(g, n, tse, uts, e, p, w, chi2_thr, kl_thr, bk.list[0], bk.seg[0], bk.count[0], b,
-                                  smem);
+                                  smem, bk.ar[0]);
         return;
     }
     b -= bk.blocks[0];
     if (b < bk.blocks[1]) {
         node_seq_body<32, OPS...>(g, n, tse, uts, e, p, w, chi2_thr, kl_thr, bk.list[1], bk.seg[1], bk.count[1], b,
-                                  smem);
+                                  smem, bk.ar[1]);
         return;
     }
     b -= bk.blocks[1];
     if (b < bk.blocks[2]) {
         node_seq_body<16, OPS...>(g, n, tse, uts, e, p, w, chi2_thr, kl_thr, bk.list[2], bk.seg[2], bk.count[2], b,
-                                  smem);
+                                  smem, bk.ar[2]);
         return;
     }
     b -= bk.blocks[2];
     if (b < bk.blocks[3]) {
-        node_seq_body<8, OPS...>(g, n, tse, uts, e, p, w, chi2_thr, kl_thr, bk.list[3], bk.seg[3], bk.count[3], b, smem);
+        node_seq_body<8, OPS...>(g, n, tse, uts, e, p, w, chi2_thr, kl_thr, bk.list[3], bk.seg[3], bk.count[3], b, smem,
+                                 bk.ar[3]);
         return;
     }
     b -= bk.blocks[3];
     if (b < bk.blocks[4]) {
         node_seq_body<4, OPS...>(g, n, tse, uts, e, p, w, chi2_thr, kl_thr, bk.list[4], bk.seg[4], bk.count[4], b,
-                                 smem);
+                                 smem, bk.ar[4]);
         return;
     }
     b -= bk.blocks[4];
-    node_seq_body<2, OPS...>(g, n, tse, uts, e, p, w, chi2_thr, kl_thr, bk.list[5], bk.seg[5], bk.count[5], b, smem);
+    node_seq_body<2, OPS...>(g, n, tse, uts, e, p, w, chi2_thr, kl_thr, bk.list[5], bk.seg[5], bk.count[5], b, smem,
+                                 bk.ar[5]);
 }
 
 // Packed lane segments (gtf_graph.pack_ent / pack_wave): wavefront wv takes the entries

@@ -696,6 +696,18 @@ int check_graph(const gtf_graph* g) {
     if (g->n_nodes > 0 && (!g->slot_ptr || !g->out_ptr || !g->gnn)) {
         snprintf(g_err, sizeof(g_err), "missing graph arrays"); return -2;
     }
+    if (g->pad_tiles != 0) {   // the padded tile layout must stay inside the arrays
+        long long tn = 0, ts = 0;
+        bool ok = g->pad_tiles > 0 && g->sched;
+        for (int j = 0; j < 6; j++) {
+            ok = ok && g->pad_count[j] >= 0;
+            tn += g->pad_count[j];
+            ts += (long long)g->pad_count[j] * (2 << j);
+        }
+        ok = ok && tn == g->pad_tile_nodes && ts == g->pad_tile_slots &&
+             (long long)g->pad_tiles * tn <= g->n_nodes && (long long)g->pad_tiles * ts <= g->n_slots;
+        if (!ok) { snprintf(g_err, sizeof(g_err), "bad padded tile layout"); return -2; }
+    }
     return 0;
 }
 
@@ -850,11 +862,23 @@ int launch_seq(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* ut
             const int32_t* starts[6] = {s8 + g->n_g8 + g->n_g16 + g->n_g32, s8 + g->n_g8 + g->n_g16, s8 + g->n_g8,
                                         s8, g->sched + n2, g->sched};
             int total = 0;
+            // padded tile layout: tile offsets of the groups G = 2, 4, 8, 16, 32, 64 (in that order)
+            int noff[6] = {0}, soff[6] = {0};
+            for (int j = 1; j < 6; j++) {
+                noff[j] = noff[j - 1] + g->pad_count[j - 1];
+                soff[j] = soff[j - 1] + g->pad_count[j - 1] * (2 << (j - 1));
+            }
             for (int q = 0; q < 6; q++) {
                 bk.list[q] = starts[q];
                 bk.seg[q] = g->sched_seg ? g->sched_seg + 2 * (starts[q] - g->sched) : nullptr;
                 bk.count[q] = cnt[q];
-                bk.blocks[q] = (cnt[q] + BLOCK / gs[q] - 1) / (BLOCK / gs[q]);
+                bk.ar[q] = Arith{0, 0, 0, 0, 0};
+                if (g->pad_tiles > 0) {   // every node of the group, in tile order, by arithmetic
+                    const int j = 5 - q;
+                    bk.ar[q] = Arith{g->pad_count[j], noff[j], soff[j], g->pad_tile_nodes, g->pad_tile_slots};
+                    bk.count[q] = g->pad_tiles * g->pad_count[j];
+                }
+                bk.blocks[q] = (bk.count[q] + BLOCK / gs[q] - 1) / (BLOCK / gs[q]);
                 total += bk.blocks[q];
             }
             if (g->pack_ent && g->pack_wave && g->n_pack_waves > 0)   // every <= 64-slot node, packed

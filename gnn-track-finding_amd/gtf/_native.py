@@ -29,7 +29,9 @@ class GtfGraph(ctypes.Structure):
                 ("sched", P), ("n_g8", I32), ("n_g16", I32), ("n_g32", I32), ("n_g64", I32), ("out_dst", P),
                 ("slot_layer", P), ("n_g4", I32), ("sched_seg", P),
                 ("out_sched", P), ("n_o4", I32), ("n_o8", I32), ("n_o16", I32), ("n_g2", I32),
-                ("pack_ent", P), ("pack_wave", P), ("n_pack_waves", I32), ("out_lanes", P)]
+                ("pack_ent", P), ("pack_wave", P), ("n_pack_waves", I32), ("out_lanes", P),
+                ("pad_tiles", I32), ("pad_tile_nodes", I32), ("pad_tile_slots", I32), ("pad_count", I32 * 6),
+                ("pad_reserved_", I32)]
 
     def __init__(self, **fields):
         super().__init__(**fields)

@@ -20,7 +20,7 @@ import ctypes
 import numpy as np
 
 from . import _native as nat
-from .graph import BUCKETS, TrackGraph, NODE_FIELDS, SLOT_FIELDS, renumber
+from .graph import BUCKETS, TrackGraph, NODE_FIELDS, SLOT_FIELDS, padded, renumber
 from .params import Params
 
 STATIC_SLOT = ("slot_src", "is_edge", "rev_edge", "send_mw")
@@ -130,11 +130,14 @@ class DeviceGraph:
         torch = _torch()
         self.layout = layout
         self.order = self.slot_perm = None
+        self.pad_plan = None
         if layout in ("schedule", "tiled"):
             self.order = schedule_order(g.slot_ptr, tile if layout == "tiled" else 0)
             g, self.slot_perm = renumber(g, self.order)
+        elif layout == "padded":   # padded tiles (graph.padded): dummy nodes / padding slots map to -1
+            g, self.order, self.slot_perm, self.pad_plan = padded(g, tile)
         elif layout != "natural":
-            raise ValueError("layout must be 'natural', 'schedule' or 'tiled'")
+            raise ValueError("layout must be 'natural', 'schedule', 'tiled' or 'padded'")
         self.slot_ptr_host = g.slot_ptr
         self.torch = torch
         self.device = torch.device(device)
@@ -238,6 +241,10 @@ class DeviceGraph:
                      n_g16=self.n_g_all[2], n_g32=self.n_g_all[3], n_g64=self.n_g_all[4], sched_seg=p("sched_seg"),
                      out_sched=p("out_sched"), n_o4=self.n_o[0], n_o8=self.n_o[1], n_o16=self.n_o[2],
                      n_g2=self.n_g2, out_lanes=p("out_lanes"))
+        if self.pad_plan is not None:
+            pl = self.pad_plan
+            sched.update(pad_tiles=pl["tiles"], pad_tile_nodes=pl["tile_nodes"], pad_tile_slots=pl["tile_slots"],
+                         pad_count=(ctypes.c_int32 * 6)(*pl["count"]))
         if not self.use_sched:   # thread per node, 8-lane sender scan
             self.cg = nat.GtfGraph(**base)
         elif pack and self.n_pack_waves:
@@ -419,20 +426,22 @@ class DeviceGraph:
     # ---------------------------------------------------------------- results
     def download(self, g: TrackGraph) -> TrackGraph:
         """copy the mutable arrays back into the host TrackGraph (in place, host order)"""
+        nm = None if self.order is None else self.order >= 0          # (padded: not a dummy node)
+        sm = None if self.slot_perm is None else self.slot_perm >= 0  # (padded: not a padding slot)
         for f in MUTABLE_NODE:
-            a = self.t[f].cpu().numpy().reshape(g.node[f].shape)
+            a = self.t[f].cpu().numpy().reshape((-1,) + g.node[f].shape[1:])
             if self.order is None:
                 g.node[f][...] = a
             else:
-                g.node[f][self.order] = a
+                g.node[f][self.order[nm]] = a[nm]
         for f in SLOT_FIELDS:
             if f in STATIC_SLOT or f == "slot_key":
                 continue
-            a = self.t[f].cpu().numpy().reshape(g.slot[f].shape)
+            a = self.t[f].cpu().numpy().reshape((-1,) + g.slot[f].shape[1:])
             if self.slot_perm is None:
                 g.slot[f][...] = a
             else:
-                g.slot[f][self.slot_perm] = a
+                g.slot[f][self.slot_perm[sm]] = a[sm]
         return g
 
     def _natural_only(self, what):

@@ -219,6 +219,95 @@ def renumber(g: TrackGraph, order) -> tuple:
     return h, slot_perm
 
 
+GROUPS = ((2, 0, 2), (4, 3, 4), (8, 5, 8), (16, 9, 16), (32, 17, 32), (64, 33, 64))   # (lanes, min, max slots)
+
+
+def padded(g: TrackGraph, tile: int = 4096) -> tuple:
+    """The padded tile layout of the node kernel (gtf_graph.pad_*): nodes grouped by the
+    lane-group size G of their slot count (GROUPS), every node of group G owning exactly G
+    slots -- its own, then inert padding slots (orphan, no edge, no key in either dict,
+    which every op treats as an absent key) -- and T tiles that each hold the same number
+    c_G of group-G nodes (the group's nodes in host order, cut into T runs; the few
+    missing ones are dummy nodes: no slots of their own, an empty TSE dict, alone in their
+    subgraph). Node (t, G, i) is t * TN + off_G + i and its slots start at t * TS + soff_G
+    + i * G, so the node kernel finds every node and slot by arithmetic. Nodes with more
+    than 64 slots follow the tiles unpadded. Returns (graph, node_of_new, slot_of_new,
+    plan): old node / slot of every new one (-1 = dummy / padding) and the tile plan
+    {"tiles", "tile_nodes", "tile_slots", "count" (c_G per GROUPS entry)}."""
+    N, S = g.n_nodes, g.n_slots
+    sp = g.slot_ptr.astype(np.int64)
+    deg = np.diff(sp)
+    T = max(1, -(-N // tile))
+    lists = [np.nonzero((deg >= lo) & (deg <= hi))[0] for _, lo, hi in GROUPS]
+    big = np.nonzero(deg > 64)[0]
+    cnt = [-(-len(L) // T) for L in lists]
+    TN = int(sum(cnt))
+    TS = int(sum(c * G for c, (G, _, _) in zip(cnt, GROUPS)))
+    n_new = T * TN + len(big)
+    node_of_new = np.full(n_new, -1, np.int64)
+    start_new = np.zeros(n_new + 1, np.int64)   # slot_ptr of the new graph
+    cap_new = np.zeros(n_new, np.int64)
+    off = soff = 0
+    for L, c, (G, _, _) in zip(lists, cnt, GROUPS):
+        j = np.arange(T * c)
+        t, i = j // max(c, 1), j % max(c, 1)
+        v = t * TN + off + i
+        if c:
+            node_of_new[v[:len(L)]] = L
+            start_new[v] = t * TS + soff + i * G
+            cap_new[v] = G
+        off += c
+        soff += c * G
+    vb = T * TN + np.arange(len(big))
+    node_of_new[vb] = big
+    cap_new[vb] = deg[big]
+    start_new[vb] = T * TS + np.concatenate([[0], np.cumsum(deg[big])[:-1]]) if len(big) else 0
+    S_new = int(T * TS + deg[big].sum())
+    start_new[n_new] = S_new
+    assert np.all(np.diff(start_new) == cap_new)
+    real = node_of_new >= 0
+    new_of_old = np.empty(N, np.int64)
+    new_of_old[node_of_new[real]] = np.nonzero(real)[0]
+    # slots: the old segment of each real node at the start of its new one
+    slot_of_new = np.full(S_new, -1, np.int64)
+    if S:
+        owner_old = np.repeat(np.arange(N), deg)
+        new_slot = start_new[new_of_old[owner_old]] + (np.arange(S) - sp[owner_old])
+        slot_of_new[new_slot] = np.arange(S)
+    new_of_old_slot = np.empty(S, np.int64)
+    new_of_old_slot[slot_of_new[slot_of_new >= 0]] = np.nonzero(slot_of_new >= 0)[0]
+    node = empty_arrays(NODE_FIELDS, n_new)
+    for k in NODE_FIELDS:
+        node[k][real] = g.node[k][node_of_new[real]]
+    dummy = ~real
+    node["has_tse"][dummy] = 1   # an empty dict: pruning and priors find no key
+    sub0 = int(g.node["sub_id"].max()) + 1 if N else 0
+    node["sub_id"][dummy] = sub0 + np.arange(int(dummy.sum()))   # alone in its subgraph
+    slot = empty_arrays(SLOT_FIELDS, S_new)
+    rs = slot_of_new >= 0
+    for k in SLOT_FIELDS:
+        slot[k][rs] = g.slot[k][slot_of_new[rs]]
+    src = slot["slot_src"].astype(np.int64)
+    slot["slot_src"] = np.where(src >= 0, new_of_old[np.maximum(src, 0)], -1).astype(np.int32)
+    # out-lists in the new node order, successor order kept
+    op = g.out_ptr.astype(np.int64)
+    odeg_new = np.zeros(n_new, np.int64)
+    odeg_new[real] = np.diff(op)[node_of_new[real]]
+    new_op = np.zeros(n_new + 1, np.int64)
+    np.cumsum(odeg_new, out=new_op[1:])
+    E = g.n_edges
+    out_slot = np.zeros(E, np.int64)
+    if E:
+        owner_o = np.repeat(np.arange(N), np.diff(op))
+        pos = new_op[new_of_old[owner_o]] + (np.arange(E) - op[owner_o])
+        out_slot[pos] = new_of_old_slot[g.out_slot.astype(np.int64)]
+    h = TrackGraph(n_new, S_new, start_new.astype(np.int32), new_op.astype(np.int32), out_slot.astype(np.int32),
+                   node, slot, g.n_subgraphs)
+    check_layout(h)
+    plan = {"tiles": T, "tile_nodes": TN, "tile_slots": TS, "count": [int(c) for c in cnt]}
+    return h, node_of_new, slot_of_new, plan
+
+
 # --------------------------------------------------------------------------
 # pack: list[nx.DiGraph] -> TrackGraph
 # --------------------------------------------------------------------------

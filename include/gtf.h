@@ -105,6 +105,19 @@ typedef struct gtf_graph {
      * beside the schedule entry instead of after it (one dependent round of loads fewer).
      * [2 * (4 * n_o4 + 8 * n_o8)], or NULL. */
     const int32_t* out_lanes;
+    /* optional padded tile layout of the node kernel (v3; gtf.graph.padded): the nodes of
+     * each lane-group size G = 2, 4, 8, 16, 32, 64 own exactly G slots (their own, then inert
+     * padding slots: orphan, no edge, rank -1 in both dicts), and each of pad_tiles tiles
+     * holds pad_count[j] nodes of group j, groups in that order: node (t, j, i) is
+     * t * pad_tile_nodes + sum(pad_count[:j]) + i, its slots start at t * pad_tile_slots +
+     * sum(pad_count[:j] * G[:j]) + i * G[j]. gtf_pass's node kernel then finds every node
+     * and slot by arithmetic (no schedule loads); sched must still list the nodes (the other
+     * entry points and the > 64-slot nodes use it). pad_tiles = 0: none. */
+    int32_t pad_tiles;
+    int32_t pad_tile_nodes;
+    int32_t pad_tile_slots;
+    int32_t pad_count[6];
+    int32_t pad_reserved_;
 } gtf_graph;
 
 /* ---- per-node mutable state ------------------------------------------------ */

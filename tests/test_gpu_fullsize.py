@@ -51,7 +51,7 @@ def _same(a, b, what):
 
 def _run(g, how, p):
     from gtf.device import DeviceGraph
-    if how in ("schedule_layout", "tiled_layout", "packed"):   # renumbered nodes (results mapped back) / packed
+    if how in ("schedule_layout", "tiled_layout", "padded_layout", "packed"):   # renumbered nodes (results mapped back) / packed
         d = (DeviceGraph(g, layout=how.split("_")[0]) if how.endswith("_layout") else DeviceGraph(g, pack=True))
         d.clear_errors()
         d.full_pass(p)
@@ -81,7 +81,7 @@ def test_fused_pass_equals_stagewise_and_other_implementations(c4):
     p = Params()
     ref, ref_flags = _run(c4, "fused", p)
     assert ref["act"].sum() > 0 and ref["has_merged"].sum() > 0
-    for how in ("stages", "interpreter", "thread_per_node", "schedule_layout", "tiled_layout", "packed"):
+    for how in ("stages", "interpreter", "thread_per_node", "schedule_layout", "tiled_layout", "padded_layout", "packed"):
         got, flags = _run(c4, how, p)
         assert flags == ref_flags, how
         _same(got, ref, how)

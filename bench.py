@@ -179,7 +179,7 @@ def bench_c5(dev, steps, warmup, n_events=256):
     truth = io.read_truth(os.path.join(kat, "truth_vol7.csv"), g.node["node_id"])
     ptr, src = parabolic.in_edge_csr(g)
     ptr, src, gnn, tr = parabolic.batch(ptr, src, g.node["gnn"], truth, n_events)
-    k = parabolic.ParabolicKL(ptr, src, gnn, tr, dev)
+    k = parabolic.ParabolicKL(ptr, src, gnn, tr, dev, ordered=True)
     res = {"workload": "%d x committed vol-7 134 event (jittered copies)" % n_events, "nodes": k.n_nodes,
            "in_edges": k.n_slots, "pairs": k.n_pairs, "listed_nodes": k.n_listed}
     outs = {}

@@ -144,12 +144,12 @@ constexpr size_t stage_bytes(int G, size_t t) { return (size_t)(BLOCK / G) * G *
 // the wavefront bucket beyond 64 in-edges, where pair lanes recompute both states)
 template <typename T, int G, bool STATES>
 __device__ __forceinline__ void pkl_node(const gtf_kl_graph& g, const gtf_kl_out& o, const int32_t* list, int count,
-                                         int bid, char* smem) {
+                                         int bid, char* smem, int first = 0) {
     using Stage = KlStage<T, G>;
     const int gi = (bid * BLOCK + (int)threadIdx.x) / G;
     const int gl = threadIdx.x & (G - 1);
     if (gi >= count) return;  // group-uniform
-    const int v = list[gi];
+    const int v = list ? list[gi] : first + gi;   // (ordered layout: the bucket is a node range)
     const int lo = g.slot_ptr[v], d = g.slot_ptr[v + 1] - lo;
     if (d < 1) return;
     Stage* stg = (Stage*)smem + (int)threadIdx.x / G;
@@ -228,6 +228,43 @@ __device__ __forceinline__ void pkl_node(const gtf_kl_graph& g, const gtf_kl_out
 // resident waves beat more chains per wave, so the default is 1.
 constexpr int NPT = GTF_KL_NPT;
 
+// ordered layout (gtf_kl_graph.first / n_d1 / slot0 / pair0): node, slots and pair of
+// bucket-0 entry gi by arithmetic, so the node's own fields and its in-edges' senders are
+// one round of independent loads and the senders' coordinates the second
+template <typename T, bool STATES>
+__device__ __forceinline__ void pkl_node1_ordered(const gtf_kl_graph& g, const gtf_kl_out& o, int bid) {
+    const int gi = bid * BLOCK + (int)threadIdx.x;
+    if (gi >= g.count[0]) return;
+    const int v = g.first[0] + gi;
+    const bool two = gi >= g.n_d1;
+    const int64_t l = g.slot0 + (two ? g.n_d1 + 2 * (int64_t)(gi - g.n_d1) : gi);
+    const int64_t pp = g.pair0 + (gi - g.n_d1);
+    const double xv = g.gnn[4 * (int64_t)v], yv = g.gnn[4 * (int64_t)v + 1];
+    const long long tv = (o.truth && g.truth) ? g.truth[v] : 0;
+    const int u0 = g.slot_src[l];
+    const int u1 = two ? g.slot_src[l + 1] : u0;
+    const double x0 = g.gnn[4 * (int64_t)u0], y0 = g.gnn[4 * (int64_t)u0 + 1];
+    const double x1 = g.gnn[4 * (int64_t)u1], y1 = g.gnn[4 * (int64_t)u1 + 1];
+    long long t0 = 0, t1 = 0;
+    if (o.truth && g.truth) { t0 = g.truth[u0]; t1 = g.truth[u1]; }
+    const Frame f = node_frame_xy(xv, yv);
+    bool s0, s1 = false;
+    const PState<T> a = pstate<T>(f, x0, y0, s0, STATES ? o.sv + 3 * l : nullptr, STATES ? o.cov + 9 * l : nullptr);
+    PState<T> b = a;
+    if (two) b = pstate<T>(f, x1, y1, s1, STATES ? o.sv + 3 * (l + 1) : nullptr, STATES ? o.cov + 9 * (l + 1) : nullptr);
+    if ((s0 || s1) && o.err) atomicOr(o.err, (uint32_t)GTF_ERR_SINGULAR_H);
+    const double g0 = (f.y - y0) / (f.x - x0);
+    const double g1 = two ? (f.y - y1) / (f.x - x1) : g0;
+    const double d = two ? 2.0 : 1.0;
+    const double mean = (two ? g0 + g1 : g0) / d;
+    if (o.emp_var) o.emp_var[v] = (two ? (g0 - mean) * (g0 - mean) + (g1 - mean) * (g1 - mean) : 0.0 * (g0 - mean)) / d;
+    if (o.emp_mean) o.emp_mean[v] = mean;
+    if (two) {
+        ((T*)o.kl)[pp] = pkl<T>(b, a);   // pair (i, j) = (1, 0)
+        if (o.truth) o.truth[pp] = (int8_t)(tv == t1 && t1 == t0 && tv == t0);
+    }
+}
+
 template <typename T, bool STATES>
 __device__ __forceinline__ void pkl_node1(const gtf_kl_graph& g, const gtf_kl_out& o, const int32_t* list, int count,
                                           int bid) {
@@ -300,6 +337,7 @@ __device__ __forceinline__ void pkl_node1(const gtf_kl_graph& g, const gtf_kl_ou
 
 struct KlBuckets {
     int32_t blocks[4];
+    int32_t ordered;   // gtf_kl_graph's ordered layout (every list NULL)
 };
 
 // one launch over the four buckets; wavefront-bucket blocks first (longest-running)
@@ -318,29 +356,31 @@ __global__ void __launch_bounds__(BLOCK) KL_ATTR k_parabolic_kl(gtf_kl_graph g, 
     // neighbouring nodes (one event's hits) share an L2
     int b = blockIdx.x;
     if (b < bk.blocks[3]) {
-        pkl_node<T, 64, STATES>(g, o, g.list[3], g.count[3], gtf::xcd_local(b, bk.blocks[3]), smem);
+        pkl_node<T, 64, STATES>(g, o, g.list[3], g.count[3], gtf::xcd_local(b, bk.blocks[3]), smem, g.first[3]);
         return;
     }
     b -= bk.blocks[3];
     if (b < bk.blocks[2]) {
-        pkl_node<T, 8, STATES>(g, o, g.list[2], g.count[2], gtf::xcd_local(b, bk.blocks[2]), smem);
+        pkl_node<T, 8, STATES>(g, o, g.list[2], g.count[2], gtf::xcd_local(b, bk.blocks[2]), smem, g.first[2]);
         return;
     }
     b -= bk.blocks[2];
     if (b < bk.blocks[1]) {
-        pkl_node<T, 4, STATES>(g, o, g.list[1], g.count[1], gtf::xcd_local(b, bk.blocks[1]), smem);
+        pkl_node<T, 4, STATES>(g, o, g.list[1], g.count[1], gtf::xcd_local(b, bk.blocks[1]), smem, g.first[1]);
         return;
     }
     b -= bk.blocks[1];
-    pkl_node1<T, STATES>(g, o, g.list[0], g.count[0], gtf::xcd_local(b, bk.blocks[0]));
+    if (bk.ordered) pkl_node1_ordered<T, STATES>(g, o, gtf::xcd_local(b, bk.blocks[0]));
+    else pkl_node1<T, STATES>(g, o, g.list[0], g.count[0], gtf::xcd_local(b, bk.blocks[0]));
 }
 
 template <typename T>
 int launch(const gtf_kl_graph* g, const gtf_kl_out* o, hipStream_t st) {
     KlBuckets bk;
+    bk.ordered = !g->list[0] && !g->list[1] && !g->list[2] && !g->list[3];
     int total = 0;
     for (int i = 0; i < 4; i++) {
-        const int per_block = i == 0 ? BLOCK * NPT : BLOCK / BG[i];   // nodes per block
+        const int per_block = i == 0 ? (bk.ordered ? BLOCK : BLOCK * NPT) : BLOCK / BG[i];   // nodes per block
         bk.blocks[i] = gtf::pad8((g->count[i] + per_block - 1) / per_block);
         total += bk.blocks[i];
     }
@@ -364,12 +404,20 @@ extern "C" int gtf_parabolic_kl(const gtf_kl_graph* g, int32_t dtype, const gtf_
     if (!g || !out) { gtf::set_error("gtf_parabolic_kl: null argument"); return -2; }
     if (g->n_nodes < 0 || g->n_slots < 0) { gtf::set_error("gtf_parabolic_kl: negative sizes"); return -2; }
     int listed = 0;
+    const bool ordered = !g->list[0] && !g->list[1] && !g->list[2] && !g->list[3];
     for (int i = 0; i < 4; i++) {
-        if (g->count[i] < 0 || (g->count[i] > 0 && !g->list[i])) {
+        if (g->count[i] < 0 || (g->count[i] > 0 && !g->list[i] && !ordered)) {
             gtf::set_error("gtf_parabolic_kl: bad node list");
             return -2;
         }
         listed += g->count[i];
+    }
+    if (ordered) {   // every address the ordered layout implies stays inside the arrays
+        bool ok = g->n_d1 >= 0 && g->n_d1 <= g->count[0] && g->slot0 >= 0 && g->pair0 >= 0 &&
+                  g->slot0 + g->n_d1 + 2 * (int64_t)(g->count[0] - g->n_d1) <= g->n_slots;
+        for (int i = 0; i < 4; i++)
+            ok = ok && g->first[i] >= 0 && (int64_t)g->first[i] + g->count[i] <= g->n_nodes;
+        if (!ok) { gtf::set_error("gtf_parabolic_kl: bad ordered layout"); return -2; }
     }
     if (listed && (!g->slot_ptr || !g->slot_src || !g->gnn || !g->pair_ptr || !out->kl)) {
         gtf::set_error("gtf_parabolic_kl: missing arrays");

@@ -46,18 +46,49 @@ def in_edge_csr(g: TrackGraph):
 
 
 class ParabolicKL:
-    """Device-resident KL graph of one or many events (events concatenated into one CSR)."""
+    """Device-resident KL graph of one or many events (events concatenated into one CSR).
 
-    def __init__(self, slot_ptr, slot_src, gnn, truth=None, device="cuda", with_single=False):
+    ordered: the nodes are renumbered on upload so that each in-degree bucket is one node
+    range -- one-edge nodes, two-edge nodes, then the 3..4, 5..8 and > 8 buckets, then the
+    unlisted nodes -- with slots and pairs following node order (gtf_kl_graph's ordered
+    layout: the kernel reaches the two-edge bucket by arithmetic). Device outputs are then
+    in that order: ``node_of`` maps a device node to the caller's, pair_index() returns the
+    caller's node ids, and ``host_nodes`` / ``host_slots`` reorder per-node / per-slot
+    outputs; pairs keep the caller's (node, i, j) rows through pair_index()."""
+
+    def __init__(self, slot_ptr, slot_src, gnn, truth=None, device="cuda", with_single=False, ordered=False):
         slot_ptr = np.ascontiguousarray(slot_ptr, np.int32)
         self.n_nodes = int(slot_ptr.shape[0] - 1)
         self.n_slots = int(slot_ptr[-1])
         d = np.diff(slot_ptr).astype(np.int64)
+        lo = 1 if with_single else 2
+        self.node_of = self.slot_of = None
+        if ordered:
+            sp = slot_ptr.astype(np.int64)
+            keys = [d == 1 if lo == 1 else np.zeros(d.size, bool), d == 2] + \
+                   [(d >= a) & (d <= b) for a, b in BUCKETS[1:]]
+            rank = np.full(d.size, len(keys), np.int64)
+            for q in reversed(range(len(keys))):
+                rank[keys[q]] = q
+            order = np.argsort(rank, kind="stable")
+            nd = d[order]
+            new_ptr = np.zeros(self.n_nodes + 1, np.int64)
+            np.cumsum(nd, out=new_ptr[1:])
+            owner = np.repeat(np.arange(self.n_nodes), nd)
+            slot_of = sp[order][owner] + (np.arange(self.n_slots) - new_ptr[owner])
+            inv = np.empty(self.n_nodes, np.int64)
+            inv[order] = np.arange(self.n_nodes)
+            slot_src = inv[np.asarray(slot_src, np.int64)[slot_of]]
+            gnn = np.asarray(gnn, np.float64).reshape(-1, 4)[order]
+            truth = np.asarray(truth, np.int64)[order] if truth is not None else None
+            slot_ptr = new_ptr.astype(np.int32)
+            d = nd
+            self.node_of, self.slot_of = order, slot_of
+            self._ranges = [int(k.sum()) for k in keys]
         npair = np.where(d >= 2, d * (d - 1) // 2, 0)
         pair_ptr = np.zeros(self.n_nodes + 1, np.int64)
         np.cumsum(npair, out=pair_ptr[1:])
         self.n_pairs = int(pair_ptr[-1])
-        lo = 1 if with_single else 2
         lists = [np.nonzero((d >= max(a, lo)) & (d <= b))[0].astype(np.int32) for a, b in BUCKETS]
         self.n_listed = int(sum(x.size for x in lists))
         self.degree = d
@@ -72,10 +103,19 @@ class ParabolicKL:
         self.lists = [t(x) for x in lists]
         self.device = dev
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)
-        self._g = nat.GtfKlGraph(self.n_nodes, self.n_slots, _ptr(self.slot_ptr), _ptr(self.slot_src),
-                                 _ptr(self.gnn), _ptr(self.truth), _ptr(self.pair_ptr),
-                                 (ctypes.c_void_p * 4)(*[x.data_ptr() if x.numel() else None for x in self.lists]),
-                                 (ctypes.c_int32 * 4)(*[x.numel() for x in self.lists]))
+        if ordered:   # bucket ranges, no lists
+            n1, n2 = self._ranges[0], self._ranges[1]
+            counts = [n1 + n2] + [int(x.size) for x in lists[1:]]
+            first = np.concatenate([[0], np.cumsum(counts)[:-1]]).astype(np.int32)
+            self._g = nat.GtfKlGraph(self.n_nodes, self.n_slots, _ptr(self.slot_ptr), _ptr(self.slot_src),
+                                     _ptr(self.gnn), _ptr(self.truth), _ptr(self.pair_ptr),
+                                     (ctypes.c_void_p * 4)(), (ctypes.c_int32 * 4)(*counts),
+                                     (ctypes.c_int32 * 4)(*first.tolist()), n1, 0, 0, 0)
+        else:
+            self._g = nat.GtfKlGraph(self.n_nodes, self.n_slots, _ptr(self.slot_ptr), _ptr(self.slot_src),
+                                     _ptr(self.gnn), _ptr(self.truth), _ptr(self.pair_ptr),
+                                     (ctypes.c_void_p * 4)(*[x.data_ptr() if x.numel() else None for x in self.lists]),
+                                     (ctypes.c_int32 * 4)(*[x.numel() for x in self.lists]))
 
     @classmethod
     def from_graph(cls, g: TrackGraph, truth=None, device="cuda", with_single=False):
@@ -114,8 +154,9 @@ class ParabolicKL:
     def errors(self):
         return int(self.err.item())
 
-    def pair_index(self):
-        """(node, i, j) of every pair row (host)."""
+    def pair_index(self, device_nodes=False):
+        """(node, i, j) of every pair row (host); node in the caller's numbering unless
+        device_nodes (the ordered layout's own)."""
         d = self.degree
         nodes = np.nonzero(d >= 2)[0]
         node = np.repeat(nodes, (d[nodes] * (d[nodes] - 1) // 2))
@@ -123,7 +164,27 @@ class ParabolicKL:
         i = np.floor((1 + np.sqrt(1 + 8 * t.astype(np.float64))) / 2).astype(np.int64)
         i -= (i * (i - 1) // 2 > t)
         i += ((i + 1) * i // 2 <= t)
+        if self.node_of is not None and not device_nodes:
+            node = self.node_of[node]
         return node, i, t - i * (i - 1) // 2
+
+    def host_nodes(self, a):
+        """a per-node device output (array, first axis = node) in the caller's node order"""
+        a = np.asarray(a)
+        if self.node_of is None:
+            return a
+        out = np.empty_like(a)
+        out[self.node_of] = a
+        return out
+
+    def host_slots(self, a):
+        """a per-slot device output in the caller's slot order"""
+        a = np.asarray(a)
+        if self.slot_of is None:
+            return a
+        out = np.empty_like(a)
+        out[self.slot_of] = a
+        return out
 
 
 def training_rows(g: TrackGraph, truth=None, dtype="f64", device="cuda"):

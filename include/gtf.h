@@ -413,6 +413,16 @@ typedef struct gtf_kl_graph {
                                  (one 64-lane wavefront each); d = 1 nodes yield states and
                                  gradient moments but no pairs */
     int32_t count[4];
+    /* ordered layout (v3; gtf.parabolic.ParabolicKL(ordered=True)): when every list[i] is
+     * NULL, bucket i is the node range [first[i], first[i] + count[i]), and bucket 0 holds
+     * n_d1 one-edge nodes, then its two-edge nodes, with consecutive slots from slot0 (in
+     * node order) and one pair each from pair0: the kernel then reaches bucket 0's slots,
+     * neighbours and pairs by arithmetic, and every bucket's nodes without a list load. */
+    int32_t first[4];
+    int32_t n_d1;
+    int32_t pad_;
+    int64_t slot0;
+    int64_t pair0;
 } gtf_kl_graph;
 
 enum { GTF_F64 = 0, GTF_F32 = 1 };

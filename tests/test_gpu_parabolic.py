@@ -10,6 +10,7 @@
 * fp32: the config-5 sweep's fp32 mode stays within its stated envelope.
 * Singular H raises LinAlgError like np.linalg.inv.
 """
+import os
 import numpy as np
 import pytest
 
@@ -17,6 +18,8 @@ import gtf_oracle as O
 from gtf import synth
 from gtf.graph import TrackGraph
 from test_kat_parabolic import kat_event, kat_rows, sorted_rows
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 pytestmark = pytest.mark.gpu
 
@@ -178,3 +181,35 @@ def test_gpu_beyond_lds_recompute_path():
     ref = np.asarray(O.parabolic_kl_pairs([s for s, _ in st], [c for _, c in st]))
     assert kl.size == ref.size == 70 * 69 // 2
     assert _rel(kl, ref).max() < 1e-6
+
+
+@pytest.mark.parametrize("with_single", [False, True])
+def test_gpu_ordered_layout_equals_lists(with_single):
+    """ParabolicKL(ordered=True) (bucket node ranges, the two-edge bucket by arithmetic)
+    gives the list layout's pair rows, truth flags, gradient moments and states bit for
+    bit once mapped back to the caller's order (16 jittered copies of the vol-7 event)"""
+    from gtf import io, parabolic
+    kat = os.path.join(GOLDEN, "kat134")
+    g = io.load_event(os.path.join(kat, "event_1_filtered_graph_"), 7, 7)
+    truth = io.read_truth(os.path.join(kat, "truth_vol7.csv"), g.node["node_id"])
+    ptr, src = parabolic.in_edge_csr(g)
+    ptr, src, gnn, tr = parabolic.batch(ptr, src, g.node["gnn"], truth, 16)
+    res = []
+    for ordered in (False, True):
+        k = parabolic.ParabolicKL(ptr, src, gnn, tr, with_single=with_single, ordered=ordered)
+        out = k.run(k.alloc("f64", emp=True, states=with_single), "f64")
+        node, i, j = k.pair_index()
+        key = np.lexsort((j, i, node))
+        r = {"rows": np.stack([node, i, j], 1)[key], "kl": out["kl"].cpu().numpy()[key],
+             "truth": out["truth"].cpu().numpy()[key],
+             "emp_var": k.host_nodes(out["emp_var"].cpu().numpy()),
+             "emp_mean": k.host_nodes(out["emp_mean"].cpu().numpy())}
+        if with_single:
+            r["sv"] = k.host_slots(out["sv"].cpu().numpy())
+            r["cov"] = k.host_slots(out["cov"].cpu().numpy())
+        assert k.errors() == 0
+        res.append(r)
+    a, b = res
+    for f in a:
+        x, y = a[f], b[f]
+        assert np.array_equal(x, y, equal_nan=x.dtype.kind == "f"), f

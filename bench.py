@@ -218,6 +218,26 @@ def bench_c5(dev, steps, warmup, n_events=256):
     return res
 
 
+def device_copy_gbps(dev, nbytes=1 << 30, reps=10):
+    """measured device-to-device copy bandwidth (bytes read + written per second), the
+    practical HBM ceiling SURVEY §8d asks the roofline to be quoted against beside the
+    spec peak"""
+    import torch
+    a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize()
+    gbps = 2.0 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del a, b
+    return gbps
+
+
 def reduce_scalar(x, op, dev, backend):
     """all-reduce one number across ranks (device tensor over RCCL, host tensor over gloo)"""
     import torch
@@ -429,6 +449,7 @@ def main():
                       "traffic_bytes": committed_traffic(args.workload, k, args.layout, args.tile, g.n_edges, g.n_nodes)} for k, v in cands.items()}
     achieved = nbytes / (ms * 1e-3) / 1e9
     traffic = committed_traffic(args.workload, name, args.layout, args.tile, g.n_edges, g.n_nodes)
+    copy_gbps = device_copy_gbps(dev) if rank == 0 else None
 
     sharded = None
     if world > 1:
@@ -475,6 +496,7 @@ def main():
             "roofline": {"bound": "hbm", "kernel": name, "achieved": achieved, "peak": rf.HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / rf.HBM_PEAK_GBS, "traffic": traffic,
                          "algorithmic_bytes_per_launch": nbytes, "kernel_ms": ms,
+                         "device_copy_GBps": copy_gbps, "frac_of_device_copy": achieved / copy_gbps if copy_gbps else None,
                          "kl_eligible_nodes": int(elig.sum()), "kl_eligible_in_edges": e_elig},
             "cpu_baseline": cpu,
             "cpu_baseline_cpp": cpu_cpp,

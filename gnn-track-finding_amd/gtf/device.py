@@ -241,7 +241,7 @@ class DeviceGraph:
                      n_g16=self.n_g_all[2], n_g32=self.n_g_all[3], n_g64=self.n_g_all[4], sched_seg=p("sched_seg"),
                      out_sched=p("out_sched"), n_o4=self.n_o[0], n_o8=self.n_o[1], n_o16=self.n_o[2],
                      n_g2=self.n_g2, out_lanes=p("out_lanes"))
-        if self.pad_plan is not None:
+        if self.pad_plan is not None and self.pad_plan["tile_nodes"] > 0:   # (an empty graph has no tiles)
             pl = self.pad_plan
             sched.update(pad_tiles=pl["tiles"], pad_tile_nodes=pl["tile_nodes"], pad_tile_slots=pl["tile_slots"],
                          pad_count=(ctypes.c_int32 * 6)(*pl["count"]))

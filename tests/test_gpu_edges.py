@@ -50,9 +50,9 @@ def hub_event(seed=7, n_tracks=400, n_hubs=3, fan=110):
     return synth._assemble(g.n_nodes, src, dst, x, y, z, r, layer, p)
 
 
-def _gpu(g, p, schedule=True):
+def _gpu(g, p, schedule=True, layout="natural"):
     from gtf.device import DeviceGraph
-    d = DeviceGraph(g, schedule=schedule)
+    d = DeviceGraph(g, schedule=schedule, layout=layout)
     d.clear_errors()
     d.full_pass(p)
     flags = d.errors()
@@ -76,19 +76,22 @@ def test_hub_nodes_beyond_64_slots_match_oracle():
     errs, stats = compare_noise(got, ref, noise, flips)
     print("hub event: %d edges, max slots %d, %s, device flags %d" % (g.n_edges, deg.max(), stats, flags))
     assert errs == [], "\n".join(errs)
-    # the same pass one thread per node everywhere: bit for bit
-    _, got1, flags1 = _gpu(g, p, schedule=False)
-    assert flags1 == flags
-    for k in ("act", "uts_rank", "uts_sv", "uts_cov", "uts_mw", "uts_prior", "edge_mw"):
-        a, b = got.slot[k], got1.slot[k]
-        assert np.array_equal(a, b, equal_nan=a.dtype.kind == "f"), k
-    for k in ("has_merged", "merged_state", "merged_cov", "degree"):
-        a, b = got.node[k], got1.node[k]
-        assert np.array_equal(a, b, equal_nan=a.dtype.kind == "f"), k
+    # the same pass one thread per node everywhere, and in the tiled and padded layouts
+    # (the > 64-slot nodes after the padded tiles): bit for bit
+    for kw in ({"schedule": False}, {"layout": "tiled"}, {"layout": "padded"}):
+        _, got1, flags1 = _gpu(g, p, **kw)
+        assert flags1 == flags, kw
+        for k in ("act", "uts_rank", "uts_sv", "uts_cov", "uts_mw", "uts_prior", "edge_mw"):
+            a, b = got.slot[k], got1.slot[k]
+            assert np.array_equal(a, b, equal_nan=a.dtype.kind == "f"), (kw, k)
+        for k in ("has_merged", "merged_state", "merged_cov", "degree"):
+            a, b = got.node[k], got1.node[k]
+            assert np.array_equal(a, b, equal_nan=a.dtype.kind == "f"), (kw, k)
 
 
+@pytest.mark.parametrize("layout", ["natural", "padded"])
 @pytest.mark.parametrize("keep", ["none", "isolated"])
-def test_graph_without_slots_is_a_no_op(keep):
+def test_graph_without_slots_is_a_no_op(keep, layout):
     g = synth.event(seed=3, n_tracks=60)
     if keep == "none":
         h = graph.subset(g, np.zeros(g.n_nodes, bool))
@@ -101,7 +104,7 @@ def test_graph_without_slots_is_a_no_op(keep):
         assert h.n_slots == 0 and h.n_nodes > 0
     p = Params()
     O.full_pass(h.copy(), p)   # the oracle takes it too
-    d, got, flags = _gpu(h, p)
+    d, got, flags = _gpu(h, p, layout=layout)
     assert flags == 0
     for k in ("has_merged", "merged_state", "merged_cov", "degree", "has_uts"):
         a, b = got.node[k], h.node[k]

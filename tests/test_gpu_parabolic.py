@@ -155,14 +155,15 @@ def test_gpu_singular_raises():
         parabolic.training_rows_csr(ptr, src, gnn)
 
 
-def test_gpu_empty_and_single():
+@pytest.mark.parametrize("ordered", [False, True])
+def test_gpu_empty_and_single(ordered):
     from gtf.parabolic import ParabolicKL
     gnn = np.array([[10.0, 1.0, 0, 10.05], [20.0, 2.0, 0, 20.1]])
-    k = ParabolicKL(np.array([0, 0, 1], np.int32), np.array([0], np.int32), gnn, with_single=True)
+    k = ParabolicKL(np.array([0, 0, 1], np.int32), np.array([0], np.int32), gnn, with_single=True, ordered=ordered)
     out = k.run(k.alloc("f64", states=True), "f64")
     assert k.n_pairs == 0 and out["kl"].numel() == 0
     assert np.isfinite(out["sv"].cpu().numpy()).all()
-    assert out["emp_var"].cpu().numpy()[1] == 0.0
+    assert k.host_nodes(out["emp_var"].cpu().numpy())[1] == 0.0
 
 
 def test_gpu_beyond_lds_recompute_path():

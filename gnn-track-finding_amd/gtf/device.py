@@ -196,6 +196,7 @@ class DeviceGraph:
                 continue
             up(f, g.slot[f])
         self._make_arena(self.PASS_INPUTS)
+        self._staged, self._resident = [], None   # stage_inputs() copies
         ws_bytes = int(self.lib.gtf_workspace_bytes(g.n_nodes, g.n_slots))
         self.t["ws"] = torch.zeros(ws_bytes, dtype=torch.uint8, device=self.device)
         self._build_structs(pack)
@@ -476,7 +477,9 @@ class DeviceGraph:
         a restore copy between them: use_inputs(i) points every stage method at copy i
         (None: the arrays of this graph). The arrays outside the arena (state values,
         degree) are shared: a pass overwrites every value it reads back."""
-        self._resident = (self.cn, self.cuts, self.ctse, self.ce)
+        if self._resident is None:
+            self._resident = (self.cn, self.cuts, self.ctse, self.ce)
+        self.use_inputs(None)
         lo = self.arena.data_ptr()
         hi = lo + self.arena.numel()
 
@@ -489,16 +492,23 @@ class DeviceGraph:
                 vals.append(v)
             return type(st)(*vals)
 
-        self._staged = []
+        self._staged = []   # (a second call replaces the copies)
         for _ in range(k):
             a = self.torch.empty_like(self.arena)
             off = a.data_ptr() - lo
             self._staged.append((a, tuple(rebase(s, off) for s in self._resident)))
 
     def fill_inputs(self, snap):
-        """copy the pass-input snapshot into every staged copy"""
+        """copy the pass-input snapshot (snapshot(PASS_INPUTS)) into every staged copy"""
+        if "__arena__" not in snap:
+            raise ValueError("fill_inputs takes snapshot(DeviceGraph.PASS_INPUTS)")
         for a, _ in self._staged:
             a.copy_(snap["__arena__"], non_blocking=True)
 
     def use_inputs(self, i):
-        self.cn, self.cuts, self.ctse, self.ce = self._resident if i is None else self._staged[i][1]
+        """point the stage methods at staged copy i, or back at this graph's arrays (None)"""
+        if i is None:
+            if self._resident is not None:
+                self.cn, self.cuts, self.ctse, self.ce = self._resident
+            return
+        self.cn, self.cuts, self.ctse, self.ce = self._staged[i][1]

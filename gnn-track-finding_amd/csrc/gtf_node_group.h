@@ -63,33 +63,6 @@ struct Grp {
         for (int o = G / 2; o > 0; o >>= 1) x |= __shfl_xor(x, o, G);
         return x;
     }
-    // lexicographic minimum of (v, p) over the group: the smallest v and the smallest p of
-    // its holders, in one chain of log2(G) exchange steps (NaN-free v)
-    __device__ __forceinline__ void min_vp(double& v, int& p) const {
-#pragma unroll
-        for (int o = G / 2; o > 0; o >>= 1) {
-            const double ov = __shfl_xor(v, o, G);
-            const int op = __shfl_xor(p, o, G);
-            if (ov < v || (ov == v && op < p)) { v = ov; p = op; }
-        }
-    }
-    // the group's minimum v with, over the lanes holding it, the two smallest of their
-    // (t0 < t1) pair indices and the union of their masks -- one chain instead of four
-    __device__ __forceinline__ void min_tie(double& v, int& t0, int& t1, unsigned& m) const {
-#pragma unroll
-        for (int o = G / 2; o > 0; o >>= 1) {
-            const double ov = __shfl_xor(v, o, G);
-            const int o0 = __shfl_xor(t0, o, G), o1 = __shfl_xor(t1, o, G);
-            const unsigned om = __shfl_xor(m, o, G);
-            if (ov < v) {
-                v = ov; t0 = o0; t1 = o1; m = om;
-            } else if (ov == v) {
-                t1 = min(max(t0, o0), min(t1, o1));
-                t0 = min(t0, o0);
-                m |= om;
-            }
-        }
-    }
     __device__ __forceinline__ int size() const { return G; }
     __device__ __forceinline__ int stage_base() const { return 0; }  // one stage struct per group
 };
@@ -124,20 +97,6 @@ struct Grp<0> {
     }
     __device__ __forceinline__ unsigned or_u(unsigned x) const {
         return reduce(x, [](unsigned a, unsigned b) { return a | b; });
-    }
-    __device__ __forceinline__ void min_vp(double& v, int& p) const {
-        const double m = min_d(v);
-        p = min_i(v == m ? p : 0x7fffffff);
-        v = m;
-    }
-    __device__ __forceinline__ void min_tie(double& v, int& t0, int& t1, unsigned& m) const {
-        const double b = min_d(v);
-        const bool tl = v == b;
-        const int a0 = min_i(tl ? t0 : (1 << 20));
-        t1 = min_i(tl ? (t0 == a0 ? t1 : t0) : (1 << 20));
-        t0 = a0;
-        m = or_u(tl ? m : 0u);
-        v = b;
     }
     __device__ __forceinline__ int size() const { return gsize; }
     __device__ __forceinline__ int stage_base() const { return gbase; }
@@ -571,11 +530,12 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
 #if GTF_ABLATE == 2
     if (c.grp.min_d(lmin) > -1.0) return;  // diagnostics build: staging + pair distances only
 #endif
-    double best = lmin;
-    int t0 = lt0, t1 = lt1;
-    unsigned tiemask = lmask;
-    c.grp.min_tie(best, t0, t1, tiemask);   // (lanes without a pair hold inf: no tie with a finite best)
+    const double best = c.grp.min_d(lmin);
     if (!(best < chi2_thr)) return;
+    const bool tl = lmin == best;
+    const int t0 = c.grp.min_i(tl ? lt0 : (1 << 20));
+    const int t1 = c.grp.min_i(tl ? (lt0 == t0 ? lt1 : lt0) : (1 << 20));
+    const unsigned tiemask = c.grp.or_u(tl ? lmask : 0u);
     int ti0, tj0, ti1 = 0, tj1;
     pair_ij(t0, ti0, tj0);
     if (t1 < (1 << 20)) pair_ij(t1, ti1, tj1);
@@ -613,10 +573,9 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
                 if (c.grp.gl == 0) atomicOr(err, (uint32_t)GTF_ERR_NAN_KL);
                 break;
             }
-            double mind = D;
-            int m = me ? pos : 99;
-            c.grp.min_vp(mind, m);   // the minimum and its first dict position (list.index)
+            const double mind = c.grp.min_d(D);
             if (!(mind < kl_thr)) break;
+            const int m = c.grp.min_i((me && D == mind) ? pos : 99);  // first minimum (list.index)
             const int lm = sb + stg->ord[sb + m];
             const Cov5 ii = stage_inv(stg, lm);
             const Cov5 nmc = inv_cov5(add_cov5(ii, im));

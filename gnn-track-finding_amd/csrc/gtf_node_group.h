@@ -628,7 +628,10 @@ __device__ __forceinline__ bool node_load(NodeCtx<G>& c, const gtf_graph& g, con
                                           const int32_t* list, const int32_t* seg, int count, int gi,
                                           const Need& nd, const Arith ar = Arith{0, 0, 0, 0, 0}) {
     if (gi >= count) return false;  // group-uniform
-    if (G > 0 && ar.c > 0) {   // padded tiles: node and slots by arithmetic, no schedule loads
+#ifndef GTF_PAD_ARITH   // the padded layout's arithmetic addressing (diagnostics builds): its
+#define GTF_PAD_ARITH 0    // arguments raise the fused kernel's SGPR spills 64 -> 120, +2-4 us on tiled
+#endif
+    if (GTF_PAD_ARITH && G > 0 && ar.c > 0) {   // padded tiles: node and slots by arithmetic, no schedule loads
         const int t = gi / ar.c, i = gi - t * ar.c;
         c.v = t * ar.tn + ar.node_off + i;
         c.lo = t * ar.ts + ar.slot_off + i * G;

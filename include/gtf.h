@@ -110,9 +110,10 @@ typedef struct gtf_graph {
      * padding slots: orphan, no edge, rank -1 in both dicts), and each of pad_tiles tiles
      * holds pad_count[j] nodes of group j, groups in that order: node (t, j, i) is
      * t * pad_tile_nodes + sum(pad_count[:j]) + i, its slots start at t * pad_tile_slots +
-     * sum(pad_count[:j] * G[:j]) + i * G[j]. gtf_pass's node kernel then finds every node
-     * and slot by arithmetic (no schedule loads); sched must still list the nodes (the other
-     * entry points and the > 64-slot nodes use it). pad_tiles = 0: none. */
+     * sum(pad_count[:j] * G[:j]) + i * G[j]. Built with -DGTF_PAD_ARITH=1, gtf_pass's node
+     * kernel then finds every node and slot by arithmetic (no schedule loads); the default
+     * build reads the schedule (sched must list the nodes either way: the other entry points
+     * and the > 64-slot nodes use it). pad_tiles = 0: none. */
     int32_t pad_tiles;
     int32_t pad_tile_nodes;
     int32_t pad_tile_slots;

@@ -218,6 +218,73 @@ def bench_c5(dev, steps, warmup, n_events=256):
     return res
 
 
+def bench_components(g, params, dev, reps=5):
+    """The north-star loop's other two device stages on the bench event (SURVEY §8 a15,
+    a16), after one fused pass (natural node order: both take host-order arrays):
+    the updated-state distance table (calculate_distance_between_updated_track_states.py,
+    gtf_updated_state_distances: pair counts, scan, pair kernel) and tag propagation
+    (tag_propagation.py:97-164, Jacobi max sweeps until flips / processed <= 10 %, the flip
+    count read back after each sweep as the script's stop test needs), initial tag = node
+    index, radius = r. Wall times with the device synchronised, median of reps."""
+    import torch
+    from gtf.device import DeviceGraph
+    from gtf import roofline as rf
+    d = DeviceGraph(g, dev)
+    d.clear_errors()
+    d.full_pass(params)
+    out = {}
+    ts = []
+    for _ in range(reps + 1):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ptr, cols = d.updated_state_distances()
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    npairs = int(cols["chi2"].numel())
+    dt = float(np.median(ts[1:]))
+    out["a15_updated_state_distances"] = {"pairs": npairs, "wall_ms": dt * 1e3, "pairs_per_s": npairs / dt}
+    tags = np.arange(g.n_nodes, dtype=np.int64)
+    radius = np.ascontiguousarray(g.node["xyzr"][:, 3])
+    ts = []
+    for _ in range(reps + 1):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        _, flips = d.tag_propagation(tags, radius)
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    dt = float(np.median(ts[1:]))
+    # the sweep kernel alone: K sweeps back to back between two events (no read-back)
+    import ctypes
+    vp = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    keep = torch.zeros(max(g.n_edges, 1), dtype=torch.uint8, device=dev)
+    proc = torch.zeros(max(g.n_nodes, 1), dtype=torch.uint8, device=dev)
+    cnt = torch.zeros(2, dtype=torch.int32, device=dev)
+    rad = torch.from_numpy(radius).to(dev)
+    ta = torch.from_numpy(tags).to(dev)
+    tb = torch.empty_like(ta)
+    d.lib.gtf_tag_prepare(ctypes.byref(d.cg), vp(rad), vp(keep), vp(proc), vp(cnt), d.stream)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    K = 50
+    e0.record()
+    for i in range(K):
+        d.lib.gtf_tag_sweep(ctypes.byref(d.cg), vp(keep), vp(proc), vp(ta if i % 2 == 0 else tb),
+                            vp(tb if i % 2 == 0 else ta), vp(cnt[1:2]), d.stream)
+    e1.record()
+    torch.cuda.synchronize()
+    sweep_ms = e0.elapsed_time(e1) / K
+    sweeps = len(flips)
+    nbytes = 4 * g.n_edges + 8 * g.n_nodes   # SURVEY §8d B_tag, per sweep
+    out["a16_tag_propagation"] = {"sweeps": sweeps, "flips": [int(x) for x in flips], "stage_wall_ms": dt * 1e3,
+                                  "sweep_call_ms": sweep_ms, "algorithmic_bytes_per_sweep": nbytes,
+                                  "achieved_GBps": nbytes / (sweep_ms * 1e-3) / 1e9,
+                                  "frac_of_peak": nbytes / (sweep_ms * 1e-3) / 1e9 / rf.HBM_PEAK_GBS,
+                                  "note": "sweep_call_ms: K gtf_tag_sweep calls back to back between two events "
+                                          "(flip-counter reset + kernel); stage wall time includes the prepare pass "
+                                          "and the flip-count read-back after every sweep (the script's stop test)"}
+    del d
+    return out
+
+
 def device_copy_gbps(dev, nbytes=1 << 30, reps=10):
     """measured device-to-device copy bandwidth (bytes read + written per second), the
     practical HBM ceiling SURVEY §8d asks the roofline to be quoted against beside the
@@ -458,9 +525,10 @@ def main():
         except Exception as ex:   # reported; the line then carries the replicas only and is marked
             sharded = {"error": repr(ex)[:300]}
 
-    c5 = None
+    c5 = comps = None
     if rank == 0 and world == 1 and not args.no_c5:
         c5 = bench_c5(dev, K, W)
+        comps = bench_components(g, p, dev)
 
     cpu = cpu_cpp = dropin = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -503,6 +571,7 @@ def main():
             "dropin_stage": dropin,
             "device_error_flags": flags,
             "c5_parabolic_kl": c5,
+            "other_path_stages": comps,
         }
         if world > 1:
             replicas = {"value": out["value"], "ms_per_step": out["ms_per_step"], "scaling": "weak",

@@ -55,6 +55,89 @@ __global__ void __launch_bounds__(BLOCK) k_tag_sweep(gtf_graph g, const uint8_t*
     const unsigned long long b = __ballot(flipped);
     if ((threadIdx.x & 63) == 0 && b) atomicAdd(flips, (int)__popcll(b));
 }
+// With the sender schedule (gtf_graph.out_sched + out_lanes): G lanes per node over its
+// out-edges, every lane's loads in one round (its keep flag, its neighbour's tag, the
+// node's own tag) and a group max, instead of a thread walking the out-list one dependent
+// gather at a time. Nodes without an out-edge keep their tag (one thread per node in the
+// launch's last blocks copies it).
+template <int G>
+__device__ __forceinline__ int tag_group_lanes(const gtf_graph& g, const uint8_t* keep, const uint8_t* processed,
+                                               const int64_t* tin, int64_t* tout, const int4* list, const int2* lanes,
+                                               int count, int b) {
+    const int t = b * BLOCK + (int)threadIdx.x;
+    const int gi = t / G, gl = t & (G - 1);
+    if (gi >= count) return 0;   // group-uniform
+    const int4 en = list[gi];
+    const int2 kv = lanes[t];
+    const int u = en.x, i = en.y + gl;
+    const bool edge = kv.x >= 0;
+    const uint8_t kp = edge ? keep[i] : 0;
+    const int64_t tw = tin[edge ? kv.y : u];
+    const int64_t t0 = tin[u];
+    const uint8_t pr = processed[u];
+    int64_t m = (edge && kp) ? (tw > t0 ? tw : t0) : t0;
+#pragma unroll
+    for (int o = G / 2; o > 0; o >>= 1) {
+        const int64_t x = __shfl_xor(m, o, G);
+        m = x > m ? x : m;
+    }
+    if (!pr) m = t0;
+    if (gl == 0) tout[u] = m;
+    return gl == 0 && m != t0;
+}
+
+template <int G>
+__device__ __forceinline__ int tag_group(const gtf_graph& g, const uint8_t* keep, const uint8_t* processed,
+                                         const int64_t* tin, int64_t* tout, const int4* list, int count, int b) {
+    const int gi = (b * BLOCK + (int)threadIdx.x) / G, gl = threadIdx.x & (G - 1);
+    if (gi >= count) return 0;
+    const int4 en = list[gi];
+    const int u = en.x;
+    const int64_t t0 = tin[u];
+    int64_t m = t0;
+    for (int i = en.y + gl; i < en.z; i += G)
+        if (keep[i]) {
+            const int64_t tw = tin[g.out_dst ? g.out_dst[i] : g.slot_dst[g.out_slot[i]]];
+            m = tw > m ? tw : m;
+        }
+#pragma unroll
+    for (int o = G / 2; o > 0; o >>= 1) {
+        const int64_t x = __shfl_xor(m, o, G);
+        m = x > m ? x : m;
+    }
+    if (!processed[u]) m = t0;
+    if (gl == 0) tout[u] = m;
+    return gl == 0 && m != t0;
+}
+
+struct TagBuckets {
+    const int4* list[3];
+    const int2* lanes[2];
+    int32_t count[3];
+    int32_t blocks[3];
+    int32_t copy_blocks;   // one thread per node: out-degree 0 -> tag kept
+};
+
+__global__ void __launch_bounds__(BLOCK) k_tag_sweep_sched(gtf_graph g, const uint8_t* keep, const uint8_t* processed,
+                                                           const int64_t* tin, int64_t* tout, int32_t* flips,
+                                                           TagBuckets tb) {
+    int b = blockIdx.x, flipped = 0;
+    if (b < tb.blocks[0]) {
+        flipped = tb.lanes[0] ? tag_group_lanes<4>(g, keep, processed, tin, tout, tb.list[0], tb.lanes[0], tb.count[0], b)
+                              : tag_group<4>(g, keep, processed, tin, tout, tb.list[0], tb.count[0], b);
+    } else if ((b -= tb.blocks[0]) < tb.blocks[1]) {
+        flipped = tb.lanes[1] ? tag_group_lanes<8>(g, keep, processed, tin, tout, tb.list[1], tb.lanes[1], tb.count[1], b)
+                              : tag_group<8>(g, keep, processed, tin, tout, tb.list[1], tb.count[1], b);
+    } else if ((b -= tb.blocks[1]) < tb.blocks[2]) {
+        flipped = tag_group<16>(g, keep, processed, tin, tout, tb.list[2], tb.count[2], b);
+    } else {
+        const int u = (b - tb.blocks[2]) * BLOCK + (int)threadIdx.x;
+        if (u < g.n_nodes && g.out_ptr[u + 1] == g.out_ptr[u]) tout[u] = tin[u];
+        return;
+    }
+    const unsigned long long m = __ballot(flipped);
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(flips, (int)__popcll(m));
+}
 }  // namespace
 
 extern "C" {
@@ -75,9 +158,30 @@ int gtf_tag_sweep(const gtf_graph* g, const uint8_t* keep, const uint8_t* proces
     if (int rc = gtf::check_abi(g, "gtf_tag_sweep")) return rc;
     hipStream_t st = (hipStream_t)stream;
     if (hipMemsetAsync(flips, 0, sizeof(int32_t), st) != hipSuccess) return -1;
-    if (g->n_nodes > 0)
+    if (g->n_nodes > 0 && g->out_sched) {   // lane groups over the sender schedule
+        TagBuckets tb;
+        const int cnt[3] = {g->n_o4, g->n_o8, g->n_o16}, gs[3] = {4, 8, 16};
+        const int4* l = reinterpret_cast<const int4*>(g->out_sched);
+        const int2* ln = reinterpret_cast<const int2*>(g->out_lanes);
+        tb.lanes[0] = ln;
+        tb.lanes[1] = ln ? ln + 4 * g->n_o4 : nullptr;
+        int total = 0;
+        for (int q = 0; q < 3; q++) {
+            tb.list[q] = l;
+            l += cnt[q];
+            tb.count[q] = cnt[q];
+            tb.blocks[q] = (cnt[q] + BLOCK / gs[q] - 1) / (BLOCK / gs[q]);
+            total += tb.blocks[q];
+        }
+        tb.copy_blocks = (g->n_nodes + BLOCK - 1) / BLOCK;   // nodes without an out-edge are not scheduled
+        total += tb.copy_blocks;
+        if (total > 0)
+            hipLaunchKernelGGL(k_tag_sweep_sched, dim3(total), dim3(BLOCK), 0, st, *g, keep, processed, tags_in,
+                               tags_out, flips, tb);
+    } else if (g->n_nodes > 0) {
         hipLaunchKernelGGL(k_tag_sweep, dim3((g->n_nodes + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, st, *g, keep,
                            processed, tags_in, tags_out, flips);
+    }
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -296,7 +296,9 @@ int gtf_halo_unpack(gtf_nodes* n, gtf_edges* e, const gtf_halo* h, const void* b
  * processed: [N] u8 output; n_processed: device int32 output. */
 int gtf_tag_prepare(const gtf_graph* g, const double* radius, uint8_t* keep, uint8_t* processed,
                     int32_t* n_processed, gtf_stream_t stream);
-/* one Jacobi sweep: tags_out[u] = max(tags_in[u], tags_in[kept neighbours]); flips += changes */
+/* one Jacobi sweep: tags_out[u] = max(tags_in[u], tags_in[kept neighbours]); *flips = the
+ * number of changed tags (zeroed first). With g->out_sched (and out_lanes) the sweep runs
+ * on the sender schedule's lane groups, otherwise one thread per node. */
 int gtf_tag_sweep(const gtf_graph* g, const uint8_t* keep, const uint8_t* processed,
                   const int64_t* tags_in, int64_t* tags_out, int32_t* flips, gtf_stream_t stream);
 

@@ -281,8 +281,51 @@ def bench_components(g, params, dev, reps=5):
                                   "note": "sweep_call_ms: K gtf_tag_sweep calls back to back between two events "
                                           "(flip-counter reset + kernel); stage wall time includes the prepare pass "
                                           "and the flip-count read-back after every sweep (the script's stop test)"}
+    # a2: the initial per-edge states of event conversion (helper.py:238-452 + priors,
+    # mixture weights, degree; pipeline.build_event's device half) on the same event
+    def tse():
+        d.track_state_estimates(params)
+        d.node_ops(["priors_tse", "mw_tse", "degree"], params)
+    tse()
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(10):
+        tse()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / 10
+    out["a2_initial_states"] = {"edges": g.n_edges, "call_ms": ms, "edges_per_s": g.n_edges / (ms * 1e-3),
+                                "reference_cpu_edges_per_s": 18900,
+                                "note": "gtf_track_state_estimates + gtf_node_ops(priors, weights, degree), 10 calls "
+                                        "back to back between two events; reference figure: its own helper.py on the "
+                                        "134 all-volume event, 1 core (BASELINE.md)"}
+    d.raise_errors()
     del d
+    out["f_pipeline_vol7"] = bench_pipeline_vol7(params, dev)
     return out
+
+
+def bench_pipeline_vol7(params, dev):
+    """event conversion (CSV -> CSR in C++, states on the device) and
+    the three iterations of run_gnn_trackml_mod.sh in one process on the committed
+    volume-7 134 event, wall times per stage (second run; the first loads code objects).
+    The candidate counts are the reference's own (1,055 / 110 / 2)."""
+    import torch
+    from gtf import pipeline
+    prefix = os.path.join(ROOT, "tests", "golden", "kat134", "event_1_filtered_graph_")
+    res = None
+    for _ in range(2):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        g7, vivl = pipeline.build_event(prefix, 7, 7, params, dev)
+        t1 = time.perf_counter()
+        its = pipeline.run(g7, vivl, 3, params, device=dev)
+        t2 = time.perf_counter()
+        res = {"event": "vol-7 134 (%d nodes, %d directed edges)" % (g7.n_nodes, g7.n_edges),
+               "event_conversion_s": t1 - t0, "three_iterations_s": t2 - t1,
+               "iterations": [{"stage": it.stage, "candidates": len(it.candidates),
+                               "seconds": {k: round(v, 5) for k, v in it.seconds.items()}} for it in its]}
+    return res
 
 
 def device_copy_gbps(dev, nbytes=1 << 30, reps=10):

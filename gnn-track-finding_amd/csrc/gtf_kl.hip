@@ -50,13 +50,22 @@ __device__ __forceinline__ Frame node_frame_xy(double x, double y) {
     f.x = x;
     f.y = y;
     const double h = sqrt(f.x * f.x + f.y * f.y);
-    f.ca = h > 0.0 ? f.x / h : 1.0;
-    f.sa = h > 0.0 ? -f.y / h : 0.0;
+    const double rh = 1.0 / h;   // one reciprocal for both
+    f.ca = h > 0.0 ? f.x * rh : 1.0;
+    f.sa = h > 0.0 ? -f.y * rh : 0.0;
     f.xt = f.x * f.ca - f.y * f.sa;
     f.yt = f.x * f.sa + f.y * f.ca;
     f.x0 = 0.0 - f.xt;  // the old origin (0, 0) rotates to (0, 0)
     return f;
 }
+
+// GNN_Measurement x / y of node v: rows of gnn_stride doubles (4: x, y, z, r; 2: the
+// compact x, y copy, half the bytes of the four-field rows)
+__device__ __forceinline__ int64_t gnn_row(const gtf_kl_graph& g, int v) {
+    return (int64_t)(g.gnn_stride ? g.gnn_stride : 4) * v;
+}
+__device__ __forceinline__ double gx(const gtf_kl_graph& g, int v) { return g.gnn[gnn_row(g, v)]; }
+__device__ __forceinline__ double gy(const gtf_kl_graph& g, int v) { return g.gnn[gnn_row(g, v) + 1]; }
 
 template <typename T>
 struct PState {
@@ -74,7 +83,8 @@ __device__ __forceinline__ PState<T> pstate(const Frame& f, double xb, double yb
     singular = (xB == 0.0) || (xB == x0) || (x0 == 0.0);
     const double s0d = 4.0 * 4.0, s1d = 0.1 * 0.1;   // sigma0**2, sigmaA**2 = sigmaB**2 (:223-229)
     if (sv_out || cov_out) {
-        const double r0 = 1.0 / (x0 * (x0 - xB)), r1 = 1.0 / (x0 * xB), r2 = 1.0 / (xB * (xB - x0));
+        const double rD = 1.0 / (x0 * xB * (x0 - xB));
+        const double r0 = xB * rD, r1 = (x0 - xB) * rD, r2 = -x0 * rD;
         const double L0[3] = {r0, -xB * r0, 0.0};
         const double L1[3] = {r1, -(x0 + xB) * r1, 1.0};
         const double L2[3] = {r2, -x0 * r2, 0.0};
@@ -86,7 +96,9 @@ __device__ __forceinline__ PState<T> pstate(const Frame& f, double xb, double yb
     }
     const T X0 = (T)x0, XB = (T)xB, MB = (T)mB;
     const T s0 = (T)s0d, s1 = (T)s1d;
-    const T r0 = T(1) / (X0 * (X0 - XB)), r1 = T(1) / (X0 * XB), r2 = T(1) / (XB * (XB - X0));
+    // the three Lagrange denominators share one reciprocal: D = x0 xB (x0 - xB)
+    const T rD = T(1) / (X0 * XB * (X0 - XB));
+    const T r0 = XB * rD, r1 = (X0 - XB) * rD, r2 = -X0 * rD;
     const T a0 = r0, b0 = -XB * r0;
     const T a1 = r1, b1 = -(X0 + XB) * r1;
     const T a2 = r2, b2 = -X0 * r2;
@@ -153,7 +165,7 @@ __device__ __forceinline__ void pkl_node(const gtf_kl_graph& g, const gtf_kl_out
     const int lo = g.slot_ptr[v], d = g.slot_ptr[v + 1] - lo;
     if (d < 1) return;
     Stage* stg = (Stage*)smem + (int)threadIdx.x / G;
-    const Frame f = node_frame_xy(g.gnn[4 * (int64_t)v], g.gnn[4 * (int64_t)v + 1]);
+    const Frame f = node_frame_xy(gx(g, v), gy(g, v));
 
     // states of the node's in-edges and the gradients dy/dx (utils.py:249-254, 273-283)
     double gsum = 0.0, gr0 = 0.0;
@@ -161,7 +173,7 @@ __device__ __forceinline__ void pkl_node(const gtf_kl_graph& g, const gtf_kl_out
     for (int q = gl; q < d; q += G) {
         const int k = lo + q;
         const int u = g.slot_src[k];
-        const double xb = g.gnn[4 * (int64_t)u], yb = g.gnn[4 * (int64_t)u + 1];
+        const double xb = gx(g, u), yb = gy(g, u);
         bool s;
         const PState<T> p = pstate<T>(f, xb, yb, s, STATES ? o.sv + 3 * (int64_t)k : nullptr,
                                       STATES ? o.cov + 9 * (int64_t)k : nullptr);
@@ -182,7 +194,7 @@ __device__ __forceinline__ void pkl_node(const gtf_kl_graph& g, const gtf_kl_out
             double gr = gr0;
             if (q != gl) {
                 const int u = g.slot_src[lo + q];
-                gr = (f.y - g.gnn[4 * (int64_t)u + 1]) / (f.x - g.gnn[4 * (int64_t)u]);
+                gr = (f.y - gy(g, u)) / (f.x - gx(g, u));
             }
             vs += (gr - mean) * (gr - mean);
         }
@@ -212,8 +224,8 @@ __device__ __forceinline__ void pkl_node(const gtf_kl_graph& g, const gtf_kl_out
         } else {  // beyond the LDS stage (wavefront bucket, d > 64): recompute both states
             bool s;
             const int ui = g.slot_src[lo + i], uj = g.slot_src[lo + j];
-            a = pstate<T>(f, g.gnn[4 * (int64_t)ui], g.gnn[4 * (int64_t)ui + 1], s, nullptr, nullptr);
-            b = pstate<T>(f, g.gnn[4 * (int64_t)uj], g.gnn[4 * (int64_t)uj + 1], s, nullptr, nullptr);
+            a = pstate<T>(f, gx(g, ui), gy(g, ui), s, nullptr, nullptr);
+            b = pstate<T>(f, gx(g, uj), gy(g, uj), s, nullptr, nullptr);
             if (o.truth) { ti = g.truth[ui]; tj = g.truth[uj]; }
         }
         kl[base + t] = pkl<T>(a, b);
@@ -239,12 +251,12 @@ __device__ __forceinline__ void pkl_node1_ordered(const gtf_kl_graph& g, const g
     const bool two = gi >= g.n_d1;
     const int64_t l = g.slot0 + (two ? g.n_d1 + 2 * (int64_t)(gi - g.n_d1) : gi);
     const int64_t pp = g.pair0 + (gi - g.n_d1);
-    const double xv = g.gnn[4 * (int64_t)v], yv = g.gnn[4 * (int64_t)v + 1];
+    const double xv = gx(g, v), yv = gy(g, v);
     const long long tv = (o.truth && g.truth) ? g.truth[v] : 0;
     const int u0 = g.slot_src[l];
     const int u1 = two ? g.slot_src[l + 1] : u0;
-    const double x0 = g.gnn[4 * (int64_t)u0], y0 = g.gnn[4 * (int64_t)u0 + 1];
-    const double x1 = g.gnn[4 * (int64_t)u1], y1 = g.gnn[4 * (int64_t)u1 + 1];
+    const double x0 = gx(g, u0), y0 = gy(g, u0);
+    const double x1 = gx(g, u1), y1 = gy(g, u1);
     long long t0 = 0, t1 = 0;
     if (o.truth && g.truth) { t0 = g.truth[u0]; t1 = g.truth[u1]; }
     const Frame f = node_frame_xy(xv, yv);
@@ -255,9 +267,9 @@ __device__ __forceinline__ void pkl_node1_ordered(const gtf_kl_graph& g, const g
     if ((s0 || s1) && o.err) atomicOr(o.err, (uint32_t)GTF_ERR_SINGULAR_H);
     const double g0 = (f.y - y0) / (f.x - x0);
     const double g1 = two ? (f.y - y1) / (f.x - x1) : g0;
-    const double d = two ? 2.0 : 1.0;
-    const double mean = (two ? g0 + g1 : g0) / d;
-    if (o.emp_var) o.emp_var[v] = (two ? (g0 - mean) * (g0 - mean) + (g1 - mean) * (g1 - mean) : 0.0 * (g0 - mean)) / d;
+    // / 2 and / 1 as exact scalings
+    const double mean = two ? (g0 + g1) * 0.5 : g0;
+    if (o.emp_var) o.emp_var[v] = two ? ((g0 - mean) * (g0 - mean) + (g1 - mean) * (g1 - mean)) * 0.5 : 0.0 * (g0 - mean);
     if (o.emp_mean) o.emp_mean[v] = mean;
     if (two) {
         ((T*)o.kl)[pp] = pkl<T>(b, a);   // pair (i, j) = (1, 0)
@@ -283,8 +295,8 @@ __device__ __forceinline__ void pkl_node1(const gtf_kl_graph& g, const gtf_kl_ou
         if (v[j] >= 0) {
             lo[j] = g.slot_ptr[v[j]];
             d[j] = g.slot_ptr[v[j] + 1] - lo[j];
-            xv[j] = g.gnn[4 * (int64_t)v[j]];
-            yv[j] = g.gnn[4 * (int64_t)v[j] + 1];
+            xv[j] = gx(g, v[j]);
+            yv[j] = gy(g, v[j]);
             pp[j] = g.pair_ptr[v[j]];
             tv[j] = (o.truth && g.truth) ? g.truth[v[j]] : 0;
         }
@@ -299,10 +311,10 @@ __device__ __forceinline__ void pkl_node1(const gtf_kl_graph& g, const gtf_kl_ou
 #pragma unroll
     for (int j = 0; j < NPT; j++)
         if (d[j]) {
-            x0[j] = g.gnn[4 * (int64_t)u0[j]];
-            y0[j] = g.gnn[4 * (int64_t)u0[j] + 1];
-            x1[j] = g.gnn[4 * (int64_t)u1[j]];
-            y1[j] = g.gnn[4 * (int64_t)u1[j] + 1];
+            x0[j] = gx(g, u0[j]);
+            y0[j] = gy(g, u0[j]);
+            x1[j] = gx(g, u1[j]);
+            y1[j] = gy(g, u1[j]);
             if (o.truth && g.truth) {
                 t0[j] = g.truth[u0[j]];
                 t1[j] = g.truth[u1[j]];
@@ -418,6 +430,10 @@ extern "C" int gtf_parabolic_kl(const gtf_kl_graph* g, int32_t dtype, const gtf_
         for (int i = 0; i < 4; i++)
             ok = ok && g->first[i] >= 0 && (int64_t)g->first[i] + g->count[i] <= g->n_nodes;
         if (!ok) { gtf::set_error("gtf_parabolic_kl: bad ordered layout"); return -2; }
+    }
+    if (g->gnn_stride != 0 && g->gnn_stride != 2 && g->gnn_stride != 4) {
+        gtf::set_error("gtf_parabolic_kl: gnn_stride must be 0, 2 or 4");
+        return -2;
     }
     if (listed && (!g->slot_ptr || !g->slot_src || !g->gnn || !g->pair_ptr || !out->kl)) {
         gtf::set_error("gtf_parabolic_kl: missing arrays");

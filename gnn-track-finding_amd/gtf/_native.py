@@ -102,7 +102,7 @@ class GtfCandidateGraph(ctypes.Structure):
 class GtfKlGraph(ctypes.Structure):
     _fields_ = [("n_nodes", I32), ("n_slots", I32), ("slot_ptr", P), ("slot_src", P), ("gnn", P), ("truth", P),
                 ("pair_ptr", P), ("list", P * 4), ("count", I32 * 4), ("first", I32 * 4), ("n_d1", I32),
-                ("pad_", I32), ("slot0", ctypes.c_int64), ("pair0", ctypes.c_int64)]
+                ("gnn_stride", I32), ("slot0", ctypes.c_int64), ("pair0", ctypes.c_int64)]
 
 
 class GtfPairOut(ctypes.Structure):

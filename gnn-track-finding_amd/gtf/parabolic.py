@@ -97,7 +97,9 @@ class ParabolicKL:
         t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
         self.slot_ptr = t(slot_ptr)
         self.slot_src = t(np.asarray(slot_src, np.int32))
-        self.gnn = t(np.asarray(gnn, np.float64).reshape(-1, 4))
+        # the kernel reads GNN_Measurement x and y only: a compact [N, 2] copy (gnn_stride 2)
+        # halves the bytes of the node and neighbour coordinate gathers
+        self.gnn = t(np.asarray(gnn, np.float64).reshape(-1, 4)[:, :2])
         self.truth = t(np.asarray(truth, np.int64)) if truth is not None else None
         self.pair_ptr = t(pair_ptr)
         self.lists = [t(x) for x in lists]
@@ -110,12 +112,12 @@ class ParabolicKL:
             self._g = nat.GtfKlGraph(self.n_nodes, self.n_slots, _ptr(self.slot_ptr), _ptr(self.slot_src),
                                      _ptr(self.gnn), _ptr(self.truth), _ptr(self.pair_ptr),
                                      (ctypes.c_void_p * 4)(), (ctypes.c_int32 * 4)(*counts),
-                                     (ctypes.c_int32 * 4)(*first.tolist()), n1, 0, 0, 0)
+                                     (ctypes.c_int32 * 4)(*first.tolist()), n1, 2, 0, 0)
         else:
             self._g = nat.GtfKlGraph(self.n_nodes, self.n_slots, _ptr(self.slot_ptr), _ptr(self.slot_src),
                                      _ptr(self.gnn), _ptr(self.truth), _ptr(self.pair_ptr),
                                      (ctypes.c_void_p * 4)(*[x.data_ptr() if x.numel() else None for x in self.lists]),
-                                     (ctypes.c_int32 * 4)(*[x.numel() for x in self.lists]))
+                                     (ctypes.c_int32 * 4)(*[x.numel() for x in self.lists]), gnn_stride=2)
 
     @classmethod
     def from_graph(cls, g: TrackGraph, truth=None, device="cuda", with_single=False):

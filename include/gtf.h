@@ -408,7 +408,7 @@ typedef struct gtf_kl_graph {
     int32_t n_nodes, n_slots;
     const int32_t* slot_ptr;  /* [N+1] in-edge CSR (every slot an edge) */
     const int32_t* slot_src;  /* [S] neighbour of each in-edge */
-    const double* gnn;        /* [N*4] GNN_Measurement x, y, z, r */
+    const double* gnn;        /* [N*gnn_stride] GNN_Measurement x, y(, z, r) */
     const int64_t* truth;     /* [N] truth_particle, or NULL */
     const int64_t* pair_ptr;  /* [N+1] */
     const int32_t* list[4];   /* nodes to process by in-degree bucket, any order within a bucket:
@@ -423,7 +423,8 @@ typedef struct gtf_kl_graph {
      * neighbours and pairs by arithmetic, and every bucket's nodes without a list load. */
     int32_t first[4];
     int32_t n_d1;
-    int32_t pad_;
+    int32_t gnn_stride;       /* doubles per gnn row: 0 or 4 (x, y, z, r), or 2 (a compact x, y copy:
+                                 the kernel reads only x and y, so half the gathered bytes) */
     int64_t slot0;
     int64_t pair0;
 } gtf_kl_graph;

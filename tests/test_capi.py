@@ -100,3 +100,14 @@ def test_abi_mismatch_is_refused_without_a_gpu():
     rc = L.gtf_updated_state_pair_counts(ctypes.byref(g), ctypes.byref(nat.GtfNodes()), ctypes.byref(nat.GtfStates()),
                                          ctypes.byref(nat.GtfEdges()), ctypes.byref(cnt), z)
     assert rc == -3 and b"ABI mismatch" in L.gtf_last_error()
+
+
+def test_kl_gnn_stride_is_checked_without_a_gpu():
+    """gtf_parabolic_kl refuses a gnn_stride other than 0, 2 or 4 (-2) before any device work"""
+    from gtf import _native as nat
+    if not os.path.exists(nat.LIB_PATH):
+        pytest.skip("libgtf.so not built")
+    L = nat.lib()
+    g = nat.GtfKlGraph(n_nodes=0, n_slots=0, gnn_stride=3)
+    rc = L.gtf_parabolic_kl(ctypes.byref(g), 0, ctypes.byref(nat.GtfKlOut()), ctypes.c_void_p(0))
+    assert rc == -2 and b"gnn_stride" in L.gtf_last_error()

@@ -214,3 +214,28 @@ def test_gpu_ordered_layout_equals_lists(with_single):
     for f in a:
         x, y = a[f], b[f]
         assert np.array_equal(x, y, equal_nan=x.dtype.kind == "f"), f
+
+
+@pytest.mark.parametrize("stride", [0, 4])
+def test_gpu_four_field_rows_equal_compact(stride):
+    """gtf_kl_graph.gnn_stride 0 / 4 (the GNN_Measurement x, y, z, r rows themselves)
+    gives the compact x, y copy's (gnn_stride 2, what ParabolicKL uploads) results bit
+    for bit, in both layouts"""
+    import ctypes
+    import torch
+    from gtf import io, parabolic
+    kat = os.path.join(GOLDEN, "kat134")
+    g = io.load_event(os.path.join(kat, "event_1_filtered_graph_"), 7, 7)
+    truth = io.read_truth(os.path.join(kat, "truth_vol7.csv"), g.node["node_id"])
+    ptr, src = parabolic.in_edge_csr(g)
+    for ordered in (False, True):
+        k = parabolic.ParabolicKL(ptr, src, g.node["gnn"], truth, ordered=ordered)
+        a = k.run(k.alloc("f64", emp=True), "f64")
+        rows = g.node["gnn"] if k.node_of is None else g.node["gnn"][k.node_of]
+        full = torch.from_numpy(np.ascontiguousarray(rows, np.float64)).to(k.device)
+        k._g.gnn, k._g.gnn_stride = ctypes.c_void_p(full.data_ptr()), stride
+        b = k.run(k.alloc("f64", emp=True), "f64")
+        for f in ("kl", "truth", "emp_var", "emp_mean"):
+            assert torch.equal(a[f], b[f]) or (a[f].dtype.is_floating_point and
+                                               torch.equal(a[f].nan_to_num(7.0), b[f].nan_to_num(7.0))), f
+        assert k.errors() == 0

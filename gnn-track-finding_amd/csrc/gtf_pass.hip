@@ -29,7 +29,7 @@ constexpr int MAX_CLUSTER = 15;  // clustering.py:207 (2 < d < 16)
 
 struct Ws {
     uint32_t* err;    // error word
-    double2* vc;      // [S] per active edge, by SLOT: (var_ms, merged_cov[1,1] its extrapolation sees)
+    double* vc;       // [S] per active edge, by SLOT: the merged_cov[1,1] its extrapolation sees
 };
 
 __host__ inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
@@ -40,7 +40,7 @@ __host__ inline Ws carve(void* base, int32_t n_nodes, int32_t n_slots) {
     Ws w;
     w.err = (uint32_t*)p;
     p += 256;
-    w.vc = (double2*)p;
+    w.vc = (double*)p;
     return w;
 }
 
@@ -84,8 +84,9 @@ __device__ __forceinline__ double highland_var_ms(double a, double b, const doub
 // sequential sum over the lanes before it (shuffles, the reference's addition
 // order), and the last value is the array the stage saves. Inactive out-edges do
 // not take part (:431). Out-list reads are contiguous per sender; each active edge's
-// (var_ms, running value) record goes to the edge's slot, where k_extrapolate reads
-// it coalesced instead of gathering it through the sender's out-list.
+// running value (8 bytes) goes to the edge's slot, where k_extrapolate reads it
+// coalesced instead of gathering it through the sender's out-list (and recomputes the
+// edge's own var_ms from operands it loads anyway).
 // ---------------------------------------------------------------------------
 // one sender u over its out-list [ob, oe) with SG lanes (lane gl), chunks of SG
 template <int SG>
@@ -116,9 +117,9 @@ __device__ __forceinline__ void sender_scan(const gtf_graph& g, gtf_nodes& n, co
             const double vmm = __shfl(vm, m, SG);
             if (m <= gl && vmm != -1.0) c = c + vmm;
         }
-        // one 16-byte record per active edge, stored at its slot: the extrapolation
+        // the running value of each active edge, stored at its slot: the extrapolation
         // thread of that slot reads it coalesced
-        if (vm != -1.0) w.vc[k] = make_double2(vm, c);
+        if (vm != -1.0) w.vc[k] = c;
         carry = __shfl(c, SG - 1, SG);  // lanes past the end carry the full sum
     }
     if (gl == 0) n.merged_cov[5 * (int64_t)u + 3] = carry;
@@ -148,7 +149,7 @@ __device__ __forceinline__ void sender_scan_lane(const gtf_graph& g, gtf_nodes& 
         const double vmm = __shfl(vm, m, G);
         if (m <= gl && vmm != -1.0) c = c + vmm;
     }
-    if (vm != -1.0) w.vc[k] = make_double2(vm, c);
+    if (vm != -1.0) w.vc[k] = c;
     const double fin = __shfl(c, G - 1, G);   // the last lane has every active edge's term
     if (gl == 0) n.merged_cov[5 * (int64_t)u + 3] = fin;
 }
@@ -226,7 +227,7 @@ __global__ void __launch_bounds__(BLOCK) k_extrapolate(gtf_graph g, gtf_nodes n,
     // exits would otherwise serialise each load behind the previous one's branch).
     const uint8_t is_edge = g.is_edge[k], act = e.act[k];
     const int src = g.slot_src[k], v = g.slot_dst[k];
-    const double2 vc = w.vc[k];        // written by k_sender for active edges of merged senders
+    const double vc = w.vc[k];         // written by k_sender for active edges of merged senders
     const double smw = e.send_mw[k];
     const int u = src >= 0 ? src : 0;   // orphan keys have no sender
     const double* ng = g.gnn + 4 * (int64_t)u;  // sender ("node" in the reference)
@@ -284,8 +285,11 @@ __global__ void __launch_bounds__(BLOCK) k_extrapolate(gtf_graph g, gtf_nodes n,
     const double dc_dc = (ds_dc * bracket) + cp;
     const Mat3 F = {{{da_da, da_db, da_dc}, {db_da, db_db, db_dc}, {dc_da, dc_db, dc_dc}}};
 
-    const double var_ms = vc.x;
-    const Mat3 C = {{{mc00, mc01, 0.0}, {mc10, vc.y, 0.0}, {0.0, 0.0, mc22}}};  // :128
+    // var_ms again from the operands k_sender used (the same bits): 8 bytes per slot
+    // cross the two kernels instead of 16
+    const double ngv[4] = {node_x, node_y, node_z, node_r}, nbv[4] = {nbx, nby, nbz, nbr};
+    const double var_ms = highland_var_ms(a, b, ngv, nbv, p.endcap_boundary);
+    const Mat3 C = {{{mc00, mc01, 0.0}, {mc10, vc, 0.0}, {0.0, 0.0, mc22}}};  // :128
     const double m[3] = {a, b, c};
     double xe[3];
     mv3(F, m, xe);                                                                 // :129
@@ -945,7 +949,7 @@ extern "C" {
 
 size_t gtf_workspace_bytes(int32_t n_nodes, int32_t n_slots) {
     (void)n_nodes;
-    return 256 + align256(2 * sizeof(double) * (size_t)(n_slots > 0 ? n_slots : 1));
+    return 256 + align256(sizeof(double) * (size_t)(n_slots > 0 ? n_slots : 1));
 }
 
 int gtf_clear_errors(void* ws, gtf_stream_t stream) {

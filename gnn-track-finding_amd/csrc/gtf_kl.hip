@@ -347,6 +347,76 @@ __device__ __forceinline__ void pkl_node1(const gtf_kl_graph& g, const gtf_kl_ou
     }
 }
 
+// 3 <= d <= 4: one thread per node as well, its <= 4 states in registers and its <= 6
+// pairs written back to back (no LDS stage, no group shuffles, every lane busy; the
+// gradient moments summed in neighbour order, numpy's order). GTF_KL_B1_LANES=1: the
+// 4-lane groups of pkl_node instead.
+#ifndef GTF_KL_B1_LANES
+#define GTF_KL_B1_LANES 0
+#endif
+template <typename T, bool STATES>
+__device__ __forceinline__ void pkl_node4(const gtf_kl_graph& g, const gtf_kl_out& o, const int32_t* list, int count,
+                                          int bid, int first) {
+    const int gi = bid * BLOCK + (int)threadIdx.x;
+    if (gi >= count) return;
+    const int v = list ? list[gi] : first + gi;
+    const int lo = g.slot_ptr[v], d = g.slot_ptr[v + 1] - lo;
+    const int64_t base = g.pair_ptr[v];
+    const double xv = gx(g, v), yv = gy(g, v);
+    const long long tv = (o.truth && g.truth) ? g.truth[v] : 0;
+    if (d < 1 || d > 4) return;
+    int u[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) u[q] = q < d ? g.slot_src[lo + q] : 0;
+    double xb[4], yb[4];
+    long long tu[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        xb[q] = q < d ? gx(g, u[q]) : 0.0;
+        yb[q] = q < d ? gy(g, u[q]) : 0.0;
+        tu[q] = (q < d && o.truth && g.truth) ? g.truth[u[q]] : 0;
+    }
+    const Frame f = node_frame_xy(xv, yv);
+    PState<T> st[4];
+    double gr[4];
+    bool sing = false;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        if (q < d) {
+            bool s;
+            st[q] = pstate<T>(f, xb[q], yb[q], s, STATES ? o.sv + 3 * (int64_t)(lo + q) : nullptr,
+                              STATES ? o.cov + 9 * (int64_t)(lo + q) : nullptr);
+            sing |= s;
+            gr[q] = (f.y - yb[q]) / (f.x - xb[q]);
+        }
+    }
+    if (sing && o.err) atomicOr(o.err, (uint32_t)GTF_ERR_SINGULAR_H);
+    if (o.emp_var || o.emp_mean) {
+        double sm = gr[0];
+#pragma unroll
+        for (int q = 1; q < 4; q++)
+            if (q < d) sm = sm + gr[q];
+        const double mean = sm / (double)d;
+        double vs = (gr[0] - mean) * (gr[0] - mean);
+#pragma unroll
+        for (int q = 1; q < 4; q++)
+            if (q < d) vs = vs + (gr[q] - mean) * (gr[q] - mean);
+        if (o.emp_var) o.emp_var[v] = vs / (double)d;
+        if (o.emp_mean) o.emp_mean[v] = mean;
+    }
+    T* kl = (T*)o.kl;
+    int t = 0;
+#pragma unroll
+    for (int i = 1; i < 4; i++)
+#pragma unroll
+        for (int j = 0; j < i; j++)
+            if (i < d) {
+                kl[base + t] = pkl<T>(st[i], st[j]);
+                if (o.truth) o.truth[base + t] = (int8_t)(tv == tu[i] && tu[i] == tu[j] && tv == tu[j]);
+                t++;
+            }
+}
+
 struct KlBuckets {
     int32_t blocks[4];
     int32_t ordered;   // gtf_kl_graph's ordered layout (every list NULL)
@@ -378,7 +448,8 @@ __global__ void __launch_bounds__(BLOCK) KL_ATTR k_parabolic_kl(gtf_kl_graph g, 
     }
     b -= bk.blocks[2];
     if (b < bk.blocks[1]) {
-        pkl_node<T, 4, STATES>(g, o, g.list[1], g.count[1], gtf::xcd_local(b, bk.blocks[1]), smem, g.first[1]);
+        if (GTF_KL_B1_LANES) pkl_node<T, 4, STATES>(g, o, g.list[1], g.count[1], gtf::xcd_local(b, bk.blocks[1]), smem, g.first[1]);
+        else pkl_node4<T, STATES>(g, o, g.list[1], g.count[1], gtf::xcd_local(b, bk.blocks[1]), g.first[1]);
         return;
     }
     b -= bk.blocks[1];
@@ -392,7 +463,8 @@ int launch(const gtf_kl_graph* g, const gtf_kl_out* o, hipStream_t st) {
     bk.ordered = !g->list[0] && !g->list[1] && !g->list[2] && !g->list[3];
     int total = 0;
     for (int i = 0; i < 4; i++) {
-        const int per_block = i == 0 ? (bk.ordered ? BLOCK : BLOCK * NPT) : BLOCK / BG[i];   // nodes per block
+        int per_block = i == 0 ? (bk.ordered ? BLOCK : BLOCK * NPT) : BLOCK / BG[i];   // nodes per block
+        if (i == 1 && !GTF_KL_B1_LANES) per_block = BLOCK;
         bk.blocks[i] = gtf::pad8((g->count[i] + per_block - 1) / per_block);
         total += bk.blocks[i];
     }

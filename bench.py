@@ -29,7 +29,8 @@ owns the receivers of its wedge, one halo all-to-all over RCCL per pass), total 
 fixed ("scaling": "strong"; at N = 1 the same event on one GPU). value = the event's
 edges x steps / max elapsed over ranks, with the barrier + synchronize bracket. The
 line also carries "event_replicas": every rank running its own C4 event (independent
-events, no collective, "weak").
+events, no collective, "weak"), and "c5_event_sharded": config 5 sharded by event, every
+rank its own 256-event batch ("weak", no collective).
 
 CPU baselines (rank 0, N = 1 only): the repository's NumPy restatement of the pass
 (oracle/gtf_oracle.py, kind "port", 1 core) on a bounded sample event of the same
@@ -328,6 +329,40 @@ def bench_pipeline_vol7(params, dev):
     return res
 
 
+def bench_c5_sharded(dev, steps, warmup, rank, world, backend, n_events=256):
+    """Config 5 event-sharded across the ranks (events are independent, no
+    exchange): every rank runs its own 256-event batch (jitter seed per rank), fp64, K
+    launches bracketed by barrier + synchronize, max over ranks. Per-rank work is fixed
+    as N grows ("weak")."""
+    import torch
+    import torch.distributed as dist
+    from gtf import io, parabolic
+    kat = os.path.join(ROOT, "tests", "golden", "kat134")
+    g = io.load_event(os.path.join(kat, "event_1_filtered_graph_"), 7, 7)
+    truth = io.read_truth(os.path.join(kat, "truth_vol7.csv"), g.node["node_id"])
+    ptr, src = parabolic.in_edge_csr(g)
+    ptr, src, gnn, tr = parabolic.batch(ptr, src, g.node["gnn"], truth, n_events, seed=rank)
+    k = parabolic.ParabolicKL(ptr, src, gnn, tr, dev, ordered=True)
+    out = k.alloc("f64", emp="var")
+    for _ in range(warmup):
+        k.run(out, "f64")
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        k.run(out, "f64")
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    el = reduce_scalar(time.perf_counter() - t0, dist.ReduceOp.MAX, dev, backend)
+    pairs = reduce_scalar(float(k.n_pairs), dist.ReduceOp.SUM, dev, backend)
+    flags = int(reduce_scalar(k.errors(), dist.ReduceOp.MAX, dev, backend))
+    return {"scaling": "weak", "n_gpus": world, "events_per_rank": n_events, "pairs_total": int(pairs),
+            "pairs_per_s": pairs * steps / el, "ms_per_launch": el / steps * 1e3, "dtype": "f64",
+            "collective": "none (events are independent)", "device_error_flags": flags}
+
+
 def device_copy_gbps(dev, nbytes=1 << 30, reps=10):
     """measured device-to-device copy bandwidth (bytes read + written per second), the
     practical HBM ceiling SURVEY §8d asks the roofline to be quoted against beside the
@@ -568,10 +603,15 @@ def main():
         except Exception as ex:   # reported; the line then carries the replicas only and is marked
             sharded = {"error": repr(ex)[:300]}
 
-    c5 = comps = None
+    c5 = comps = c5_sharded = None
     if rank == 0 and world == 1 and not args.no_c5:
         c5 = bench_c5(dev, K, W)
         comps = bench_components(g, p, dev)
+    if world > 1 and not args.no_c5:
+        try:
+            c5_sharded = bench_c5_sharded(dev, K, W, rank, world, args.backend)
+        except Exception as ex:   # reported, the headline stands
+            c5_sharded = {"error": repr(ex)[:300]}
 
     cpu = cpu_cpp = dropin = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -616,6 +656,8 @@ def main():
             "c5_parabolic_kl": c5,
             "other_path_stages": comps,
         }
+        if c5_sharded is not None:
+            out["c5_event_sharded"] = c5_sharded
         if world > 1:
             replicas = {"value": out["value"], "ms_per_step": out["ms_per_step"], "scaling": "weak",
                         "parallelism": "event-parallel x%d (each rank its own C4 event, no collective)" % world,

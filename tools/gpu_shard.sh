@@ -5,5 +5,5 @@ set -e
 mkdir -p gpurun_out/shard
 timeout -k 10 300 python -u -m pytest tests/test_shard.py -v --timeout 200 --timeout-method thread > gpurun_out/shard/tests.log 2>&1
 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 \
-  bench.py --gpus 2 --steps 10 --warmup 2 --backend gloo --no-c5 > gpurun_out/shard/bench2.log 2>&1
+  bench.py --gpus 2 --steps 10 --warmup 2 --backend gloo > gpurun_out/shard/bench2.log 2>&1
 echo shard-done

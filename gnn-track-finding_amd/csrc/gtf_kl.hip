@@ -423,10 +423,12 @@ struct KlBuckets {
 };
 
 // one launch over the four buckets; wavefront-bucket blocks first (longest-running)
-// 6 waves per SIMD: fewer VGPRs than the compiler's default pick (measured 10 % faster
-// on config 5 without spills); 8 spills
+// 5 waves per SIMD (96 VGPRs, 6 spilled in the fp64 kernel): the compiler's default pick
+// takes more registers and fewer waves; at 6 waves (80 VGPRs) the 3-4-edge bucket's
+// register-resident states spill 32 (config 5 fp64: 4 waves 26.6 us, 5 waves 25.7 us,
+// 6 waves 28.1 us, 8 waves 44.7 us)
 #ifndef GTF_KL_WAVES
-#define GTF_KL_WAVES 6
+#define GTF_KL_WAVES 5
 #endif
 #define KL_ATTR __attribute__((amdgpu_waves_per_eu(GTF_KL_WAVES)))
 template <typename T, bool STATES>

@@ -2,12 +2,13 @@
 // a17) for gfx950: the training-data generator of learn_KL_parabolic_model
 // (utils.py:221-289 states, extract_metadata_trackml_parabolic_model.py:15-99 pairs).
 //
-// One group of G lanes per node, G by in-degree bucket (one thread for d <= 2 with
-// both states in registers; 4 and 8 lanes for d <= 4, <= 8; one 64-lane wavefront
-// beyond), one in-edge per lane, all buckets in one launch. Each lane forms its neighbour's parabolic
-// state in closed form and stages it in LDS; the group then deals the node's
-// d(d-1)/2 pairs round-robin over its lanes and writes them to the node's
-// contiguous pair range (coalesced: a group's lanes write consecutive pairs).
+// Nodes by in-degree bucket, all buckets in one launch: one thread per node for d <= 4
+// (the states in registers, the pairs written back to back); beyond, one group of G
+// lanes per node (8 lanes for d <= 8, a 64-lane wavefront above), one in-edge per
+// lane: each lane forms its neighbour's parabolic state in closed form and stages it
+// in LDS, and the group deals the node's d(d-1)/2 pairs round-robin over its lanes,
+// writing them to the node's contiguous pair range (consecutive lanes, consecutive
+// pairs).
 //
 // Closed form. The reference inverts H = [[x0^2, x0, 1], [0, 0, 1], [xB^2, xB, 1]]
 // with np.linalg.inv. H maps parabola coefficients (a, b, c) to the parabola's

@@ -412,7 +412,7 @@ typedef struct gtf_kl_graph {
     const int64_t* truth;     /* [N] truth_particle, or NULL */
     const int64_t* pair_ptr;  /* [N+1] */
     const int32_t* list[4];   /* nodes to process by in-degree bucket, any order within a bucket:
-                                 d in [1, 2] (one thread each), [3, 4], [5, 8] (4-, 8-lane groups) and d > 8
+                                 d in [1, 2], [3, 4] (one thread each), [5, 8] (8-lane groups) and d > 8
                                  (one 64-lane wavefront each); d = 1 nodes yield states and
                                  gradient moments but no pairs */
     int32_t count[4];

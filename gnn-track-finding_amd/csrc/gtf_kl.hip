@@ -35,7 +35,12 @@ void set_error(const char* msg);
 
 namespace {
 
-constexpr int BLOCK = 256;
+// one-wavefront blocks: config 5 fp64 25.9-26.1 us at 256 threads, 25.5-25.6 at 128,
+// 25.1-25.4 at 64 (finer-grained dispatch of the mixed buckets), 29.3-29.5 at 512
+#ifndef GTF_KL_BLOCK
+#define GTF_KL_BLOCK 64
+#endif
+constexpr int BLOCK = GTF_KL_BLOCK;
 #ifndef GTF_KL_NPT
 #define GTF_KL_NPT 1
 #endif

@@ -796,10 +796,10 @@ __device__ __forceinline__ void node_seq_body(const gtf_graph& g, gtf_nodes& n, 
     using Q = OpSeq<OPS...>;
     using Stage = StageT<G>;
     NodeCtx<G> c;
-    const int gi = (bid * BLOCK + (int)threadIdx.x) / G;
+    const int gi = (bid * NBLOCK + (int)threadIdx.x) / G;
     if (!node_load(c, g, n, tse, uts, e, list, seg, count, gi, Q::need, ar)) return;
     double* sval = (double*)smem + (threadIdx.x & ~63);
-    Stage* stg = (Stage*)(smem + BLOCK * sizeof(double)) + (Q::cluster ? (int)threadIdx.x / G : 0);
+    Stage* stg = (Stage*)(smem + NBLOCK * sizeof(double)) + (Q::cluster ? (int)threadIdx.x / G : 0);
 #if GTF_EARLY_STAGE
     // the clustering operands of every slot of a node that may cluster (>= 3 slots), read
     // with the slot fields and parked in the group's LDS stage at the slot lane
@@ -833,7 +833,7 @@ struct Buckets {
 };
 
 template <int G>
-constexpr size_t stage_bytes() { return (size_t)(BLOCK / G) * sizeof(StageT<G>); }
+constexpr size_t stage_bytes() { return (size_t)(NBLOCK / G) * sizeof(StageT<G>); }
 constexpr size_t node_smem_bytes() {
     size_t m = stage_bytes<2>();
     m = stage_bytes<4>() > m ? stage_bytes<4>() : m;
@@ -841,17 +841,17 @@ constexpr size_t node_smem_bytes() {
     m = stage_bytes<16>() > m ? stage_bytes<16>() : m;
     m = stage_bytes<32>() > m ? stage_bytes<32>() : m;
     m = stage_bytes<64>() > m ? stage_bytes<64>() : m;
-    return BLOCK * sizeof(double) + m;
+    return NBLOCK * sizeof(double) + m;
 }
 
 // one launch over every bucket: blocks of the long-running buckets (many slots per node)
 // are dealt first so they overlap the bulk of small nodes instead of trailing it
 template <int... OPS>
-__global__ void __launch_bounds__(BLOCK) k_node_multi(gtf_graph g, gtf_nodes n, gtf_states tse, gtf_states uts,
+__global__ void __launch_bounds__(NBLOCK) k_node_multi(gtf_graph g, gtf_nodes n, gtf_states tse, gtf_states uts,
                                                       gtf_edges e, gtf_params p, Ws w, double chi2_thr,
                                                       double kl_thr, Buckets bk) {
     using Q = OpSeq<OPS...>;
-    __shared__ __attribute__((aligned(16))) char smem[Q::cluster ? node_smem_bytes() : BLOCK * sizeof(double)];
+    __shared__ __attribute__((aligned(16))) char smem[Q::cluster ? node_smem_bytes() : NBLOCK * sizeof(double)];
     // Blocks stay in dispatch order (round-robin over the XCDs): per-node cost varies
     // with the node's state count and clustering work, and an XCD-contiguous remap
     // (gtf::xcd_local) made this kernel 35 % slower on config 4, presumably by putting
@@ -896,14 +896,14 @@ __global__ void __launch_bounds__(BLOCK) k_node_multi(gtf_graph g, gtf_nodes n, 
 // one lane per slot (one for a slot-free node) back to back, so 90+ % of the lanes hold a
 // slot instead of the 59-88 % of power-of-two groups. Same op code as the groups (G = 0).
 template <int... OPS>
-__global__ void __launch_bounds__(BLOCK) k_node_pack(gtf_graph g, gtf_nodes n, gtf_states tse, gtf_states uts,
+__global__ void __launch_bounds__(NBLOCK) k_node_pack(gtf_graph g, gtf_nodes n, gtf_states tse, gtf_states uts,
                                                      gtf_edges e, gtf_params p, Ws w, double chi2_thr, double kl_thr) {
     using Q = OpSeq<OPS...>;
     using Stage = StageT<64>;   // one per wavefront, a group's states at [gbase + i]
-    __shared__ __attribute__((aligned(16))) char smem[BLOCK * sizeof(double) +
-                                                      (Q::cluster ? (BLOCK / 64) * sizeof(Stage) : 0)];
-    __shared__ uint8_t s_start[BLOCK];
-    const int wv = blockIdx.x * (BLOCK / 64) + (int)threadIdx.x / 64;
+    __shared__ __attribute__((aligned(16))) char smem[NBLOCK * sizeof(double) +
+                                                      (Q::cluster ? (NBLOCK / 64) * sizeof(Stage) : 0)];
+    __shared__ uint8_t s_start[NBLOCK];
+    const int wv = blockIdx.x * (NBLOCK / 64) + (int)threadIdx.x / 64;
     if (wv >= g.n_pack_waves) return;  // wavefront-uniform
     const int lane = threadIdx.x & 63;
     const int e0 = g.pack_wave[wv], ne = g.pack_wave[wv + 1] - e0;
@@ -931,7 +931,7 @@ __global__ void __launch_bounds__(BLOCK) k_node_pack(gtf_graph g, gtf_nodes n, g
     if (c.grp.gl >= c.grp.gsize) return;  // past the last segment
     if (!node_fields(c, g, tse, uts, e, Q::need)) return;
     double* sval = (double*)smem + (threadIdx.x & ~63);
-    Stage* stg = (Stage*)(smem + BLOCK * sizeof(double)) + (Q::cluster ? (int)threadIdx.x / 64 : 0);
+    Stage* stg = (Stage*)(smem + NBLOCK * sizeof(double)) + (Q::cluster ? (int)threadIdx.x / 64 : 0);
     const bool has_tse = n.has_tse[c.v];
     const bool has_uts = fresh_has_uts(c, n, Q::fresh);
     (node_op<0, OPS, Stage>(c, g, n, tse, uts, p, w, sval, stg, chi2_thr, kl_thr, has_tse, has_uts), ...);
@@ -940,15 +940,15 @@ __global__ void __launch_bounds__(BLOCK) k_node_pack(gtf_graph g, gtf_nodes n, g
 
 // run-time op sequence (gtf_node_ops): any order of any ops
 template <int G>
-__global__ void __launch_bounds__(BLOCK) k_node_group(gtf_graph g, gtf_nodes n, gtf_states tse, gtf_states uts,
+__global__ void __launch_bounds__(NBLOCK) k_node_group(gtf_graph g, gtf_nodes n, gtf_states tse, gtf_states uts,
                                                       gtf_edges e, gtf_params p, Ws w, NodeOps ops,
                                                       double chi2_thr, double kl_thr, const int32_t* list,
                                                       const int32_t* seg, int count) {
     using Stage = StageT<G>;
-    __shared__ double s_val[BLOCK];
-    __shared__ Stage s_stage[BLOCK / G];
+    __shared__ double s_val[NBLOCK];
+    __shared__ Stage s_stage[NBLOCK / G];
     NodeCtx<G> c;
-    const int gi = (blockIdx.x * BLOCK + (int)threadIdx.x) / G;
+    const int gi = (blockIdx.x * NBLOCK + (int)threadIdx.x) / G;
     const Need nd{(bool)ops.uses_tse, (bool)ops.uses_tse, (bool)ops.uses_uts, (bool)ops.uses_uts,
                   (bool)ops.uses_uts, (bool)ops.uses_uts, (bool)ops.uses_uts, (bool)ops.uses_uts,
                   (bool)ops.uses_uts, true, true, true};

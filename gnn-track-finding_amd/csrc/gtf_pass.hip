@@ -24,7 +24,12 @@ using namespace gtf;
 
 namespace {
 
-constexpr int BLOCK = 256;
+// block sizes (diagnostics knobs): 64- or 128-thread blocks for every pass kernel, or
+// for the node kernels alone, measured within noise of 256 or slower
+#ifndef GTF_PASS_BLOCK
+#define GTF_PASS_BLOCK 256
+#endif
+constexpr int BLOCK = GTF_PASS_BLOCK;
 constexpr int MAX_CLUSTER = 15;  // clustering.py:207 (2 < d < 16)
 
 struct Ws {
@@ -683,6 +688,11 @@ __global__ void __launch_bounds__(BLOCK) k_node(gtf_graph g, gtf_nodes n, gtf_st
     }
 }
 
+// node kernels' block size (k_node_multi / k_node_group / k_node_pack)
+#ifndef GTF_NODE_BLOCK
+#define GTF_NODE_BLOCK 256
+#endif
+constexpr int NBLOCK = GTF_NODE_BLOCK;
 #include "gtf_node_group.h"
 
 thread_local char g_err[512] = "";
@@ -814,27 +824,27 @@ int launch_ops(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* ut
             auto seg = [&](const int32_t* at) { return g->sched_seg ? g->sched_seg + 2 * (at - g->sched) : nullptr; };
             const int n2 = g->n_g2 > 0 && g->n_g2 <= g->n_g4 ? g->n_g2 : 0, n4 = g->n_g4 - n2;
             if (n2 > 0)
-                hipLaunchKernelGGL(k_node_group<2>, dim3((n2 + BLOCK / 2 - 1) / (BLOCK / 2)), dim3(BLOCK), 0, st,
+                hipLaunchKernelGGL(k_node_group<2>, dim3((n2 + NBLOCK / 2 - 1) / (NBLOCK / 2)), dim3(NBLOCK), 0, st,
                                    *g, *n, T, U, *e, *p, w, ops, chi2, kl, l, seg(l), n2);
             l += n2;
             if (n4 > 0)
-                hipLaunchKernelGGL(k_node_group<4>, dim3((n4 + BLOCK / 4 - 1) / (BLOCK / 4)), dim3(BLOCK), 0, st,
+                hipLaunchKernelGGL(k_node_group<4>, dim3((n4 + NBLOCK / 4 - 1) / (NBLOCK / 4)), dim3(NBLOCK), 0, st,
                                    *g, *n, T, U, *e, *p, w, ops, chi2, kl, l, seg(l), n4);
             l += n4;
             if (g->n_g8 > 0)
-                hipLaunchKernelGGL(k_node_group<8>, dim3((g->n_g8 + BLOCK / 8 - 1) / (BLOCK / 8)), dim3(BLOCK), 0, st,
+                hipLaunchKernelGGL(k_node_group<8>, dim3((g->n_g8 + NBLOCK / 8 - 1) / (NBLOCK / 8)), dim3(NBLOCK), 0, st,
                                    *g, *n, T, U, *e, *p, w, ops, chi2, kl, l, seg(l), g->n_g8);
             l += g->n_g8;
             if (g->n_g16 > 0)
-                hipLaunchKernelGGL(k_node_group<16>, dim3((g->n_g16 + BLOCK / 16 - 1) / (BLOCK / 16)), dim3(BLOCK), 0,
+                hipLaunchKernelGGL(k_node_group<16>, dim3((g->n_g16 + NBLOCK / 16 - 1) / (NBLOCK / 16)), dim3(NBLOCK), 0,
                                    st, *g, *n, T, U, *e, *p, w, ops, chi2, kl, l, seg(l), g->n_g16);
             l += g->n_g16;
             if (g->n_g32 > 0)
-                hipLaunchKernelGGL(k_node_group<32>, dim3((g->n_g32 + BLOCK / 32 - 1) / (BLOCK / 32)), dim3(BLOCK), 0,
+                hipLaunchKernelGGL(k_node_group<32>, dim3((g->n_g32 + NBLOCK / 32 - 1) / (NBLOCK / 32)), dim3(NBLOCK), 0,
                                    st, *g, *n, T, U, *e, *p, w, ops, chi2, kl, l, seg(l), g->n_g32);
             l += g->n_g32;
             if (g->n_g64 > 0)
-                hipLaunchKernelGGL(k_node_group<64>, dim3((g->n_g64 + BLOCK / 64 - 1) / (BLOCK / 64)), dim3(BLOCK), 0,
+                hipLaunchKernelGGL(k_node_group<64>, dim3((g->n_g64 + NBLOCK / 64 - 1) / (NBLOCK / 64)), dim3(NBLOCK), 0,
                                    st, *g, *n, T, U, *e, *p, w, ops, chi2, kl, l, seg(l), g->n_g64);
         }
         launch_serial_rest(g, n, T, U, e, p, w, ops, chi2, kl, st);
@@ -882,14 +892,14 @@ int launch_seq(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* ut
                     bk.ar[q] = Arith{g->pad_count[j], noff[j], soff[j], g->pad_tile_nodes, g->pad_tile_slots};
                     bk.count[q] = g->pad_tiles * g->pad_count[j];
                 }
-                bk.blocks[q] = (bk.count[q] + BLOCK / gs[q] - 1) / (BLOCK / gs[q]);
+                bk.blocks[q] = (bk.count[q] + NBLOCK / gs[q] - 1) / (NBLOCK / gs[q]);
                 total += bk.blocks[q];
             }
             if (g->pack_ent && g->pack_wave && g->n_pack_waves > 0)   // every <= 64-slot node, packed
-                hipLaunchKernelGGL((k_node_pack<OPS...>), dim3((g->n_pack_waves + BLOCK / 64 - 1) / (BLOCK / 64)),
-                                   dim3(BLOCK), 0, st, *g, *n, T, U, *e, *p, w, chi2, kl);
+                hipLaunchKernelGGL((k_node_pack<OPS...>), dim3((g->n_pack_waves + NBLOCK / 64 - 1) / (NBLOCK / 64)),
+                                   dim3(NBLOCK), 0, st, *g, *n, T, U, *e, *p, w, chi2, kl);
             else if (total > 0)
-                hipLaunchKernelGGL((k_node_multi<OPS...>), dim3(total), dim3(BLOCK), 0, st, *g, *n, T, U, *e, *p, w,
+                hipLaunchKernelGGL((k_node_multi<OPS...>), dim3(total), dim3(NBLOCK), 0, st, *g, *n, T, U, *e, *p, w,
                                    chi2, kl, bk);
         }
         launch_serial_rest(g, n, T, U, e, p, w, ops, chi2, kl, st);

@@ -447,7 +447,7 @@ def bench_sharded(workload, rank, world, dev, steps, warmup, params, backend="nc
 # the fused node kernel: priors, side norm, reweights, update and KL clustering of every
 # receiver in one launch (gtf_pass.hip run_pass)
 NODE_KERNEL = "k_node_multi<update+cluster> (KL-distance kernel)"
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02_v4", "pmc_c4.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02_v5", "pmc_c4.json")
 
 
 def committed_traffic(workload, kernel, layout, tile, edges, nodes):

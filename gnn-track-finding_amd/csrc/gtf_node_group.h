@@ -324,7 +324,7 @@ __device__ __forceinline__ void g_reweight(NodeCtx<G>& c, double* sval, const do
     const int dr = c.grp.count(first && !left);
     const int nact = c.grp.count(act);
     if (nact > 0) {
-        if (!last_is_edge && c.grp.gl == 0) atomicOr(err, (uint32_t)GTF_ERR_STALE_KEY_NO_EDGE);
+        if (!last_is_edge && c.grp.gl == 0) raise_node(err, c.v, GTF_ERR_STALE_KEY_NO_EDGE);
         if (act) {
             c.side = left ? 0 : 1;
             c.lr = (last_is_edge && last_act == 1) ? (double)(left ? dl : dr) : 1.0;
@@ -353,7 +353,7 @@ __device__ __forceinline__ void g_degree(NodeCtx<G>& c) {
 template <int G>
 __device__ __forceinline__ void g_prune(NodeCtx<G>& c, bool has_tse, bool has_uts, uint32_t* err) {
     if (!has_uts && !has_tse) {
-        if (c.grp.gl == 0) atomicOr(err, (uint32_t)GTF_ERR_NO_STATE_DICT);
+        if (c.grp.gl == 0) raise_node(err, c.v, GTF_ERR_NO_STATE_DICT);
         return;
     }
     LaneDict& st = has_uts ? c.uts : c.tse;
@@ -369,7 +369,7 @@ template <int G>
 __device__ __forceinline__ void g_mixture_weights(NodeCtx<G>& c, LaneDict& st, bool solo, uint32_t* err) {
     const int cnt = c.grp.count(c.valid && st.rank >= 0);
     if (cnt == 0) {
-        if (!solo && c.grp.gl == 0) atomicOr(err, (uint32_t)GTF_ERR_EMPTY_DICT_MW);
+        if (!solo && c.grp.gl == 0) raise_node(err, c.v, GTF_ERR_EMPTY_DICT_MW);
         return;
     }
     if (c.valid && st.rank >= 0) {
@@ -523,7 +523,7 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
         }
     }
     if (!c.grp.any(lnz)) {
-        if (c.grp.gl == 0) atomicOr(err, (uint32_t)GTF_ERR_ALL_ZERO_DIST);
+        if (c.grp.gl == 0) raise_node(err, c.v, GTF_ERR_ALL_ZERO_DIST);
         return;
     }
     if (c.grp.any(lnan)) return;                       // np.min over a NaN -> no merge (:228)
@@ -557,7 +557,7 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
     double mprior = stg->prior[l0] + stg->prior[l1];
     unsigned alive = ((1u << d) - 1u) & ~tiemask;
     if (alive == 0) {
-        if (c.grp.gl == 0) atomicOr(err, (uint32_t)GTF_ERR_TIE_EMPTIED);
+        if (c.grp.gl == 0) raise_node(err, c.v, GTF_ERR_TIE_EMPTIED);
     } else {
         while (GTF_ABLATE != 3) {                                                  // :251-287
             const Cov5 im = inv_cov5(mc);   // the merged state's inverse, shared by KL and the next merge
@@ -570,7 +570,7 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
                 if (D != D) { dn = true; D = INFINITY; }
             }
             if (c.grp.any(dn)) {
-                if (c.grp.gl == 0) atomicOr(err, (uint32_t)GTF_ERR_NAN_KL);
+                if (c.grp.gl == 0) raise_node(err, c.v, GTF_ERR_NAN_KL);
                 break;
             }
             const double mind = c.grp.min_d(D);
@@ -844,51 +844,68 @@ constexpr size_t node_smem_bytes() {
     return NBLOCK * sizeof(double) + m;
 }
 
+// All arguments of k_node_multi in one by-value struct (the kernarg segment).
+struct NodeKArgs {
+    gtf_graph g;
+    gtf_nodes n;
+    gtf_states tse, uts;
+    gtf_edges e;
+    gtf_params p;
+    Ws w;
+    double chi2_thr, kl_thr;
+    Buckets bk;
+};
+typedef const __attribute__((address_space(4))) NodeKArgs* KArgPtr;
+
+// The kernarg segment through an opaque copy of its address: the compiler cannot hoist the
+// argument loads of the six bucket bodies into the kernel's entry (they are speculatable
+// kernarg loads otherwise), where their union -- ~90 SGPRs of pointers live across the
+// whole op sequence -- spilled 64 SGPRs into VGPR lanes on every wave. Each body now loads
+// only its own arguments, where it uses them (scalar loads from the constant segment).
+#ifndef GTF_KARG_LAUNDER
+#define GTF_KARG_LAUNDER 1
+#endif
+__device__ __forceinline__ KArgPtr node_kargs() {
+    uint64_t a = (uint64_t)(uintptr_t)__builtin_amdgcn_kernarg_segment_ptr();
+#if GTF_KARG_LAUNDER
+    asm volatile("" : "+s"(a));
+#endif
+    return (KArgPtr)a;
+}
+
+template <int G, int... OPS>
+__device__ __forceinline__ void node_bucket(int q, int b, char* smem) {
+    const KArgPtr A = node_kargs();
+    node_seq_body<G, OPS...>(*(const gtf_graph*)&A->g, *(gtf_nodes*)&A->n, *(gtf_states*)&A->tse,
+                             *(gtf_states*)&A->uts, *(gtf_edges*)&A->e, *(const gtf_params*)&A->p,
+                             *(const Ws*)&A->w, A->chi2_thr, A->kl_thr, A->bk.list[q], A->bk.seg[q],
+                             A->bk.count[q], b, smem, *(const Arith*)&A->bk.ar[q]);
+}
+
 // one launch over every bucket: blocks of the long-running buckets (many slots per node)
 // are dealt first so they overlap the bulk of small nodes instead of trailing it
 template <int... OPS>
-__global__ void __launch_bounds__(NBLOCK) k_node_multi(gtf_graph g, gtf_nodes n, gtf_states tse, gtf_states uts,
-                                                      gtf_edges e, gtf_params p, Ws w, double chi2_thr,
-                                                      double kl_thr, Buckets bk) {
+__global__ void __launch_bounds__(NBLOCK) k_node_multi(NodeKArgs args) {
+    (void)args;   // read through node_kargs()
     using Q = OpSeq<OPS...>;
     __shared__ __attribute__((aligned(16))) char smem[Q::cluster ? node_smem_bytes() : NBLOCK * sizeof(double)];
     // Blocks stay in dispatch order (round-robin over the XCDs): per-node cost varies
     // with the node's state count and clustering work, and an XCD-contiguous remap
     // (gtf::xcd_local) made this kernel 35 % slower on config 4, presumably by putting
     // the costly nodes of a node range on one XCD.
+    const KArgPtr A = node_kargs();
     int b = blockIdx.x;
-    if (b < bk.blocks[0]) {
-        node_seq_body<64, OPS...>(g, n, tse, uts, e, p, w, chi2_thr, kl_thr, bk.list[0], bk.seg[0], bk.count[0], b,
-                                  smem, bk.ar[0]);
-        return;
-    }
-    b -= bk.blocks[0];
-    if (b < bk.blocks[1]) {
-        node_seq_body<32, OPS...>(g, n, tse, uts, e, p, w, chi2_thr, kl_thr, bk.list[1], bk.seg[1], bk.count[1], b,
-                                  smem, bk.ar[1]);
-        return;
-    }
-    b -= bk.blocks[1];
-    if (b < bk.blocks[2]) {
-        node_seq_body<16, OPS...>(g, n, tse, uts, e, p, w, chi2_thr, kl_thr, bk.list[2], bk.seg[2], bk.count[2], b,
-                                  smem, bk.ar[2]);
-        return;
-    }
-    b -= bk.blocks[2];
-    if (b < bk.blocks[3]) {
-        node_seq_body<8, OPS...>(g, n, tse, uts, e, p, w, chi2_thr, kl_thr, bk.list[3], bk.seg[3], bk.count[3], b, smem,
-                                 bk.ar[3]);
-        return;
-    }
-    b -= bk.blocks[3];
-    if (b < bk.blocks[4]) {
-        node_seq_body<4, OPS...>(g, n, tse, uts, e, p, w, chi2_thr, kl_thr, bk.list[4], bk.seg[4], bk.count[4], b,
-                                 smem, bk.ar[4]);
-        return;
-    }
-    b -= bk.blocks[4];
-    node_seq_body<2, OPS...>(g, n, tse, uts, e, p, w, chi2_thr, kl_thr, bk.list[5], bk.seg[5], bk.count[5], b, smem,
-                                 bk.ar[5]);
+    if (b < A->bk.blocks[0]) { node_bucket<64, OPS...>(0, b, smem); return; }
+    b -= A->bk.blocks[0];
+    if (b < A->bk.blocks[1]) { node_bucket<32, OPS...>(1, b, smem); return; }
+    b -= A->bk.blocks[1];
+    if (b < A->bk.blocks[2]) { node_bucket<16, OPS...>(2, b, smem); return; }
+    b -= A->bk.blocks[2];
+    if (b < A->bk.blocks[3]) { node_bucket<8, OPS...>(3, b, smem); return; }
+    b -= A->bk.blocks[3];
+    if (b < A->bk.blocks[4]) { node_bucket<4, OPS...>(4, b, smem); return; }
+    b -= A->bk.blocks[4];
+    node_bucket<2, OPS...>(5, b, smem);
 }
 
 // Packed lane segments (gtf_graph.pack_ent / pack_wave): wavefront wv takes the entries

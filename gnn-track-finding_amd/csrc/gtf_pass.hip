@@ -33,8 +33,9 @@ constexpr int BLOCK = GTF_PASS_BLOCK;
 constexpr int MAX_CLUSTER = 15;  // clustering.py:207 (2 < d < 16)
 
 struct Ws {
-    uint32_t* err;    // error word
+    uint32_t* err;    // error word (the workspace's first bytes; gtf_diag at GTF_DIAG_OFFSET)
     double* vc;       // [S] per active edge, by SLOT: the merged_cov[1,1] its extrapolation sees
+    const gtf_diag* diag;   // optional diagnostics outputs (gtf_set_diagnostics), in the workspace
 };
 
 __host__ inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
@@ -44,12 +45,19 @@ __host__ inline Ws carve(void* base, int32_t n_nodes, int32_t n_slots) {
     char* p = (char*)base;
     Ws w;
     w.err = (uint32_t*)p;
+    w.diag = (const gtf_diag*)(p + GTF_DIAG_OFFSET);
     p += 256;
     w.vc = (double*)p;
     return w;
 }
 
-__device__ __forceinline__ void raise_flag(uint32_t* err, uint32_t f) { atomicOr(err, f); }
+// a reference exception at node v: the workspace error word, and v's entry of the optional
+// per-node diagnostics array (gtf_diag.node_err, read from the workspace only on this path)
+__device__ __forceinline__ void raise_node(uint32_t* err, int v, uint32_t f) {
+    atomicOr(err, f);
+    uint32_t* ne = reinterpret_cast<const gtf_diag*>(reinterpret_cast<const char*>(err) + GTF_DIAG_OFFSET)->node_err;
+    if (ne) atomicOr(ne + v, f);
+}
 
 __device__ __forceinline__ Cov5 load_cov5(const double* c, int64_t i) {
     const double* p = c + 5 * i;
@@ -304,6 +312,7 @@ __global__ void __launch_bounds__(BLOCK) k_extrapolate(gtf_graph g, gtf_nodes n,
     const double invS = 1.0 / S;
     const double resid = 0.0 - xe[2];
     const double chi2 = (resid * invS) * resid;                                    // :140
+    if (w.diag->edge_chi2) w.diag->edge_chi2[k] = chi2;   // diagnostics (gtf_set_diagnostics), off by default
     if (!(chi2 <= p.chi2_cut)) {                                                   // :298
         e.act[k] = 0;                                                              // :393
         uts.fresh[k] = 0;
@@ -357,7 +366,7 @@ __global__ void __launch_bounds__(BLOCK) k_extrapolate(gtf_graph g, gtf_nodes n,
     vt = fma(J2 * (sigma_r * sigma_r), J2, vt);
     vt = fma(J3 * (sigma_rn * sigma_rn), J3, vt);
 
-    if (isnan(smw)) raise_flag(w.err, GTF_ERR_SEND_MW_MISSING);
+    if (isnan(smw)) raise_node(w.err, v, GTF_ERR_SEND_MW_MISSING);
     uts.sv[3 * (int64_t)k + 0] = xu0;
     uts.sv[3 * (int64_t)k + 1] = xu1;
     uts.sv[3 * (int64_t)k + 2] = xu2;
@@ -458,7 +467,7 @@ __device__ void node_reweight(const gtf_graph& g, gtf_edges& e, gtf_states& st, 
         if (left) { nl++; if (!dup) dl++; } else { nr++; if (!dup) dr++; }
     }
     if (nl + nr > 0) {
-        if (!g.is_edge[last]) raise_flag(err, GTF_ERR_STALE_KEY_NO_EDGE);
+        if (!g.is_edge[last]) raise_node(err, v, GTF_ERR_STALE_KEY_NO_EDGE);
         const bool last_act = g.is_edge[last] && e.act[last] == 1;
         for (int k = s.lo; k < s.hi; k++) {
             if (st.rank[k] < 0 || !edge_active(g, e, k)) continue;
@@ -492,7 +501,7 @@ __device__ void node_mixture_weights(const gtf_graph& g, gtf_states& st, Seg s, 
     int cnt = 0;
     for (int k = s.lo; k < s.hi; k++) cnt += st.rank[k] >= 0 ? 1 : 0;
     if (cnt == 0) {
-        if (!g.solo[v]) raise_flag(err, GTF_ERR_EMPTY_DICT_MW);
+        if (!g.solo[v]) raise_node(err, v, GTF_ERR_EMPTY_DICT_MW);
         return;
     }
     const double mw = 1.0 / (double)cnt;
@@ -527,7 +536,7 @@ __device__ void node_prune(const gtf_graph& g, const gtf_nodes& n, gtf_states& t
                            uint32_t* err) {
     gtf_states& st = n.has_uts[v] ? uts : tse;
     if (!n.has_uts[v] && !n.has_tse[v]) {
-        raise_flag(err, GTF_ERR_NO_STATE_DICT);
+        raise_node(err, v, GTF_ERR_NO_STATE_DICT);
         return;
     }
     for (int k = s.lo; k < s.hi; k++)
@@ -573,7 +582,7 @@ __device__ void node_cluster(const gtf_graph& g, gtf_nodes& n, const gtf_states&
             }
         }
     }
-    if (!any_nonzero) { raise_flag(err, GTF_ERR_ALL_ZERO_DIST); return; }
+    if (!any_nonzero) { raise_node(err, v, GTF_ERR_ALL_ZERO_DIST); return; }
     if (has_nan || !(best < chi2_thr)) return;                                     // :228
     // merge pair = (idx[0], idx[1]) of concatenate((rows, cols))
     const int p0 = ti0, p1 = (ti1 >= 0) ? ti1 : tj0;
@@ -592,7 +601,7 @@ __device__ void node_cluster(const gtf_graph& g, gtf_nodes& n, const gtf_states&
     double mprior = st.prior[ord[p0]] + st.prior[ord[p1]];
     uint32_t alive = ((1u << d) - 1u) & ~tiemask;
     if (alive == 0) {
-        raise_flag(err, GTF_ERR_TIE_EMPTIED);
+        raise_node(err, v, GTF_ERR_TIE_EMPTIED);
     } else {
         while (true) {                                                             // :251-287
             double mind = 0.0;
@@ -606,7 +615,7 @@ __device__ void node_cluster(const gtf_graph& g, gtf_nodes& n, const gtf_states&
                 if (isnan(D)) nan_seen = true;
                 if (mi < 0 || D < mind) { mind = D; mi = i; }  // first minimum (list.index)
             }
-            if (nan_seen) { raise_flag(err, GTF_ERR_NAN_KL); break; }
+            if (nan_seen) { raise_node(err, v, GTF_ERR_NAN_KL); break; }
             if (!(mind < kl_thr)) break;
             const int ki = ord[mi];
             const double ps[3] = {st.sv[3 * (int64_t)ki], st.sv[3 * (int64_t)ki + 1], st.sv[3 * (int64_t)ki + 2]};
@@ -899,8 +908,8 @@ int launch_seq(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* ut
                 hipLaunchKernelGGL((k_node_pack<OPS...>), dim3((g->n_pack_waves + NBLOCK / 64 - 1) / (NBLOCK / 64)),
                                    dim3(NBLOCK), 0, st, *g, *n, T, U, *e, *p, w, chi2, kl);
             else if (total > 0)
-                hipLaunchKernelGGL((k_node_multi<OPS...>), dim3(total), dim3(NBLOCK), 0, st, *g, *n, T, U, *e, *p, w,
-                                   chi2, kl, bk);
+                hipLaunchKernelGGL((k_node_multi<OPS...>), dim3(total), dim3(NBLOCK), 0, st,
+                                   NodeKArgs{*g, *n, T, U, *e, *p, w, chi2, kl, bk});
         }
         launch_serial_rest(g, n, T, U, e, p, w, ops, chi2, kl, st);
     }
@@ -963,8 +972,17 @@ size_t gtf_workspace_bytes(int32_t n_nodes, int32_t n_slots) {
 }
 
 int gtf_clear_errors(void* ws, gtf_stream_t stream) {
-    hipError_t e = hipMemsetAsync(ws, 0, 256, (hipStream_t)stream);
+    hipError_t e = hipMemsetAsync(ws, 0, GTF_DIAG_OFFSET, (hipStream_t)stream);   // (keeps gtf_diag)
     return e == hipSuccess ? 0 : fail("clear errors", e);
+}
+
+int gtf_set_diagnostics(void* ws, const gtf_diag* d, gtf_stream_t stream) {
+    gtf_diag z;
+    memset(&z, 0, sizeof(z));
+    hipError_t e = hipMemcpyAsync((char*)ws + GTF_DIAG_OFFSET, d ? d : &z, sizeof(gtf_diag), hipMemcpyHostToDevice,
+                                  (hipStream_t)stream);
+    if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)stream);   // (d / z are host stack memory)
+    return e == hipSuccess ? 0 : fail("set diagnostics", e);
 }
 
 int gtf_read_errors(void* ws, uint32_t* flags, gtf_stream_t stream) {

@@ -105,6 +105,13 @@ class GtfKlGraph(ctypes.Structure):
                 ("gnn_stride", I32), ("slot0", ctypes.c_int64), ("pair0", ctypes.c_int64)]
 
 
+class GtfDiag(ctypes.Structure):
+    _fields_ = [("node_err", P), ("edge_chi2", P), ("reserved_", P * 6)]
+
+
+DIAG_OFFSET = 64
+
+
 class GtfPairOut(ctypes.Structure):
     _fields_ = [("chi2", P), ("avg_tau", P), ("avg_theta", P), ("delta_theta", P), ("truth", P), ("err", P)]
 
@@ -136,7 +143,7 @@ SYMBOLS = ["gtf_workspace_bytes", "gtf_clear_errors", "gtf_read_errors", "gtf_ex
            "gtf_shard_chunk_bytes", "gtf_shard_pack", "gtf_shard_unpack", "gtf_halo_pack", "gtf_halo_unpack",
            "gtf_extract_workspace_bytes",
            "gtf_extract_candidates", "gtf_build_event_csr", "gtf_candidate_order",
-           "gtf_updated_state_pair_counts", "gtf_updated_state_distances",
+           "gtf_updated_state_pair_counts", "gtf_updated_state_distances", "gtf_set_diagnostics",
            "gtf_last_error",
            "gtf_version"]
 
@@ -163,6 +170,7 @@ def lib():
     L.gtf_workspace_bytes.argtypes = [I32, I32]
     L.gtf_clear_errors.argtypes = [P, P]
     L.gtf_read_errors.argtypes = [P, ctypes.POINTER(ctypes.c_uint32), P]
+    L.gtf_set_diagnostics.argtypes = [P, ctypes.POINTER(GtfDiag), P]
     G, N, S, E, PR = (ctypes.POINTER(GtfGraph), ctypes.POINTER(GtfNodes), ctypes.POINTER(GtfStates),
                       ctypes.POINTER(GtfEdges), ctypes.POINTER(GtfParams))
     L.gtf_extrapolate.argtypes = [G, N, S, E, PR, P, P]
@@ -198,7 +206,8 @@ def lib():
                "gtf_pass_ev", "gtf_message_passing", "gtf_node_ops",
                "gtf_tag_prepare", "gtf_tag_sweep", "gtf_parabolic_kl", "gtf_track_state_estimates", "gtf_pass_shard", "gtf_shard_pack",
                "gtf_shard_unpack", "gtf_halo_pack", "gtf_halo_unpack", "gtf_extract_candidates", "gtf_build_event_csr",
-               "gtf_candidate_order", "gtf_updated_state_pair_counts", "gtf_updated_state_distances"):
+               "gtf_candidate_order", "gtf_updated_state_pair_counts", "gtf_updated_state_distances",
+               "gtf_set_diagnostics"):
         getattr(L, fn).restype = ctypes.c_int
     _lib = L
     return L

@@ -424,6 +424,50 @@ class DeviceGraph:
             ta, tb = tb, ta
         return ta.cpu().numpy(), flips_hist
 
+    # ------------------------------------------------------------ diagnostics
+    def set_diagnostics(self, node_err: bool = True, edge_chi2: bool = True):
+        """SURVEY §5's optional diagnostic outputs (gtf_set_diagnostics), written by the stage
+        kernels from now on: the GTF_ERR_* bits of every reference exception per node (which
+        node, so which subgraph, would make the reference raise) and the chi2 of every
+        extrapolated edge (the values extrapolate_merged_states.py:134-172 prints to CSV).
+        Off by default and never on the benchmark's path; set_diagnostics(False, False)
+        unregisters them."""
+        torch = self.torch
+        self.diag_t = {}
+        if node_err:
+            self.diag_t["node_err"] = torch.zeros(max(self.n_nodes, 1), dtype=torch.int32, device=self.device)
+        if edge_chi2:
+            self.diag_t["edge_chi2"] = torch.full((max(self.n_slots, 1),), float("nan"), dtype=torch.float64,
+                                                  device=self.device)
+        vp = lambda k: ctypes.c_void_p(self.diag_t[k].data_ptr()) if k in self.diag_t else ctypes.c_void_p(0)  # noqa: E731
+        d = nat.GtfDiag(vp("node_err"), vp("edge_chi2"))
+        nat.check(self.lib.gtf_set_diagnostics(self.ptr("ws"), ctypes.byref(d), self.stream))
+
+    def diagnostics(self) -> dict:
+        """the registered diagnostics in host order: node_err [N] uint32, edge_chi2 [S]
+        (NaN where no extrapolation ran)"""
+        out = {}
+        for k, v in getattr(self, "diag_t", {}).items():
+            if k == "node_err":
+                a = v.cpu().numpy()[:self.n_nodes].astype(np.uint32)
+                out[k] = a if self.order is None else self._host_nodes(a)
+            else:
+                a = v.cpu().numpy()[:self.n_slots]
+                out[k] = a if self.slot_perm is None else self._host_slots(a, np.nan)
+        return out
+
+    def _host_nodes(self, a, fill=0):
+        nm = self.order >= 0
+        h = np.full(int(nm.sum()), fill, a.dtype)
+        h[self.order[nm]] = a[nm]
+        return h
+
+    def _host_slots(self, a, fill=0):
+        sm = self.slot_perm >= 0
+        h = np.full(int(sm.sum()), fill, a.dtype)
+        h[self.slot_perm[sm]] = a[sm]
+        return h
+
     # ---------------------------------------------------------------- results
     def download(self, g: TrackGraph) -> TrackGraph:
         """copy the mutable arrays back into the host TrackGraph (in place, host order)"""

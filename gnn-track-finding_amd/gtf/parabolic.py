@@ -119,6 +119,46 @@ class ParabolicKL:
                                      (ctypes.c_void_p * 4)(*[x.data_ptr() if x.numel() else None for x in self.lists]),
                                      (ctypes.c_int32 * 4)(*[x.numel() for x in self.lists]), gnn_stride=2)
 
+    def replica(self, gnn=None):
+        """An independent copy of this batch in its own device buffers (same structure):
+        ``gnn`` (caller's node order, [N, 4] or [N, 2]) replaces the coordinates, e.g. a
+        batch jittered with another seed. Used to rotate launches over several resident
+        batches so that no launch finds its inputs in the caches (bench.py, config 5)."""
+        import copy
+        r = copy.copy(self)
+        cl = lambda t: t.clone() if t is not None else None  # noqa: E731
+        r.slot_ptr, r.slot_src, r.pair_ptr = cl(self.slot_ptr), cl(self.slot_src), cl(self.pair_ptr)
+        r.truth = cl(self.truth)
+        r.lists = [cl(x) for x in self.lists]
+        r.err = torch.zeros(1, dtype=torch.int32, device=self.device)
+        if gnn is None:
+            r.gnn = cl(self.gnn)
+        else:
+            gh = np.asarray(gnn, np.float64)[:, :2]
+            if self.node_of is not None:
+                gh = gh[self.node_of]
+            r.gnn = torch.from_numpy(np.ascontiguousarray(gh)).to(self.device)
+        g = nat.GtfKlGraph.from_buffer_copy(self._g)
+        g.slot_ptr, g.slot_src, g.gnn = _ptr(r.slot_ptr), _ptr(r.slot_src), _ptr(r.gnn)
+        g.truth, g.pair_ptr = _ptr(r.truth), _ptr(r.pair_ptr)
+        for q in range(4):
+            if g.list[q]:
+                g.list[q] = r.lists[q].data_ptr() if r.lists[q].numel() else None
+        r._g = g
+        return r
+
+    def footprint_bytes(self, out) -> int:
+        """device bytes of this batch's inputs and the outputs in ``out``"""
+        ts = [self.slot_ptr, self.slot_src, self.gnn, self.truth, self.pair_ptr] + list(self.lists)
+        ts += [v for k, v in out.items() if k not in ("kl", "truth")]   # (views of _kl / _truth)
+        seen, tot = set(), 0
+        for t in ts:
+            if t is None or t.data_ptr() in seen:
+                continue
+            seen.add(t.data_ptr())
+            tot += t.numel() * t.element_size()
+        return tot
+
     @classmethod
     def from_graph(cls, g: TrackGraph, truth=None, device="cuda", with_single=False):
         ptr, src = in_edge_csr(g)

@@ -180,11 +180,35 @@ enum {
     GTF_ERR_TOO_MANY_STATES = 1024 /* a15: a node with more than 2048 updated states (not processed) */
 };
 
-/* Workspace: caller allocates gtf_workspace_bytes() bytes of device memory. */
+/* Workspace: caller allocates gtf_workspace_bytes() bytes of device memory, zeroed once
+ * (its first 256 bytes are a header: the error word at offset 0, gtf_diag at
+ * GTF_DIAG_OFFSET). */
 size_t gtf_workspace_bytes(int32_t n_nodes, int32_t n_slots);
 
-/* Zero the error word (stream-ordered). */
+/* Zero the error word (stream-ordered; the registered diagnostics stay). */
 int gtf_clear_errors(void* workspace, gtf_stream_t stream);
+
+/* ---- Optional diagnostics outputs (SURVEY §5 "Metrics / logging"), off by default ----
+ * The reference prints per-edge chi2 values to CSV files (extrapolate_merged_states.py
+ * :143-172, the xy-plane chi2 of :134-140 is the one its gate uses) and raises exceptions
+ * that abort a whole stage (the GTF_ERR_* places). Registered in the workspace by
+ * gtf_set_diagnostics (NULL = all off), the pass kernels of that workspace then write:
+ *   node_err[v]  |= the GTF_ERR_* bits of every reference exception node v raised
+ *                  (gtf_pass / gtf_extrapolate / gtf_update / gtf_cluster / gtf_node_ops);
+ *                  caller-zeroed uint32 [N]: which node (so which subgraph) would raise;
+ *   edge_chi2[k]  = chi2 of the extrapolation of slot k's edge (every active out-edge of a
+ *                  merged sender, accepted or not; untouched elsewhere), double [S].
+ * The truth-based confusion counts of the reference's printouts (helper.py:186-225,
+ * extrapolate_merged_states.py:496-518, clustering.py:342-369) follow on the host from
+ * the masks (gtf/diagnostics.py). Nothing here is on the timed path: with no diagnostics
+ * registered a kernel reads one uniform pointer. */
+#define GTF_DIAG_OFFSET 64
+typedef struct gtf_diag {
+    uint32_t* node_err;       /* [N] device, or NULL */
+    double*   edge_chi2;      /* [S] device, or NULL */
+    void*     reserved_[6];   /* zero */
+} gtf_diag;
+int gtf_set_diagnostics(void* workspace, const gtf_diag* d, gtf_stream_t stream);
 /* Copy the error word to the host (synchronises the stream). */
 int gtf_read_errors(void* workspace, uint32_t* flags, gtf_stream_t stream);
 

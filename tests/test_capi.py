@@ -45,7 +45,8 @@ def test_struct_layout_matches_header():
           "gtf_edges": nat.GtfEdges, "gtf_params": nat.GtfParams, "gtf_kl_graph": nat.GtfKlGraph, "gtf_tse_extra": nat.GtfTseExtra, "gtf_shard": nat.GtfShard, "gtf_halo": nat.GtfHalo,
           "gtf_extract_params": nat.GtfExtractParams, "gtf_extract_io": nat.GtfExtractIO,
           "gtf_kl_out": nat.GtfKlOut, "gtf_event_csr": nat.GtfEventCsr,
-          "gtf_candidate_graph": nat.GtfCandidateGraph, "gtf_pair_out": nat.GtfPairOut}
+          "gtf_candidate_graph": nat.GtfCandidateGraph, "gtf_pair_out": nat.GtfPairOut,
+          "gtf_diag": nat.GtfDiag}
     lines = []
     for t, cls in py.items():
         lines += ['  printf("%s.%s %%zu\\n", offsetof(%s, %s));' % (t, f, t, f) for f, _ in cls._fields_]

@@ -24,7 +24,7 @@ pinned.
   updated_track_states (-c 1000 -k 100, run_gnn_trackml_mod.sh:112).
 
 Stored in the packed node / slot order of gtf.graph.pack (= gtf_build_event_csr's order;
-a structure digest pins it): masks and flags exactly, merged states of merged nodes, the
+a structure digest pins it): masks and flags exactly, merged states of merged nodes (every 2nd one on the full load), the
 updated states' dict order, and the updated-state floats of every 4th present slot
 (fixture size). raised[sub] = 1 where the reference raised in that subgraph (its outputs
 are then not pinned), tie_nodes = the receivers whose get_smallest_dist_idx returned a
@@ -160,9 +160,13 @@ def save(name, g_in, g_out, raised, ties, uts):
         "act_bits": np.packbits(g_out.slot["act"].astype(np.uint8)),
         "has_merged_bits": np.packbits(mm.astype(np.uint8)),
         "degree": g_out.node["degree"].astype(np.int16),
-        "merged_state": g_out.node["merged_state"][mm], "merged_cov": g_out.node["merged_cov"][mm],
-        "merged_prior": g_out.node["merged_prior"][mm],
     }
+    # merged floats of every merged node, or of every 2nd one when all of them are (the full
+    # load: every node starts with a merged state; fixture size)
+    sn = np.nonzero(mm)[0]
+    sn = sn[::2] if sn.size > 10000 else sn
+    arrs.update({"sample_node": sn.astype(np.int32), "merged_state": g_out.node["merged_state"][sn],
+                 "merged_cov": g_out.node["merged_cov"][sn], "merged_prior": g_out.node["merged_prior"][sn]})
     if uts:
         from compare import dense_ranks
         arrs["has_uts_bits"] = np.packbits(g_out.node["has_uts"].astype(np.uint8))

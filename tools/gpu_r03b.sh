@@ -1,0 +1,20 @@
+#!/bin/bash
+# round 3: GPU suite (incl. the 800' real-data parity and the sharded C4 test), then the
+# rocprofv3 kernel trace of the default bench, PMC passes of the C4 pass and of the cold
+# config-5 rotation, one bench line, and (if the profiler offers it) PC sampling of the
+# C4 pass loop. Stops at the first failing GPU step.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=gpurun_out/r03b
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+tail -3 $O/pytest.log
+bash tools/gpu_profile.sh $O/c4 --steps 20 --warmup 3 --no-c5 --no-dropin || exit 1
+python tools/pmc_summary.py $O/c4 profiles/r01_pmc/calib $O/c4/pmc_c4.json c4 > /dev/null || exit 1
+bash tools/gpu_profile_py.sh $O/c5 tools/pkl_time.py 48 || exit 1
+timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || exit 1
+echo r03b-bench-done
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 60 rocprofv3 -L > $R/$O/rocprof_list.txt 2>&1
+timeout -k 10 120 rocprofv3 --pc-sampling-beta-enabled --pc-sampling-method stochastic --pc-sampling-unit cycles --pc-sampling-interval 65536 -d $R/$O/pcs -o run --output-format csv -- python3 $R/tools/pass_loop.py 200 > $R/$O/pcs.log 2>&1
+echo pcs rc $?

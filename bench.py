@@ -137,12 +137,15 @@ def dropin_input_vol7(params):
 def dropin_stage_wall(params, reps=3):
     """the drop-in stage wall time, gpickle in -> gpickle out, of the
     extrapolation stage (extrapolate_merged_states.py:521-572's main body through the
-    drop-in module: read every subgraph, message passing + priors / reweight x2 + degree
-    on the GPU, write every subgraph), in process (interpreter start excluded), on the
-    full-load volume-7 134 network (14,766 directed edges); median of reps. BASELINE.md
-    times the reference's own stage on this input at 788 edges/s as is (18.7 s) and
-    5,367 edges/s with its prints stubbed."""
+    drop-in runner gtf.dropin.run_dir: the per-file pickle reading / packing and unpacking /
+    writing on worker processes, message passing + priors / reweight x2 + degree in one
+    device call), on the full-load volume-7 134 network (14,766 directed edges), median of
+    reps. Timed in a fresh child process (python -m gtf.dropin), whose workers fork before
+    it touches the GPU; interpreter start and imports excluded, worker start-up included.
+    BASELINE.md times the reference's own stage on this input at 788 edges/s as is
+    (18.7 s) and 5,367 edges/s with its prints stubbed."""
     import shutil
+    import subprocess
     import tempfile
     from gtf import stages as st
     graphs = dropin_input_vol7(params)
@@ -153,22 +156,19 @@ def dropin_stage_wall(params, reps=3):
         os.makedirs(outd)
         for i, s in enumerate(graphs):
             st.save_network(ind, i, s)
-        ts, tk = [], []
-        for _ in range(reps + 1):
-            t0 = time.perf_counter()
-            subs = st.read_subgraphs(ind)
-            t1 = time.perf_counter()
-            st.extrapolate_stage(subs, params)
-            t2 = time.perf_counter()
-            for i, s in enumerate(subs):
-                st.save_network(outd, i, s)
-            ts.append(time.perf_counter() - t0)
-            tk.append(t2 - t1)
         edges = sum(s.number_of_edges() for s in graphs)
-        dt = float(np.median(ts[1:]))
-        return {"stage": "extrapolate (drop-in main body, in process)", "input": "vol-7 134 full load",
-                "subgraphs": len(graphs), "edges": edges, "wall_s": dt, "edges_per_s": edges / dt,
-                "stage_call_s": float(np.median(tk[1:])),
+        env = dict(os.environ, PYTHONPATH=os.path.join(ROOT, "gnn-track-finding_amd"))
+        r = subprocess.run([sys.executable, "-m", "gtf.dropin", ind, outd, str(reps)], env=env, cwd=ROOT,
+                           capture_output=True, text=True, timeout=600)
+        if r.returncode != 0:
+            return {"error": r.stderr[-400:]}
+        runs = json.loads(r.stdout)["runs"]
+        med = sorted(runs, key=lambda x: x["wall_s"])[len(runs) // 2]
+        return {"stage": "extrapolate (drop-in runner gtf.dropin.run_dir, child process)",
+                "input": "vol-7 134 full load", "subgraphs": len(graphs), "edges": edges,
+                "wall_s": med["wall_s"], "edges_per_s": edges / med["wall_s"], "workers": med["workers"],
+                "read_pack_s": med["read_pack_s"], "device_s": med["device_s"],
+                "unpack_write_s": med["unpack_write_s"],
                 "reference_as_is_edges_per_s": 788, "reference_prints_stubbed_edges_per_s": 5367}
     finally:
         shutil.rmtree(tmp, ignore_errors=True)

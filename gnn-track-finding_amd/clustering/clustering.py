@@ -16,19 +16,19 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from gtf import stages as _st  # noqa: E402
+from gtf.dropin import run_dir  # noqa: E402
 from gtf.params import Params  # noqa: E402
 
 
 def cluster(inputDir, outputDir, track_state_key, chi2_threshold, KL_threshold, KL_lut, iteration_num, reactivate,
             sigma0rz, sigma0rz2, endcap_boundary):
-    subGraphs = _st.read_subgraphs(inputDir)
     if reactivate:
         raise TypeError("compute_track_state_estimates() missing 4 required positional arguments "
                         "(reference clustering.py:141)")
     p = Params(sigma0rz=sigma0rz, sigma0rz2=sigma0rz2, endcap_boundary=endcap_boundary)
-    _st.cluster_graphs(subGraphs, track_state_key, chi2_threshold, KL_threshold, p)
-    for i, sub in enumerate(subGraphs):
-        _st.save_network(outputDir, i, sub)
+    k = _st._key(track_state_key)
+    # read -> one device call -> save, the pickle work on worker processes (gtf.dropin)
+    run_dir(inputDir, outputDir, lambda d: d.cluster(k, chi2_threshold, KL_threshold, p))
 
 
 def main():

@@ -130,9 +130,9 @@ __device__ __forceinline__ void sender_scan(const gtf_graph& g, gtf_nodes& n, co
             const double vmm = __shfl(vm, m, SG);
             if (m <= gl && vmm != -1.0) c = c + vmm;
         }
-        // the running value of each active edge, stored at its slot: the extrapolation
-        // thread of that slot reads it coalesced
-        if (vm != -1.0) w.vc[k] = c;
+        // the running value of each active edge, stored in out-edge order (contiguous per
+        // sender: coalesced stores) when the graph has slot_outidx, else at its slot
+        if (vm != -1.0) w.vc[g.slot_outidx ? i : k] = c;
         carry = __shfl(c, SG - 1, SG);  // lanes past the end carry the full sum
     }
     if (gl == 0) n.merged_cov[5 * (int64_t)u + 3] = carry;
@@ -143,7 +143,8 @@ __device__ __forceinline__ void sender_scan(const gtf_graph& g, gtf_nodes& n, co
 // is issued in one round, beside the sender's own fields
 template <int G>
 __device__ __forceinline__ void sender_scan_lane(const gtf_graph& g, gtf_nodes& n, const gtf_edges& e,
-                                                 const gtf_params& p, const Ws& w, int u, int k, int v, int gl) {
+                                                 const gtf_params& p, const Ws& w, int u, int ob, int k, int v,
+                                                 int gl) {
     const uint8_t hm = n.has_merged[u];
     const double a = n.merged_state[3 * (int64_t)u + 0];
     const double b = n.merged_state[3 * (int64_t)u + 1];
@@ -162,7 +163,7 @@ __device__ __forceinline__ void sender_scan_lane(const gtf_graph& g, gtf_nodes& 
         const double vmm = __shfl(vm, m, G);
         if (m <= gl && vmm != -1.0) c = c + vmm;
     }
-    if (vm != -1.0) w.vc[k] = c;
+    if (vm != -1.0) w.vc[g.slot_outidx ? ob + gl : k] = c;
     const double fin = __shfl(c, G - 1, G);   // the last lane has every active edge's term
     if (gl == 0) n.merged_cov[5 * (int64_t)u + 3] = fin;
 }
@@ -205,9 +206,9 @@ __device__ __forceinline__ void sender_bucket_lanes(const gtf_graph& g, gtf_node
     const int t = xcd_local(b, nb) * BLOCK + (int)threadIdx.x;
     const int gi = t / G;
     if (gi >= count) return;  // group-uniform
-    const int u = list[gi].x;
+    const int4 en = list[gi];
     const int2 kv = lanes[t];  // lane t of the bucket = lane (t % G) of entry gi
-    sender_scan_lane<G>(g, n, e, p, w, u, kv.x, kv.y, t & (G - 1));
+    sender_scan_lane<G>(g, n, e, p, w, en.x, en.y, kv.x, kv.y, t & (G - 1));
 }
 
 __global__ void __launch_bounds__(BLOCK) k_sender_sched(gtf_graph g, gtf_nodes n, gtf_edges e, gtf_params p, Ws w,
@@ -240,7 +241,10 @@ __global__ void __launch_bounds__(BLOCK) k_extrapolate(gtf_graph g, gtf_nodes n,
     // exits would otherwise serialise each load behind the previous one's branch).
     const uint8_t is_edge = g.is_edge[k], act = e.act[k];
     const int src = g.slot_src[k], v = g.slot_dst[k];
-    const double vc = w.vc[k];         // written by k_sender for active edges of merged senders
+    // written by k_sender for active edges of merged senders: in out-edge order through
+    // slot_outidx (one gather beside the sender's), or by slot
+    const int oi = g.slot_outidx ? g.slot_outidx[k] : k;
+    const double vc = w.vc[oi >= 0 ? oi : 0];
     const double smw = e.send_mw[k];
     const int u = src >= 0 ? src : 0;   // orphan keys have no sender
     const double* ng = g.gnn + 4 * (int64_t)u;  // sender ("node" in the reference)

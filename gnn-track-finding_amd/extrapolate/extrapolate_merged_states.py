@@ -5,7 +5,8 @@
 main() reads every ``*_subgraph.gpickle`` of the input directory (glob order,
 :544-548), runs message passing + priors/reweight x2 + node degree as one fused
 HIP call (gtf_extrapolate, :552-566) and saves the graphs renumbered in the
-same order (:570-571). The per-edge diagnostic CSVs and prints of the reference
+same order (:570-571); the pickle reading / writing runs on worker processes
+(gtf.dropin.run_dir). The per-edge diagnostic CSVs and prints of the reference
 (:143-295, :496-518) have no effect on outputs and are not produced.
 """
 import argparse
@@ -15,6 +16,7 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from gtf import stages as _st  # noqa: E402
+from gtf.dropin import run_dir  # noqa: E402
 from gtf.params import Params  # noqa: E402
 
 
@@ -35,10 +37,9 @@ def main():
     args = parser.parse_args()
     p = Params(sigma0xy=float(args.sigma0xy), sigma0rz=float(args.sigma0rz), sigma0rz2=float(args.sigma0rz2),
                endcap_boundary=float(args.endcapboundary), chi2_cut=float(args.chi2CutFactor))
-    subGraphs = _st.read_subgraphs(args.inputDir)
-    _st.extrapolate_stage(subGraphs, p)
-    for i, sub in enumerate(subGraphs):
-        _st.save_network(args.outputDir, i, sub)
+    # read -> one fused device call -> save, the per-file pickle work on worker processes
+    # (gtf.dropin: same outputs and file numbering as the loop over read_subgraphs)
+    run_dir(args.inputDir, args.outputDir, lambda d: d.extrapolate(p))
 
 
 if __name__ == "__main__":

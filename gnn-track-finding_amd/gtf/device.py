@@ -158,6 +158,14 @@ class DeviceGraph:
             owner = np.repeat(np.arange(g.n_nodes, dtype=np.int64), np.diff(g.out_ptr.astype(np.int64)))
             outpos[g.out_slot] = (np.arange(g.n_edges) - g.out_ptr[owner]).astype(np.int32)
         up("slot_outpos", outpos)
+        # global out-edge index of every slot's edge (gtf_graph.slot_outidx): the sender scan
+        # stores its running values in out-edge order (GTF_NO_OUTIDX=1: by slot, for A/B)
+        import os
+        self.use_outidx = os.environ.get("GTF_NO_OUTIDX", "0") != "1"
+        oidx = np.full(g.n_slots, -1, np.int32)
+        if g.n_edges:
+            oidx[g.out_slot] = np.arange(g.n_edges, dtype=np.int32)
+        up("slot_outidx", oidx)
         sub = g.node["sub_id"].astype(np.int64)
         if g.n_nodes:
             sizes = np.bincount(sub - sub.min())
@@ -236,7 +244,8 @@ class DeviceGraph:
                     slot_ptr=p("slot_ptr"), slot_src=p("slot_src"), slot_dst=p("slot_dst"), out_ptr=p("out_ptr"),
                     out_slot=p("out_slot"), slot_outpos=p("slot_outpos"), is_edge=p("is_edge"),
                     rev_edge=p("rev_edge"), solo=p("solo"), gnn=p("gnn"), xyzr=p("xyzr"), layer=p("layer"),
-                    out_dst=p("out_dst"), slot_layer=p("slot_layer"))
+                    out_dst=p("out_dst"), slot_layer=p("slot_layer"),
+                    slot_outidx=p("slot_outidx") if self.use_outidx else ctypes.c_void_p(0))
         # with the node schedule (lane groups) and the sender schedule
         sched = dict(n_big=self.n_big, sched=p("sched"), n_g4=self.n_g_all[0], n_g8=self.n_g_all[1],
                      n_g16=self.n_g_all[2], n_g32=self.n_g_all[3], n_g64=self.n_g_all[4], sched_seg=p("sched_seg"),

@@ -1,0 +1,182 @@
+"""Directory-to-directory stage runner for the drop-in CLIs: gpickle in -> GPU -> gpickle out,
+with the per-file host work spread over worker processes.
+
+The reference's stages (extrapolate_merged_states.py:521-572, clustering.py:380-415,
+remove_state_metadata.py:11-57) read every ``*_subgraph.gpickle`` of a directory in glob
+order, mutate the graphs and save them renumbered 0..n-1 in that order
+(helper.save_network, helper.py:585-587). Reading and writing those pickles -- networkx
+graphs whose state dicts hold small numpy arrays, ~10 us per array to pickle -- costs
+far more host time than the stage itself on the GPU (SURVEY §7 "End-to-end vs kernel
+time"). Here the files are split into contiguous chunks, one per worker process:
+
+  worker w: unpickle its files -> pack them (gtf.graph.pack) -> send the packed arrays
+  main:     concatenate the chunks (gtf.graph.concat) -> one device stage call ->
+            send each worker the mutable arrays of its node / slot range
+  worker w: write them back into its graphs (gtf.graph.unpack) -> pickle each graph to
+            the output directory under its global glob index
+
+Subgraphs are independent (no edge crosses two of them), so the concatenated stage
+equals the stage on all subgraphs together: same values, same file numbering. The
+workers are forked before this process initialises the GPU and never touch it; only
+numpy arrays cross the pipes. Reference exceptions raised on the device are re-raised
+as the reference's exception class before any output is written (the reference loses
+the stage's output too).
+"""
+from __future__ import annotations
+
+import glob
+import os
+import pickle
+from typing import Callable, List
+
+import numpy as np
+
+from .graph import SLOT_FIELDS, concat, pack, unpack
+from .stages import SUBGRAPH_SUFFIX, _raise_flags
+
+STATIC_SLOT = ("slot_src", "slot_key", "is_edge", "rev_edge", "send_mw")
+MUTABLE_NODE = ("has_merged", "merged_state", "merged_cov", "merged_prior", "has_tse", "has_uts", "degree")
+
+
+def default_workers() -> int:
+    """this process's CPU share (the GPU box gives a process 16 CPUs of a large host)"""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return max(1, min(n, env) if env else min(n, 16))
+
+
+def _chunks(n_files: int, workers: int):
+    w = max(1, min(workers, n_files))
+    bounds = np.linspace(0, n_files, w + 1).round().astype(int)
+    return [(int(bounds[i]), int(bounds[i + 1])) for i in range(w)]
+
+
+def _worker(conn, files, first_index, out_dir, states, merged):
+    """read + pack, wait for the stage's arrays, unpack + write"""
+    try:
+        subs = []
+        for f in files:
+            with open(f, "rb") as fh:
+                subs.append(pickle.load(fh))
+        g = pack(subs)
+        conn.send(g)
+        msg = conn.recv()
+        if msg is None:            # the stage raised: write nothing
+            conn.send(("ok", 0))
+            return
+        node, slot = msg
+        g.node.update(node)
+        g.slot.update(slot)
+        if g.n_nodes:
+            unpack(g, subs, states=states, merged=merged)
+        for i, s in enumerate(subs):
+            with open(os.path.join(out_dir, "%d%s" % (first_index + i, SUBGRAPH_SUFFIX)), "wb") as fh:
+                pickle.dump(s, fh, pickle.HIGHEST_PROTOCOL)
+        conn.send(("ok", len(subs)))
+    except BaseException as e:     # reported to the main process
+        conn.send(("error", repr(e)))
+    finally:
+        conn.close()
+
+
+def run_dir(input_dir: str, output_dir: str, body: Callable, *, states=("tse", "uts"), merged=True,
+            workers: int = None, host_stage: Callable = None) -> dict:
+    """Run one stage over a directory of subgraph pickles. ``body(DeviceGraph)`` issues the
+    stage's device calls (e.g. ``lambda d: d.extrapolate(p)``). Returns counts and the
+    host / device split of the wall time. ``host_stage(TrackGraph) -> flags`` replaces the
+    device (tests run the CPU checker through the same worker machinery)."""
+    import multiprocessing as mp
+    import time
+    t0 = time.perf_counter()
+    files = glob.glob(input_dir + "*" + SUBGRAPH_SUFFIX)        # the reference's glob order
+    workers = workers or default_workers()
+    chunks = _chunks(len(files), workers)
+    ctx = mp.get_context("fork")   # no exec: this process may hold the GPU (bench)
+    procs, conns = [], []
+    for lo, hi in chunks:
+        a, b = ctx.Pipe()
+        p = ctx.Process(target=_worker, args=(b, files[lo:hi], lo, output_dir, states, merged), daemon=True)
+        p.start()
+        b.close()
+        procs.append(p)
+        conns.append(a)
+    try:
+        parts = []
+        for c in conns:
+            m = c.recv()
+            if isinstance(m, tuple) and m and m[0] == "error":
+                raise RuntimeError("drop-in worker: " + m[1])
+            parts.append(m)
+        t1 = time.perf_counter()
+        nonempty = [g for g in parts if g.n_nodes]
+        flags = 0
+        out_node, out_slot = None, None
+        if nonempty and host_stage is not None:
+            g = concat(nonempty)
+            flags = int(host_stage(g) or 0)
+            out_node, out_slot = g.node, g.slot
+        elif nonempty:
+            from .device import DeviceGraph
+            g = concat(nonempty)
+            d = DeviceGraph(g)
+            d.clear_errors()
+            body(d)
+            flags = d.errors()
+            d.download(g)
+            out_node, out_slot = g.node, g.slot
+        t2 = time.perf_counter()
+        if flags:
+            for c in conns:
+                c.send(None)
+            for c in conns:
+                c.recv()
+            _raise_flags(flags)
+        n0 = s0 = 0
+        for c, part in zip(conns, parts):
+            if not part.n_nodes:
+                c.send(({}, {}))
+                continue
+            n1, s1 = n0 + part.n_nodes, s0 + part.n_slots
+            c.send(({k: out_node[k][n0:n1] for k in MUTABLE_NODE},
+                    {k: out_slot[k][s0:s1] for k in SLOT_FIELDS if k not in STATIC_SLOT}))
+            n0, s0 = n1, s1
+        written = 0
+        for c in conns:
+            m = c.recv()
+            if m[0] != "ok":
+                raise RuntimeError("drop-in worker: " + m[1])
+            written += m[1]
+        t3 = time.perf_counter()
+        return {"files": len(files), "written": written, "workers": len(chunks),
+                "edges": int(sum(p.n_edges for p in parts)), "read_pack_s": t1 - t0, "device_s": t2 - t1,
+                "unpack_write_s": t3 - t2, "wall_s": t3 - t0}
+    finally:
+        for c in conns:
+            c.close()
+        for p in procs:
+            p.join(30)
+            if p.is_alive():
+                p.kill()
+
+
+def _time_extrapolate(argv):
+    """python -m gtf.dropin IN/ OUT/ REPS: the drop-in extrapolation stage (reference flags
+    -c 2.0 -e 0.3 -z 0.4 -m 0.6 -b 550) over IN/, REPS + 1 times in this fresh process (the
+    first run loads the code objects), printing the wall time of each as JSON. bench.py's
+    dropin_stage runs it as a child process: its workers are forked before this process
+    touches the GPU."""
+    import json
+    import sys
+    from .params import Params
+    ind, outd, reps = argv[0], argv[1], int(argv[2])
+    p = Params()
+    runs = [run_dir(ind, outd, lambda d: d.extrapolate(p)) for _ in range(reps + 1)]
+    json.dump({"runs": runs[1:], "first": runs[0]}, sys.stdout)
+
+
+if __name__ == "__main__":
+    import sys
+    _time_extrapolate(sys.argv[1:])

@@ -265,7 +265,8 @@ class ShardedDeviceGraph:
                                n_g16=n_g[2], n_g32=n_g[3], n_g64=n_g[4], out_dst=p("out_dst"),
                                slot_layer=p("slot_layer"), sched_seg=vp(self.sched_seg),
                                out_sched=vp(self.out_sched), n_o4=n_o[0], n_o8=n_o[1], n_o16=n_o[2], n_g2=n_g2,
-                               out_lanes=vp(self.out_lanes))
+                               out_lanes=vp(self.out_lanes),
+                               slot_outidx=p("slot_outidx") if d.use_outidx else ctypes.c_void_p(0))
         self.shard = nat.GtfShard(vp(self.senders), int(self.senders.numel()), int(pl.node_lo[rank]),
                                   int(pl.node_hi[rank]), int(pl.slot_lo[rank]), int(pl.slot_hi[rank]))
         # halo exchange buffers and lists (fixed per plan)

@@ -10,17 +10,18 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-from gtf import stages as _st  # noqa: E402
+from gtf.dropin import run_dir  # noqa: E402
+from gtf.params import Params  # noqa: E402
 
 
 def main():
     parser = argparse.ArgumentParser(description='extract track candidates')
     parser.add_argument('-r', '--remain', help='output directory to save remaining network')
     args = parser.parse_args()
-    subGraphs = _st.read_subgraphs(args.remain)
-    _st.update_stage(subGraphs)
-    for i, sub in enumerate(subGraphs):
-        _st.save_network(args.remain, i, sub)
+    # read -> one device call -> save in place, the pickle work on worker processes
+    # (gtf.dropin; every file is read before any is written)
+    p = Params()
+    run_dir(args.remain, args.remain, lambda d: d.update(p))
 
 
 if __name__ == "__main__":

@@ -40,7 +40,7 @@ typedef void* gtf_stream_t; /* a hipStream_t */
 /* Version of the struct layouts below. gtf_graph carries it with its own size, and every
  * entry point taking a gtf_graph refuses a caller built against another layout
  * (status -3, gtf_last_error() names both). Bumped on every layout change. */
-#define GTF_ABI_VERSION 3u
+#define GTF_ABI_VERSION 4u
 
 /* ---- graph structure (read-only on the path) ------------------------------ */
 typedef struct gtf_graph {
@@ -119,6 +119,11 @@ typedef struct gtf_graph {
     int32_t pad_tile_slots;
     int32_t pad_count[6];
     int32_t pad_reserved_;
+    /* optional (v4): global out-edge index of each slot's edge, out_ptr[slot_src] + slot_outpos
+     * (-1 = no edge), or NULL. With it the sender scan stores the running merged_cov[1,1]
+     * each extrapolation sees in out-edge order (contiguous per sender, coalesced stores)
+     * and the extrapolation reads it through this index; NULL: stored by slot. [S] */
+    const int32_t* slot_outidx;
 } gtf_graph;
 
 /* ---- per-node mutable state ------------------------------------------------ */

@@ -14,6 +14,10 @@ python tools/pmc_summary.py $O/c4 profiles/r01_pmc/calib $O/c4/pmc_c4.json c4 > 
 bash tools/gpu_profile_py.sh $O/c5 tools/pkl_time.py 48 || exit 1
 timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || exit 1
 echo r03b-bench-done
+for i in 1 2; do
+  GTF_NO_OUTIDX=1 timeout -k 10 120 python tools/pass_loop.py 150 >> $O/ab_outidx.jsonl || exit 1
+  timeout -k 10 120 python tools/pass_loop.py 150 >> $O/ab_outidx.jsonl || exit 1
+done
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 60 rocprofv3 -L > $R/$O/rocprof_list.txt 2>&1
 timeout -k 10 120 rocprofv3 --pc-sampling-beta-enabled --pc-sampling-method stochastic --pc-sampling-unit cycles --pc-sampling-interval 65536 -d $R/$O/pcs -o run --output-format csv -- python3 $R/tools/pass_loop.py 200 > $R/$O/pcs.log 2>&1

@@ -1,4 +1,7 @@
-"""C4 passes back to back (tiled layout, staged inputs) for a profiler: python tools/pass_loop.py [passes]"""
+"""C4 passes back to back (tiled layout, staged inputs): device time per pass between two
+events, for A/B of builds / env switches and for profilers.
+    python tools/pass_loop.py [passes]"""
+import json
 import os
 import sys
 
@@ -13,11 +16,26 @@ K = int(sys.argv[1]) if len(sys.argv) > 1 else 100
 g = synth.workload("c4", seed=0)
 d = DeviceGraph(g, "cuda:0", layout="tiled")
 snap = d.snapshot(DeviceGraph.PASS_INPUTS)
-d.stage_inputs(min(K, 50))
+S = min(K, 50)
+d.stage_inputs(S)
 d.fill_inputs(snap)
 p = Params()
-for i in range(K):
-    d.use_inputs(i % min(K, 50))
+for i in range(5):
+    d.use_inputs(i)
     d.full_pass(p)
+d.fill_inputs(snap)
 torch.cuda.synchronize()
-print("passes", K, "flags", d.errors())
+a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+times = []
+for r in range(max(1, K // S)):
+    d.fill_inputs(snap)
+    torch.cuda.synchronize()
+    a.record()
+    for i in range(S):
+        d.use_inputs(i)
+        d.full_pass(p)
+    b.record()
+    torch.cuda.synchronize()
+    times.append(a.elapsed_time(b) / S)
+print(json.dumps({"env": {k: v for k, v in os.environ.items() if k.startswith("GTF_")}, "passes": S * len(times),
+                  "ms_per_pass": times, "flags": d.errors()}))

@@ -283,6 +283,42 @@ __device__ __forceinline__ void pkl_node1_ordered(const gtf_kl_graph& g, const g
     }
 }
 
+// tiled layout (gtf_kl_graph.blk): one block record = cnt <= BLOCK bucket-0 nodes of one tile
+// from node v0, n1 one-edge nodes first, their slots from slot0, pairs from pair0
+template <typename T, bool STATES>
+__device__ __forceinline__ void pkl_node1_tiled(const gtf_kl_graph& g, const gtf_kl_out& o, int v0, int cnt, int n1,
+                                                int64_t slot0, int64_t pair0) {
+    const int gi = (int)threadIdx.x;
+    if (gi >= cnt) return;
+    const int v = v0 + gi;
+    const bool two = gi >= n1;
+    const int64_t l = slot0 + (two ? n1 + 2 * (int64_t)(gi - n1) : gi);
+    const int64_t pp = pair0 + (gi - n1);
+    const double xv = gx(g, v), yv = gy(g, v);
+    const long long tv = (o.truth && g.truth) ? g.truth[v] : 0;
+    const int u0 = g.slot_src[l];
+    const int u1 = two ? g.slot_src[l + 1] : u0;
+    const double x0 = gx(g, u0), y0 = gy(g, u0);
+    const double x1 = gx(g, u1), y1 = gy(g, u1);
+    long long t0 = 0, t1 = 0;
+    if (o.truth && g.truth) { t0 = g.truth[u0]; t1 = g.truth[u1]; }
+    const Frame f = node_frame_xy(xv, yv);
+    bool s0, s1 = false;
+    const PState<T> a = pstate<T>(f, x0, y0, s0, STATES ? o.sv + 3 * l : nullptr, STATES ? o.cov + 9 * l : nullptr);
+    PState<T> b = a;
+    if (two) b = pstate<T>(f, x1, y1, s1, STATES ? o.sv + 3 * (l + 1) : nullptr, STATES ? o.cov + 9 * (l + 1) : nullptr);
+    if ((s0 || s1) && o.err) atomicOr(o.err, (uint32_t)GTF_ERR_SINGULAR_H);
+    const double g0 = (f.y - y0) / (f.x - x0);
+    const double g1 = two ? (f.y - y1) / (f.x - x1) : g0;
+    const double mean = two ? (g0 + g1) * 0.5 : g0;   // / 2 and / 1 as exact scalings
+    if (o.emp_var) o.emp_var[v] = two ? ((g0 - mean) * (g0 - mean) + (g1 - mean) * (g1 - mean)) * 0.5 : 0.0 * (g0 - mean);
+    if (o.emp_mean) o.emp_mean[v] = mean;
+    if (two) {
+        ((T*)o.kl)[pp] = pkl<T>(b, a);   // pair (i, j) = (1, 0)
+        if (o.truth) o.truth[pp] = (int8_t)(tv == t1 && t1 == t0 && tv == t0);
+    }
+}
+
 template <typename T, bool STATES>
 __device__ __forceinline__ void pkl_node1(const gtf_kl_graph& g, const gtf_kl_out& o, const int32_t* list, int count,
                                           int bid) {
@@ -442,6 +478,22 @@ __global__ void __launch_bounds__(BLOCK) KL_ATTR k_parabolic_kl(gtf_kl_graph g, 
     __shared__ __attribute__((aligned(16))) char smem[stage_bytes(4, sizeof(T)) > stage_bytes(64, sizeof(T))
                                                           ? stage_bytes(4, sizeof(T))
                                                           : stage_bytes(64, sizeof(T))];
+    if (g.blk) {   // tiled layout: one record per block, the blocks XCD-contiguous tile by tile
+        const int32_t* r = g.blk + 8 * (int64_t)gtf::xcd_local(blockIdx.x, gridDim.x);
+        const int q = r[0], v0 = r[1], cnt = r[2];
+        if (q == 0) {
+            const int64_t pair0 = (int64_t)(uint32_t)r[5] | ((int64_t)r[6] << 32);
+            pkl_node1_tiled<T, STATES>(g, o, v0, cnt, r[3], (int64_t)(uint32_t)r[4], pair0);
+        } else if (q == 1) {
+            if (GTF_KL_B1_LANES) pkl_node<T, 4, STATES>(g, o, nullptr, cnt, 0, smem, v0);
+            else pkl_node4<T, STATES>(g, o, nullptr, cnt, 0, v0);
+        } else if (q == 2) {
+            pkl_node<T, 8, STATES>(g, o, nullptr, cnt, 0, smem, v0);
+        } else if (q == 3) {
+            pkl_node<T, 64, STATES>(g, o, nullptr, cnt, 0, smem, v0);
+        }
+        return;
+    }
     // bucket block ranges are multiples of 8, each remapped XCD-contiguous on its own:
     // neighbouring nodes (one event's hits) share an L2
     int b = blockIdx.x;
@@ -467,6 +519,21 @@ __global__ void __launch_bounds__(BLOCK) KL_ATTR k_parabolic_kl(gtf_kl_graph g, 
 
 template <typename T>
 int launch(const gtf_kl_graph* g, const gtf_kl_out* o, hipStream_t st) {
+    if (g->blk) {   // tiled layout: the grid is the block table
+        KlBuckets bk{};
+        if (g->n_blk > 0) {
+            if (o->sv || o->cov)
+                hipLaunchKernelGGL((k_parabolic_kl<T, true>), dim3(g->n_blk), dim3(BLOCK), 0, st, *g, *o, bk);
+            else
+                hipLaunchKernelGGL((k_parabolic_kl<T, false>), dim3(g->n_blk), dim3(BLOCK), 0, st, *g, *o, bk);
+        }
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) {
+            gtf::set_error(hipGetErrorString(e));
+            return -1;
+        }
+        return 0;
+    }
     KlBuckets bk;
     bk.ordered = !g->list[0] && !g->list[1] && !g->list[2] && !g->list[3];
     int total = 0;
@@ -495,6 +562,7 @@ int launch(const gtf_kl_graph* g, const gtf_kl_out* o, hipStream_t st) {
 extern "C" int gtf_parabolic_kl(const gtf_kl_graph* g, int32_t dtype, const gtf_kl_out* out, gtf_stream_t stream) {
     if (!g || !out) { gtf::set_error("gtf_parabolic_kl: null argument"); return -2; }
     if (g->n_nodes < 0 || g->n_slots < 0) { gtf::set_error("gtf_parabolic_kl: negative sizes"); return -2; }
+    if (g->blk && g->n_blk < 0) { gtf::set_error("gtf_parabolic_kl: bad block table"); return -2; }
     int listed = 0;
     const bool ordered = !g->list[0] && !g->list[1] && !g->list[2] && !g->list[3];
     for (int i = 0; i < 4; i++) {
@@ -515,7 +583,7 @@ extern "C" int gtf_parabolic_kl(const gtf_kl_graph* g, int32_t dtype, const gtf_
         gtf::set_error("gtf_parabolic_kl: gnn_stride must be 0, 2 or 4");
         return -2;
     }
-    if (listed && (!g->slot_ptr || !g->slot_src || !g->gnn || !g->pair_ptr || !out->kl)) {
+    if ((listed || (g->blk && g->n_blk > 0)) && (!g->slot_ptr || !g->slot_src || !g->gnn || !g->pair_ptr || !out->kl)) {
         gtf::set_error("gtf_parabolic_kl: missing arrays");
         return -2;
     }

@@ -602,6 +602,8 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
         n.merged_prior[c.v] = mprior;
     }
     if (pres && (alive >> pos & 1u) && c.is_edge) c.act = 0;                       // :311-321
+    uint8_t* sc = reinterpret_cast<const gtf_diag*>(reinterpret_cast<const char*>(err) + GTF_DIAG_OFFSET)->slot_cluster;
+    if (sc && pres) sc[c.k] = (alive >> pos & 1u) ? 2 : 1;   // diagnostics: merged (1) or left (2)
 }
 
 // ---------------------------------------------------------------------------

@@ -647,6 +647,9 @@ __device__ void node_cluster(const gtf_graph& g, gtf_nodes& n, const gtf_states&
             const int ki = ord[i];
             if (g.is_edge[ki]) e.act[ki] = 0;
         }
+    uint8_t* sc = reinterpret_cast<const gtf_diag*>(reinterpret_cast<const char*>(err) + GTF_DIAG_OFFSET)->slot_cluster;
+    if (sc)   // diagnostics: merged (1) or left (2)
+        for (int i = 0; i < d; i++) sc[ord[i]] = (alive & (1u << i)) ? 2 : 1;
 }
 
 // node-local operations, executed in sequence per node by k_node

@@ -102,11 +102,12 @@ class GtfCandidateGraph(ctypes.Structure):
 class GtfKlGraph(ctypes.Structure):
     _fields_ = [("n_nodes", I32), ("n_slots", I32), ("slot_ptr", P), ("slot_src", P), ("gnn", P), ("truth", P),
                 ("pair_ptr", P), ("list", P * 4), ("count", I32 * 4), ("first", I32 * 4), ("n_d1", I32),
-                ("gnn_stride", I32), ("slot0", ctypes.c_int64), ("pair0", ctypes.c_int64)]
+                ("gnn_stride", I32), ("slot0", ctypes.c_int64), ("pair0", ctypes.c_int64), ("blk", P),
+                ("n_blk", I32), ("pad_blk_", I32)]
 
 
 class GtfDiag(ctypes.Structure):
-    _fields_ = [("node_err", P), ("edge_chi2", P), ("reserved_", P * 6)]
+    _fields_ = [("node_err", P), ("edge_chi2", P), ("slot_cluster", P), ("reserved_", P * 5)]
 
 
 DIAG_OFFSET = 64

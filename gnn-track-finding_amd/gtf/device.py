@@ -434,7 +434,7 @@ class DeviceGraph:
         return ta.cpu().numpy(), flips_hist
 
     # ------------------------------------------------------------ diagnostics
-    def set_diagnostics(self, node_err: bool = True, edge_chi2: bool = True):
+    def set_diagnostics(self, node_err: bool = True, edge_chi2: bool = True, slot_cluster: bool = False):
         """SURVEY §5's optional diagnostic outputs (gtf_set_diagnostics), written by the stage
         kernels from now on: the GTF_ERR_* bits of every reference exception per node (which
         node, so which subgraph, would make the reference raise) and the chi2 of every
@@ -448,13 +448,15 @@ class DeviceGraph:
         if edge_chi2:
             self.diag_t["edge_chi2"] = torch.full((max(self.n_slots, 1),), float("nan"), dtype=torch.float64,
                                                   device=self.device)
+        if slot_cluster:
+            self.diag_t["slot_cluster"] = torch.zeros(max(self.n_slots, 1), dtype=torch.uint8, device=self.device)
         vp = lambda k: ctypes.c_void_p(self.diag_t[k].data_ptr()) if k in self.diag_t else ctypes.c_void_p(0)  # noqa: E731
-        d = nat.GtfDiag(vp("node_err"), vp("edge_chi2"))
+        d = nat.GtfDiag(vp("node_err"), vp("edge_chi2"), vp("slot_cluster"))
         nat.check(self.lib.gtf_set_diagnostics(self.ptr("ws"), ctypes.byref(d), self.stream))
 
     def diagnostics(self) -> dict:
         """the registered diagnostics in host order: node_err [N] uint32, edge_chi2 [S]
-        (NaN where no extrapolation ran)"""
+        (NaN where no extrapolation ran), slot_cluster [S] uint8"""
         out = {}
         for k, v in getattr(self, "diag_t", {}).items():
             if k == "node_err":
@@ -462,8 +464,13 @@ class DeviceGraph:
                 out[k] = a if self.order is None else self._host_nodes(a)
             else:
                 a = v.cpu().numpy()[:self.n_slots]
-                out[k] = a if self.slot_perm is None else self._host_slots(a, np.nan)
+                out[k] = a if self.slot_perm is None else self._host_slots(a, np.nan if a.dtype.kind == "f" else 0)
         return out
+
+    def clear_diagnostics(self):
+        """zero node_err / slot_cluster and NaN-fill edge_chi2 (stream-ordered)"""
+        for k, v in getattr(self, "diag_t", {}).items():
+            v.fill_(float("nan") if k == "edge_chi2" else 0)
 
     def _host_nodes(self, a, fill=0):
         nm = self.order >= 0

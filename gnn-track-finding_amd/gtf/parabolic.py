@@ -54,15 +54,24 @@ class ParabolicKL:
     layout: the kernel reaches the two-edge bucket by arithmetic). Device outputs are then
     in that order: ``node_of`` maps a device node to the caller's, pair_index() returns the
     caller's node ids, and ``host_nodes`` / ``host_slots`` reorder per-node / per-slot
-    outputs; pairs keep the caller's (node, i, j) rows through pair_index()."""
+    outputs; pairs keep the caller's (node, i, j) rows through pair_index().
 
-    def __init__(self, slot_ptr, slot_src, gnn, truth=None, device="cuda", with_single=False, ordered=False):
+    tile = T > 0: the same bucket order inside every tile of T consecutive nodes (an event
+    of a batch, or part of one) instead of over the whole batch, with one block record per
+    wavefront (gtf_kl_graph.blk): a node's neighbours are hits of its own event, so they sit
+    in its own tile and the neighbour gathers find the lines the tile's own reads brought
+    into L2, instead of reaching across the whole batch."""
+
+    def __init__(self, slot_ptr, slot_src, gnn, truth=None, device="cuda", with_single=False, ordered=False,
+                 tile=0):
         slot_ptr = np.ascontiguousarray(slot_ptr, np.int32)
         self.n_nodes = int(slot_ptr.shape[0] - 1)
         self.n_slots = int(slot_ptr[-1])
         d = np.diff(slot_ptr).astype(np.int64)
         lo = 1 if with_single else 2
         self.node_of = self.slot_of = None
+        self.tile = int(tile)
+        ordered = ordered or self.tile > 0
         if ordered:
             sp = slot_ptr.astype(np.int64)
             keys = [d == 1 if lo == 1 else np.zeros(d.size, bool), d == 2] + \
@@ -70,7 +79,12 @@ class ParabolicKL:
             rank = np.full(d.size, len(keys), np.int64)
             for q in reversed(range(len(keys))):
                 rank[keys[q]] = q
-            order = np.argsort(rank, kind="stable")
+            if self.tile > 0:   # bucket order inside each tile of consecutive nodes
+                tid = np.arange(d.size, dtype=np.int64) // self.tile
+                order = np.lexsort((np.arange(d.size), rank, tid))
+                self._tiles = (tid[order], rank[order])
+            else:
+                order = np.argsort(rank, kind="stable")
             nd = d[order]
             new_ptr = np.zeros(self.n_nodes + 1, np.int64)
             np.cumsum(nd, out=new_ptr[1:])
@@ -85,6 +99,7 @@ class ParabolicKL:
             d = nd
             self.node_of, self.slot_of = order, slot_of
             self._ranges = [int(k.sum()) for k in keys]
+        self.slot_ptr_host = np.asarray(slot_ptr, np.int64)
         npair = np.where(d >= 2, d * (d - 1) // 2, 0)
         pair_ptr = np.zeros(self.n_nodes + 1, np.int64)
         np.cumsum(npair, out=pair_ptr[1:])
@@ -105,7 +120,15 @@ class ParabolicKL:
         self.lists = [t(x) for x in lists]
         self.device = dev
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)
-        if ordered:   # bucket ranges, no lists
+        if self.tile > 0:   # one block record per wavefront (gtf_kl_graph.blk)
+            blk = self._block_table(d, pair_ptr)
+            self.blk = t(blk)
+            self.n_blk = int(blk.size // 8)
+            self._g = nat.GtfKlGraph(self.n_nodes, self.n_slots, _ptr(self.slot_ptr), _ptr(self.slot_src),
+                                     _ptr(self.gnn), _ptr(self.truth), _ptr(self.pair_ptr),
+                                     (ctypes.c_void_p * 4)(), (ctypes.c_int32 * 4)(), (ctypes.c_int32 * 4)(), 0, 2,
+                                     0, 0, _ptr(self.blk), self.n_blk)
+        elif ordered:   # bucket ranges, no lists
             n1, n2 = self._ranges[0], self._ranges[1]
             counts = [n1 + n2] + [int(x.size) for x in lists[1:]]
             first = np.concatenate([[0], np.cumsum(counts)[:-1]]).astype(np.int32)
@@ -119,6 +142,32 @@ class ParabolicKL:
                                      (ctypes.c_void_p * 4)(*[x.data_ptr() if x.numel() else None for x in self.lists]),
                                      (ctypes.c_int32 * 4)(*[x.numel() for x in self.lists]), gnn_stride=2)
 
+    def _block_table(self, d, pair_ptr, block=64):
+        """gtf_kl_graph.blk of the tiled layout: per tile (in node order) the blocks of its
+        > 8-edge nodes (one per block), 5..8-edge nodes (8 per block), 3..4-edge nodes (64)
+        and one- / two-edge nodes (64; one-edge first), each record (q, first node, count,
+        one-edge count, first slot, first pair lo / hi, 0)"""
+        tid, rank = self._tiles
+        sp = self.slot_ptr_host
+        recs = []
+        nt = int(tid.max()) + 1 if tid.size else 0
+        bounds = np.searchsorted(tid, np.arange(nt + 1))
+        for t_ in range(nt):
+            a, b = int(bounds[t_]), int(bounds[t_ + 1])
+            r = rank[a:b]
+            cut = a + np.searchsorted(r, np.arange(7))      # rank runs inside the tile
+            for q, (r0, r1), per in ((3, (4, 5), 1), (2, (3, 4), block // 8), (1, (2, 3), block), (0, (0, 2), block)):
+                s0, s1 = int(cut[r0]), int(cut[r1])
+                n1_all = int(cut[1] - cut[0]) if q == 0 else 0
+                for v0 in range(s0, s1, per):
+                    cnt = min(per, s1 - v0)
+                    n1 = max(0, min(cnt, n1_all - (v0 - s0))) if q == 0 else 0
+                    pr = int(pair_ptr[v0 + n1]) if q == 0 and n1 < cnt else 0
+                    recs.append((q, v0, cnt, n1, int(sp[v0]) if q == 0 else 0, pr & 0xFFFFFFFF, pr >> 32, 0))
+        a = np.asarray(recs, np.int64).reshape(-1, 8)
+        a[:, 5] = np.where(a[:, 5] >= 2**31, a[:, 5] - 2**32, a[:, 5])   # the low word as int32 bits
+        return a.astype(np.int32).reshape(-1)
+
     def replica(self, gnn=None):
         """An independent copy of this batch in its own device buffers (same structure):
         ``gnn`` (caller's node order, [N, 4] or [N, 2]) replaces the coordinates, e.g. a
@@ -130,6 +179,8 @@ class ParabolicKL:
         r.slot_ptr, r.slot_src, r.pair_ptr = cl(self.slot_ptr), cl(self.slot_src), cl(self.pair_ptr)
         r.truth = cl(self.truth)
         r.lists = [cl(x) for x in self.lists]
+        if getattr(self, "blk", None) is not None:
+            r.blk = cl(self.blk)
         r.err = torch.zeros(1, dtype=torch.int32, device=self.device)
         if gnn is None:
             r.gnn = cl(self.gnn)
@@ -141,6 +192,8 @@ class ParabolicKL:
         g = nat.GtfKlGraph.from_buffer_copy(self._g)
         g.slot_ptr, g.slot_src, g.gnn = _ptr(r.slot_ptr), _ptr(r.slot_src), _ptr(r.gnn)
         g.truth, g.pair_ptr = _ptr(r.truth), _ptr(r.pair_ptr)
+        if getattr(r, "blk", None) is not None:
+            g.blk = _ptr(r.blk)
         for q in range(4):
             if g.list[q]:
                 g.list[q] = r.lists[q].data_ptr() if r.lists[q].numel() else None

@@ -202,7 +202,8 @@ int gtf_clear_errors(void* workspace, gtf_stream_t stream);
  *                  (gtf_pass / gtf_extrapolate / gtf_update / gtf_cluster / gtf_node_ops);
  *                  caller-zeroed uint32 [N]: which node (so which subgraph) would raise;
  *   edge_chi2[k]  = chi2 of the extrapolation of slot k's edge (every active out-edge of a
- *                  merged sender, accepted or not; untouched elsewhere), double [S].
+ *                  merged sender, accepted or not; untouched elsewhere), double [S];
+ *   slot_cluster  = which states each clustered node merged and which it left (below).
  * The truth-based confusion counts of the reference's printouts (helper.py:186-225,
  * extrapolate_merged_states.py:496-518, clustering.py:342-369) follow on the host from
  * the masks (gtf/diagnostics.py). Nothing here is on the timed path: with no diagnostics
@@ -211,7 +212,12 @@ int gtf_clear_errors(void* workspace, gtf_stream_t stream);
 typedef struct gtf_diag {
     uint32_t* node_err;       /* [N] device, or NULL */
     double*   edge_chi2;      /* [S] device, or NULL */
-    void*     reserved_[6];   /* zero */
+    uint8_t*  slot_cluster;   /* [S] device, or NULL: for every node that clustered (gtf_cluster,
+                                 gtf_pass), 1 on the slots of the states merged into its merged
+                                 state (clustering.py's edges_to_remain_active), 2 on the states
+                                 left over, whose in-edges it deactivates (edges_to_deactivate);
+                                 untouched elsewhere (caller-zeroed) */
+    void*     reserved_[5];   /* zero */
 } gtf_diag;
 int gtf_set_diagnostics(void* workspace, const gtf_diag* d, gtf_stream_t stream);
 /* Copy the error word to the host (synchronises the stream). */
@@ -456,6 +462,17 @@ typedef struct gtf_kl_graph {
                                  the kernel reads only x and y, so half the gathered bytes) */
     int64_t slot0;
     int64_t pair0;
+    /* tiled layout (gtf.parabolic.ParabolicKL(tile=T)): nodes in tiles of consecutive nodes,
+     * each tile ordered by bucket like the ordered layout, so a node's neighbours -- the
+     * same event's hits -- sit in its own tile and the neighbour gathers hit the L2 the
+     * tile's own reads filled. One record of 8 int32 per block (one wavefront):
+     * (bucket q, first node, node count, one-edge nodes among them (q = 0), first slot
+     * (q = 0), first pair (q = 0, low and high 32 bits), 0); a block takes count <= 64
+     * nodes of one tile's bucket q (8 per block for q = 2, 1 for q = 3). blk != NULL
+     * overrides list / first / count. The blocks run in XCD-contiguous order. */
+    const int32_t* blk;       /* [8 * n_blk] or NULL */
+    int32_t n_blk;
+    int32_t pad_blk_;
 } gtf_kl_graph;
 
 enum { GTF_F64 = 0, GTF_F32 = 1 };

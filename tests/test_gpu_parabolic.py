@@ -196,11 +196,14 @@ def test_gpu_beyond_lds_recompute_path():
     assert _rel(kl, ref).max() < 1e-6
 
 
+@pytest.mark.parametrize("tile", [0, 8748, 1000])
 @pytest.mark.parametrize("with_single", [False, True])
-def test_gpu_ordered_layout_equals_lists(with_single):
-    """ParabolicKL(ordered=True) (bucket node ranges, the two-edge bucket by arithmetic)
-    gives the list layout's pair rows, truth flags, gradient moments and states bit for
-    bit once mapped back to the caller's order (16 jittered copies of the vol-7 event)"""
+def test_gpu_ordered_layout_equals_lists(with_single, tile):
+    """ParabolicKL(ordered=True) (bucket node ranges, the two-edge bucket by arithmetic) and
+    ParabolicKL(tile=T) (the same inside tiles of T nodes, one block record per wavefront:
+    T = one event, and tiles that cut events) give the list layout's pair rows, truth
+    flags, gradient moments and states bit for bit once mapped back to the caller's order
+    (16 jittered copies of the vol-7 event)"""
     from gtf import io, parabolic
     kat = os.path.join(GOLDEN, "kat134")
     g = io.load_event(os.path.join(kat, "event_1_filtered_graph_"), 7, 7)
@@ -209,7 +212,8 @@ def test_gpu_ordered_layout_equals_lists(with_single):
     ptr, src, gnn, tr = parabolic.batch(ptr, src, g.node["gnn"], truth, 16)
     res = []
     for ordered in (False, True):
-        k = parabolic.ParabolicKL(ptr, src, gnn, tr, with_single=with_single, ordered=ordered)
+        k = parabolic.ParabolicKL(ptr, src, gnn, tr, with_single=with_single, ordered=ordered,
+                                  tile=tile if ordered else 0)
         out = k.run(k.alloc("f64", emp=True, states=with_single), "f64")
         node, i, j = k.pair_index()
         key = np.lexsort((j, i, node))

@@ -21,4 +21,4 @@ if __name__ == "__main__":
     print(json.dumps({"lib": os.environ.get("GTF_LIB", "default"),
                       **{dt + "_ms": r[dt]["kernel_ms"] for dt in dts},
                       **{dt + "_frac": r[dt]["roofline"]["frac"] for dt in dts},
-                      "footprint": r["f64"]["roofline"]["footprint_bytes_all_batches"]}))
+                      "footprint": r["f64"]["roofline"]["footprint_bytes_all_batches"], "layout": r["layout"]}))

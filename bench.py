@@ -174,7 +174,7 @@ def dropin_stage_wall(params, reps=3):
         shutil.rmtree(tmp, ignore_errors=True)
 
 
-def bench_c5(dev, steps, warmup, n_events=256, n_batches=8, hot=True, dtypes=("f64", "f32")):
+def bench_c5(dev, steps, warmup, n_events=256, n_batches=8, hot=True, dtypes=("f64", "f32"), kl_tile=None):
     """Config 5: parabolic-model states + pairwise KL (gtf_parabolic_kl) over a batch of
     256 copies of the committed volume-7 134 event (tests/golden/kat134, coordinates
     jittered per copy), fp64 and fp32, with the fp32-vs-fp64 tolerance sweep.
@@ -193,10 +193,14 @@ def bench_c5(dev, steps, warmup, n_events=256, n_batches=8, hot=True, dtypes=("f
     truth = io.read_truth(os.path.join(kat, "truth_vol7.csv"), g.node["node_id"])
     ptr0, src0 = parabolic.in_edge_csr(g)
     ptr, src, gnn, tr = parabolic.batch(ptr0, src0, g.node["gnn"], truth, n_events)
-    k = parabolic.ParabolicKL(ptr, src, gnn, tr, dev, ordered=True)
+    if kl_tile is None:
+        kl_tile = int(os.environ.get("GTF_KL_TILE", "0"))   # 0: the ordered layout (the tiled one measured no faster)
+    # tiled: azimuth-sorted per event (sort window = one event's nodes), then tiles
+    k = parabolic.ParabolicKL(ptr, src, gnn, tr, dev, ordered=True, tile=kl_tile, sort_window=ptr0.size - 1)
     ks = [k] + [k.replica(gnn=parabolic.batch(ptr0, src0, g.node["gnn"], truth, n_events, seed=e)[2])
                 for e in range(1, n_batches)]
     res = {"workload": "%d x committed vol-7 134 event (jittered copies)" % n_events, "nodes": k.n_nodes,
+           "layout": "tiled, %d nodes per tile" % kl_tile if kl_tile else "ordered (bucket ranges over the batch)",
            "in_edges": k.n_slots, "pairs": k.n_pairs, "listed_nodes": k.n_listed, "batches_rotated": n_batches}
     outs = {}
     launches = max(steps, 2 * n_batches) // n_batches * n_batches
@@ -253,7 +257,8 @@ def bench_c5(dev, steps, warmup, n_events=256, n_batches=8, hot=True, dtypes=("f
 
 def bench_components(g, params, dev, reps=5):
     """The north-star loop's other two device stages on the bench event (SURVEY §8 a15,
-    a16), after one fused pass (natural node order: both take host-order arrays):
+    a16), after one fused pass, in the headline's tiled node order (host-order inputs and
+    outputs are mapped by DeviceGraph):
     the updated-state distance table (calculate_distance_between_updated_track_states.py,
     gtf_updated_state_distances: pair counts, scan, pair kernel) and tag propagation
     (tag_propagation.py:97-164, Jacobi max sweeps until flips / processed <= 10 %, the flip
@@ -262,7 +267,7 @@ def bench_components(g, params, dev, reps=5):
     import torch
     from gtf.device import DeviceGraph
     from gtf import roofline as rf
-    d = DeviceGraph(g, dev)
+    d = DeviceGraph(g, dev, layout="tiled")
     d.clear_errors()
     d.full_pass(params)
     out = {}
@@ -292,8 +297,8 @@ def bench_components(g, params, dev, reps=5):
     keep = torch.zeros(max(g.n_edges, 1), dtype=torch.uint8, device=dev)
     proc = torch.zeros(max(g.n_nodes, 1), dtype=torch.uint8, device=dev)
     cnt = torch.zeros(2, dtype=torch.int32, device=dev)
-    rad = torch.from_numpy(radius).to(dev)
-    ta = torch.from_numpy(tags).to(dev)
+    rad = torch.from_numpy(np.ascontiguousarray(d._to_dev_nodes(radius))).to(dev)
+    ta = torch.from_numpy(np.ascontiguousarray(d._to_dev_nodes(tags))).to(dev)
     tb = torch.empty_like(ta)
     d.lib.gtf_tag_prepare(ctypes.byref(d.cg), vp(rad), vp(keep), vp(proc), vp(cnt), d.stream)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

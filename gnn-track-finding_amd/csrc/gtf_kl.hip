@@ -73,6 +73,38 @@ __device__ __forceinline__ int64_t gnn_row(const gtf_kl_graph& g, int v) {
 __device__ __forceinline__ double gx(const gtf_kl_graph& g, int v) { return g.gnn[gnn_row(g, v)]; }
 __device__ __forceinline__ double gy(const gtf_kl_graph& g, int v) { return g.gnn[gnn_row(g, v) + 1]; }
 
+// where a kernel reads neighbour coordinates and truth ids: global memory, or a block's
+// LDS window of consecutive nodes [lo, hi) with global memory beyond it
+struct GSrc {
+    const gtf_kl_graph* g;
+    __device__ __forceinline__ double x(int u) const { return gx(*g, u); }
+    __device__ __forceinline__ double y(int u) const { return gy(*g, u); }
+    __device__ __forceinline__ long long t(int u) const { return g->truth[u]; }
+};
+struct WSrc {
+    const gtf_kl_graph* g;
+    const double* sx;
+    const double* sy;
+    const long long* st;
+    int lo, hi;
+    __device__ __forceinline__ bool in(int u) const { return u >= lo && u < hi; }
+    // the LDS read at a clamped index always, the global one only outside the window: a
+    // select of values (a select of an LDS and a global address miscompiles on gfx950)
+    __device__ __forceinline__ int at(int u) const { return min(max(u - lo, 0), hi - lo - 1); }
+    __device__ __forceinline__ double x(int u) const {
+        const double a = sx[at(u)];
+        return in(u) ? a : gx(*g, u);
+    }
+    __device__ __forceinline__ double y(int u) const {
+        const double a = sy[at(u)];
+        return in(u) ? a : gy(*g, u);
+    }
+    __device__ __forceinline__ long long t(int u) const {
+        const long long a = st[at(u)];
+        return in(u) ? a : g->truth[u];
+    }
+};
+
 template <typename T>
 struct PState {
     T s0, s1, c00, c11, i00, i01, i11;
@@ -160,18 +192,13 @@ constexpr size_t stage_bytes(int G, size_t t) { return (size_t)(BLOCK / G) * G *
 
 // one node per group of G lanes; states staged in LDS when d <= G (always, except in
 // the wavefront bucket beyond 64 in-edges, where pair lanes recompute both states)
-template <typename T, int G, bool STATES>
-__device__ __forceinline__ void pkl_node(const gtf_kl_graph& g, const gtf_kl_out& o, const int32_t* list, int count,
-                                         int bid, char* smem, int first = 0) {
-    using Stage = KlStage<T, G>;
-    const int gi = (bid * BLOCK + (int)threadIdx.x) / G;
-    const int gl = threadIdx.x & (G - 1);
-    if (gi >= count) return;  // group-uniform
-    const int v = list ? list[gi] : first + gi;   // (ordered layout: the bucket is a node range)
+// node v on G lanes (lane gl), its states staged at stg
+template <typename T, int G, bool STATES, typename S>
+__device__ __forceinline__ void pkl_node_body(const gtf_kl_graph& g, const gtf_kl_out& o, const S& src, int v, int gl,
+                                              KlStage<T, G>* stg) {
     const int lo = g.slot_ptr[v], d = g.slot_ptr[v + 1] - lo;
     if (d < 1) return;
-    Stage* stg = (Stage*)smem + (int)threadIdx.x / G;
-    const Frame f = node_frame_xy(gx(g, v), gy(g, v));
+    const Frame f = node_frame_xy(src.x(v), src.y(v));
 
     // states of the node's in-edges and the gradients dy/dx (utils.py:249-254, 273-283)
     double gsum = 0.0, gr0 = 0.0;
@@ -179,14 +206,14 @@ __device__ __forceinline__ void pkl_node(const gtf_kl_graph& g, const gtf_kl_out
     for (int q = gl; q < d; q += G) {
         const int k = lo + q;
         const int u = g.slot_src[k];
-        const double xb = gx(g, u), yb = gy(g, u);
+        const double xb = src.x(u), yb = src.y(u);
         bool s;
         const PState<T> p = pstate<T>(f, xb, yb, s, STATES ? o.sv + 3 * (int64_t)k : nullptr,
                                       STATES ? o.cov + 9 * (int64_t)k : nullptr);
         sing |= s;
         if (d <= G) {
             put<T>(stg, q, p);
-            if (g.truth) stg->tr[q] = g.truth[u];
+            if (g.truth) stg->tr[q] = src.t(u);
         }
         const double gr = (f.y - yb) / (f.x - xb);
         if (q == gl) gr0 = gr;
@@ -200,7 +227,7 @@ __device__ __forceinline__ void pkl_node(const gtf_kl_graph& g, const gtf_kl_out
             double gr = gr0;
             if (q != gl) {
                 const int u = g.slot_src[lo + q];
-                gr = (f.y - gy(g, u)) / (f.x - gx(g, u));
+                gr = (f.y - src.y(u)) / (f.x - src.x(u));
             }
             vs += (gr - mean) * (gr - mean);
         }
@@ -216,7 +243,7 @@ __device__ __forceinline__ void pkl_node(const gtf_kl_graph& g, const gtf_kl_out
     // consecutive distances (calc_pairwise_distances, :19-25)
     const int np = d * (d - 1) / 2;
     const int64_t base = g.pair_ptr[v];
-    const long long tv = g.truth ? g.truth[v] : 0;
+    const long long tv = g.truth ? src.t(v) : 0;
     T* kl = (T*)o.kl;
     for (int t = gl; t < np; t += G) {
         int i, j;
@@ -230,13 +257,23 @@ __device__ __forceinline__ void pkl_node(const gtf_kl_graph& g, const gtf_kl_out
         } else {  // beyond the LDS stage (wavefront bucket, d > 64): recompute both states
             bool s;
             const int ui = g.slot_src[lo + i], uj = g.slot_src[lo + j];
-            a = pstate<T>(f, gx(g, ui), gy(g, ui), s, nullptr, nullptr);
-            b = pstate<T>(f, gx(g, uj), gy(g, uj), s, nullptr, nullptr);
-            if (o.truth) { ti = g.truth[ui]; tj = g.truth[uj]; }
+            a = pstate<T>(f, src.x(ui), src.y(ui), s, nullptr, nullptr);
+            b = pstate<T>(f, src.x(uj), src.y(uj), s, nullptr, nullptr);
+            if (o.truth) { ti = src.t(ui); tj = src.t(uj); }
         }
         kl[base + t] = pkl<T>(a, b);
         if (o.truth) o.truth[base + t] = (int8_t)(tv == ti && ti == tj && tv == tj);  // (:84-95)
     }
+}
+
+template <typename T, int G, bool STATES>
+__device__ __forceinline__ void pkl_node(const gtf_kl_graph& g, const gtf_kl_out& o, const int32_t* list, int count,
+                                         int bid, char* smem, int first = 0) {
+    const int gi = (bid * BLOCK + (int)threadIdx.x) / G;
+    if (gi >= count) return;  // group-uniform
+    const int v = list ? list[gi] : first + gi;   // (ordered layout: the bucket is a node range)
+    pkl_node_body<T, G, STATES>(g, o, GSrc{&g}, v, threadIdx.x & (G - 1),
+                                (KlStage<T, G>*)smem + (int)threadIdx.x / G);
 }
 
 // d <= 2: one thread per node, both states in registers (the bulk of a TrackML
@@ -283,25 +320,19 @@ __device__ __forceinline__ void pkl_node1_ordered(const gtf_kl_graph& g, const g
     }
 }
 
-// tiled layout (gtf_kl_graph.blk): one block record = cnt <= BLOCK bucket-0 nodes of one tile
-// from node v0, n1 one-edge nodes first, their slots from slot0, pairs from pair0
-template <typename T, bool STATES>
-__device__ __forceinline__ void pkl_node1_tiled(const gtf_kl_graph& g, const gtf_kl_out& o, int v0, int cnt, int n1,
-                                                int64_t slot0, int64_t pair0) {
-    const int gi = (int)threadIdx.x;
-    if (gi >= cnt) return;
-    const int v = v0 + gi;
-    const bool two = gi >= n1;
-    const int64_t l = slot0 + (two ? n1 + 2 * (int64_t)(gi - n1) : gi);
-    const int64_t pp = pair0 + (gi - n1);
-    const double xv = gx(g, v), yv = gy(g, v);
-    const long long tv = (o.truth && g.truth) ? g.truth[v] : 0;
+// one- or two-edge node v (two: its slots l, l + 1 and pair pp; else slot l): both states
+// in registers
+template <typename T, bool STATES, typename S>
+__device__ __forceinline__ void pkl_b0_body(const gtf_kl_graph& g, const gtf_kl_out& o, const S& src, int v, bool two,
+                                            int64_t l, int64_t pp) {
+    const double xv = src.x(v), yv = src.y(v);
+    const long long tv = (o.truth && g.truth) ? src.t(v) : 0;
     const int u0 = g.slot_src[l];
     const int u1 = two ? g.slot_src[l + 1] : u0;
-    const double x0 = gx(g, u0), y0 = gy(g, u0);
-    const double x1 = gx(g, u1), y1 = gy(g, u1);
+    const double x0 = src.x(u0), y0 = src.y(u0);
+    const double x1 = src.x(u1), y1 = src.y(u1);
     long long t0 = 0, t1 = 0;
-    if (o.truth && g.truth) { t0 = g.truth[u0]; t1 = g.truth[u1]; }
+    if (o.truth && g.truth) { t0 = src.t(u0); t1 = src.t(u1); }
     const Frame f = node_frame_xy(xv, yv);
     bool s0, s1 = false;
     const PState<T> a = pstate<T>(f, x0, y0, s0, STATES ? o.sv + 3 * l : nullptr, STATES ? o.cov + 9 * l : nullptr);
@@ -396,16 +427,12 @@ __device__ __forceinline__ void pkl_node1(const gtf_kl_graph& g, const gtf_kl_ou
 #ifndef GTF_KL_B1_LANES
 #define GTF_KL_B1_LANES 0
 #endif
-template <typename T, bool STATES>
-__device__ __forceinline__ void pkl_node4(const gtf_kl_graph& g, const gtf_kl_out& o, const int32_t* list, int count,
-                                          int bid, int first) {
-    const int gi = bid * BLOCK + (int)threadIdx.x;
-    if (gi >= count) return;
-    const int v = list ? list[gi] : first + gi;
+template <typename T, bool STATES, typename S>
+__device__ __forceinline__ void pkl_node4_body(const gtf_kl_graph& g, const gtf_kl_out& o, const S& src, int v) {
     const int lo = g.slot_ptr[v], d = g.slot_ptr[v + 1] - lo;
     const int64_t base = g.pair_ptr[v];
-    const double xv = gx(g, v), yv = gy(g, v);
-    const long long tv = (o.truth && g.truth) ? g.truth[v] : 0;
+    const double xv = src.x(v), yv = src.y(v);
+    const long long tv = (o.truth && g.truth) ? src.t(v) : 0;
     if (d < 1 || d > 4) return;
     int u[4];
 #pragma unroll
@@ -414,9 +441,9 @@ __device__ __forceinline__ void pkl_node4(const gtf_kl_graph& g, const gtf_kl_ou
     long long tu[4];
 #pragma unroll
     for (int q = 0; q < 4; q++) {
-        xb[q] = q < d ? gx(g, u[q]) : 0.0;
-        yb[q] = q < d ? gy(g, u[q]) : 0.0;
-        tu[q] = (q < d && o.truth && g.truth) ? g.truth[u[q]] : 0;
+        xb[q] = q < d ? src.x(u[q]) : 0.0;
+        yb[q] = q < d ? src.y(u[q]) : 0.0;
+        tu[q] = (q < d && o.truth && g.truth) ? src.t(u[q]) : 0;
     }
     const Frame f = node_frame_xy(xv, yv);
     PState<T> st[4];
@@ -459,6 +486,14 @@ __device__ __forceinline__ void pkl_node4(const gtf_kl_graph& g, const gtf_kl_ou
             }
 }
 
+template <typename T, bool STATES>
+__device__ __forceinline__ void pkl_node4(const gtf_kl_graph& g, const gtf_kl_out& o, const int32_t* list, int count,
+                                          int bid, int first) {
+    const int gi = bid * BLOCK + (int)threadIdx.x;
+    if (gi >= count) return;
+    pkl_node4_body<T, STATES>(g, o, GSrc{&g}, list ? list[gi] : first + gi);
+}
+
 struct KlBuckets {
     int32_t blocks[4];
     int32_t ordered;   // gtf_kl_graph's ordered layout (every list NULL)
@@ -478,22 +513,6 @@ __global__ void __launch_bounds__(BLOCK) KL_ATTR k_parabolic_kl(gtf_kl_graph g, 
     __shared__ __attribute__((aligned(16))) char smem[stage_bytes(4, sizeof(T)) > stage_bytes(64, sizeof(T))
                                                           ? stage_bytes(4, sizeof(T))
                                                           : stage_bytes(64, sizeof(T))];
-    if (g.blk) {   // tiled layout: one record per block, the blocks XCD-contiguous tile by tile
-        const int32_t* r = g.blk + 8 * (int64_t)gtf::xcd_local(blockIdx.x, gridDim.x);
-        const int q = r[0], v0 = r[1], cnt = r[2];
-        if (q == 0) {
-            const int64_t pair0 = (int64_t)(uint32_t)r[5] | ((int64_t)r[6] << 32);
-            pkl_node1_tiled<T, STATES>(g, o, v0, cnt, r[3], (int64_t)(uint32_t)r[4], pair0);
-        } else if (q == 1) {
-            if (GTF_KL_B1_LANES) pkl_node<T, 4, STATES>(g, o, nullptr, cnt, 0, smem, v0);
-            else pkl_node4<T, STATES>(g, o, nullptr, cnt, 0, v0);
-        } else if (q == 2) {
-            pkl_node<T, 8, STATES>(g, o, nullptr, cnt, 0, smem, v0);
-        } else if (q == 3) {
-            pkl_node<T, 64, STATES>(g, o, nullptr, cnt, 0, smem, v0);
-        }
-        return;
-    }
     // bucket block ranges are multiples of 8, each remapped XCD-contiguous on its own:
     // neighbouring nodes (one event's hits) share an L2
     int b = blockIdx.x;
@@ -517,15 +536,73 @@ __global__ void __launch_bounds__(BLOCK) KL_ATTR k_parabolic_kl(gtf_kl_graph g, 
     else pkl_node1<T, STATES>(g, o, g.list[0], g.count[0], gtf::xcd_local(b, bk.blocks[0]));
 }
 
+// Tiled layout (gtf_kl_graph.blk, gtf.parabolic.ParabolicKL(tile=T)): one block of WBLOCK
+// threads per tile of <= WTILE nodes, the nodes of a tile ordered by bucket (one- and
+// two-edge, 3..4, 5..8, > 8 in-edges), the tiles cut from an azimuth-sorted node order.
+// The block first copies the x, y and truth ids of its window -- the tile and its two
+// neighbours, where the neighbours of its nodes lie -- into LDS in one round of coalesced
+// loads; every node then reads its neighbours from LDS (global memory beyond the window),
+// so a node costs one round of memory latency instead of two dependent ones (the slot
+// list, then the gathers). Record per tile (12 int32): first node, bucket-0 count, its
+// one-edge count, bucket 1 / 2 / 3 counts, bucket 0's first slot, its first pair (lo, hi),
+// window [lo, hi), 0.
+constexpr int WBLOCK = 256;
+constexpr int WTILE = 256;
+constexpr int WWIN = 3 * WTILE;
+constexpr size_t wstage_bytes(size_t t) {
+    return stage_bytes(8, t) * (WBLOCK / BLOCK) > stage_bytes(64, t) * (WBLOCK / BLOCK)
+               ? stage_bytes(8, t) * (WBLOCK / BLOCK) : stage_bytes(64, t) * (WBLOCK / BLOCK);
+}
+#ifndef GTF_KL_WIN_WAVES
+#define GTF_KL_WIN_WAVES 4
+#endif
+template <typename T, bool STATES>
+__global__ void __launch_bounds__(WBLOCK) __attribute__((amdgpu_waves_per_eu(GTF_KL_WIN_WAVES)))
+k_parabolic_kl_win(gtf_kl_graph g, gtf_kl_out o) {
+    __shared__ double sx[WWIN], sy[WWIN];
+    __shared__ long long st[WWIN];
+    __shared__ __attribute__((aligned(16))) char stage[wstage_bytes(sizeof(T))];
+    const int32_t* r = g.blk + 12 * (int64_t)gtf::xcd_local(blockIdx.x, gridDim.x);
+    const int node_lo = r[0], n0 = r[1], n1 = r[2], nb1 = r[3], nb2 = r[4], nb3 = r[5];
+    const int64_t slot_lo = (int64_t)(uint32_t)r[6];
+    const int64_t pair_lo = (int64_t)(uint32_t)r[7] | ((int64_t)r[8] << 32);
+    const int wlo = r[9], whi = r[10];
+    for (int i = (int)threadIdx.x; i < whi - wlo; i += WBLOCK) {
+        sx[i] = gx(g, wlo + i);
+        sy[i] = gy(g, wlo + i);
+        if (g.truth) st[i] = g.truth[wlo + i];
+    }
+    __syncthreads();
+    const WSrc src{&g, sx, sy, st, wlo, whi};
+    const int t = (int)threadIdx.x;
+    // > 8 in-edges: one wavefront per node (each wave's stage region is its own 4 KB)
+    for (int i = t / 64, v = node_lo + n0 + nb1 + nb2; i < nb3; i += WBLOCK / 64) {
+        pkl_node_body<T, 64, STATES>(g, o, src, v + i, t & 63, (KlStage<T, 64>*)stage + t / 64);
+        gtf::wave_lds_sync();
+    }
+    // 5..8: 8 lanes per node (the groups of a wave use that wave's 4 KB as well)
+    for (int i = t / 8, v = node_lo + n0 + nb1; i < nb2; i += WBLOCK / 8) {
+        pkl_node_body<T, 8, STATES>(g, o, src, v + i, t & 7, (KlStage<T, 8>*)stage + t / 8);
+        gtf::wave_lds_sync();
+    }
+    // 3..4: one thread per node
+    for (int i = t, v = node_lo + n0; i < nb1; i += WBLOCK) pkl_node4_body<T, STATES>(g, o, src, v + i);
+    // one and two in-edges: one thread per node, slots and pair by arithmetic
+    for (int i = t; i < n0; i += WBLOCK) {
+        const bool two = i >= n1;
+        pkl_b0_body<T, STATES>(g, o, src, node_lo + i, two, slot_lo + (two ? n1 + 2 * (int64_t)(i - n1) : i),
+                               pair_lo + (i - n1));
+    }
+}
+
 template <typename T>
 int launch(const gtf_kl_graph* g, const gtf_kl_out* o, hipStream_t st) {
-    if (g->blk) {   // tiled layout: the grid is the block table
-        KlBuckets bk{};
+    if (g->blk) {   // tiled layout: one block per tile record
         if (g->n_blk > 0) {
             if (o->sv || o->cov)
-                hipLaunchKernelGGL((k_parabolic_kl<T, true>), dim3(g->n_blk), dim3(BLOCK), 0, st, *g, *o, bk);
+                hipLaunchKernelGGL((k_parabolic_kl_win<T, true>), dim3(g->n_blk), dim3(WBLOCK), 0, st, *g, *o);
             else
-                hipLaunchKernelGGL((k_parabolic_kl<T, false>), dim3(g->n_blk), dim3(BLOCK), 0, st, *g, *o, bk);
+                hipLaunchKernelGGL((k_parabolic_kl_win<T, false>), dim3(g->n_blk), dim3(WBLOCK), 0, st, *g, *o);
         }
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) {

@@ -363,6 +363,9 @@ class DeviceGraph:
         cp = self.cparams(p)
         nat.check(self.lib.gtf_track_state_estimates(ctypes.byref(self.cg_sched), ctypes.byref(self.ctse),
                                                      ctypes.byref(ex), ctypes.byref(cp), self.stream))
+        if self.order is not None:   # per-node outputs in host node order
+            inv = self._inv_order()
+            x = {k: v[inv] for k, v in x.items()}
         return x
 
     # ------------------------------------------ a15: distances between updated states
@@ -393,6 +396,8 @@ class DeviceGraph:
             tr = torch.as_tensor(np.asarray(truth, dtype=np.int64) if not torch.is_tensor(truth) else truth,
                                  device=dev).to(torch.int64).contiguous()
             out["truth"] = torch.empty(max(P, 1), dtype=torch.int8, device=dev)
+        if tr is not None and self.order is not None:
+            tr = tr[torch.from_numpy(self.order).to(dev)].contiguous()   # device node order
         err = torch.zeros(1, dtype=torch.int32, device=dev)
         po = nat.GtfPairOut(vp(out["chi2"]), vp(out["avg_tau"]), vp(out["avg_theta"]), vp(out["delta_theta"]),
                             vp(out.get("truth")), vp(err))
@@ -403,7 +408,17 @@ class DeviceGraph:
         if f:
             raise ValueError("updated-state distances: " +
                              "; ".join(m for b, m in nat.ERR_FLAGS.items() if f & b))
-        return pair_ptr, {k: v[:P] for k, v in out.items()}
+        cols = {k: v[:P] for k, v in out.items()}
+        if self.order is not None and N:   # node segments of pairs in host node order
+            inv = self._inv_order()
+            cnt = counts[:N][inv]
+            hptr = torch.zeros(N + 1, dtype=torch.int64, device=dev)
+            torch.cumsum(cnt, 0, out=hptr[1:])
+            first = torch.repeat_interleave(pair_ptr[:N][inv], cnt, output_size=P)
+            idx = first + (torch.arange(P, device=dev) - torch.repeat_interleave(hptr[:N], cnt, output_size=P))
+            cols = {k: v[idx] for k, v in cols.items()}
+            pair_ptr = hptr
+        return pair_ptr, cols
 
     # ------------------------------------------------------- tag propagation
     def tag_propagation(self, tags, radius, threshold=0.1, max_sweeps=100000):
@@ -415,8 +430,8 @@ class DeviceGraph:
         keep = torch.zeros(max(E, 1), dtype=torch.uint8, device=dev)
         proc = torch.zeros(max(self.n_nodes, 1), dtype=torch.uint8, device=dev)
         cnt = torch.zeros(2, dtype=torch.int32, device=dev)
-        r = torch.from_numpy(np.ascontiguousarray(radius, dtype=np.float64)).to(dev)
-        ta = torch.from_numpy(np.ascontiguousarray(tags, dtype=np.int64)).to(dev)
+        r = torch.from_numpy(np.ascontiguousarray(self._to_dev_nodes(radius), dtype=np.float64)).to(dev)
+        ta = torch.from_numpy(np.ascontiguousarray(self._to_dev_nodes(tags), dtype=np.int64)).to(dev)
         tb = torch.empty_like(ta)
         vp = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
         nat.check(self.lib.gtf_tag_prepare(ctypes.byref(self.cg), vp(r), vp(keep), vp(proc), vp(cnt), self.stream))
@@ -431,7 +446,12 @@ class DeviceGraph:
             flips_hist.append(f)
             frac = f / total if total else 0.0
             ta, tb = tb, ta
-        return ta.cpu().numpy(), flips_hist
+        out = ta.cpu().numpy()
+        if self.order is not None:
+            h = np.empty_like(out)
+            h[self.order] = out
+            out = h
+        return out, flips_hist
 
     # ------------------------------------------------------------ diagnostics
     def set_diagnostics(self, node_err: bool = True, edge_chi2: bool = True, slot_cluster: bool = False):
@@ -506,8 +526,23 @@ class DeviceGraph:
         return g
 
     def _natural_only(self, what):
-        if self.layout != "natural":
-            raise NotImplementedError("%s takes node-indexed host arrays: use layout='natural'" % what)
+        """node-indexed arrays cross these methods in host order: every layout whose node order
+        is a permutation of the host's maps them (the padded layout's dummy nodes do not)"""
+        if self.layout == "padded":
+            raise NotImplementedError("%s takes node-indexed host arrays: not with layout='padded'" % what)
+
+    def _to_dev_nodes(self, a):
+        """a host-order per-node array (numpy) in device node order"""
+        a = np.asarray(a)
+        return a if self.order is None else a[self.order]
+
+    def _inv_order(self):
+        """device tensor: host node h -> device node"""
+        if getattr(self, "_inv_t", None) is None:
+            inv = np.empty(self.order.size, np.int64)
+            inv[self.order] = np.arange(self.order.size)
+            self._inv_t = self.torch.from_numpy(inv).to(self.device)
+        return self._inv_t
 
     # arrays whose values decide how much work the next pass does: restoring
     # them makes every benchmark step process the same input

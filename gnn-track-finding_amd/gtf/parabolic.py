@@ -27,6 +27,7 @@ from . import _native as nat
 from .graph import TrackGraph
 
 BUCKETS = ((1, 2), (3, 4), (5, 8), (9, 1 << 30))   # in-degree ranges of the 1/4/8/64-lane groups
+TILE_MAX = 256   # nodes per tile of the tiled layout (gtf_kl.hip WTILE)
 
 
 def _ptr(t):
@@ -63,7 +64,7 @@ class ParabolicKL:
     into L2, instead of reaching across the whole batch."""
 
     def __init__(self, slot_ptr, slot_src, gnn, truth=None, device="cuda", with_single=False, ordered=False,
-                 tile=0):
+                 tile=0, sort_window=8192):
         slot_ptr = np.ascontiguousarray(slot_ptr, np.int32)
         self.n_nodes = int(slot_ptr.shape[0] - 1)
         self.n_slots = int(slot_ptr[-1])
@@ -79,9 +80,16 @@ class ParabolicKL:
             rank = np.full(d.size, len(keys), np.int64)
             for q in reversed(range(len(keys))):
                 rank[keys[q]] = q
-            if self.tile > 0:   # bucket order inside each tile of consecutive nodes
-                tid = np.arange(d.size, dtype=np.int64) // self.tile
-                order = np.lexsort((np.arange(d.size), rank, tid))
+            if self.tile > 0:   # azimuth order in sort windows, cut into tiles, buckets inside a tile
+                if not 0 < self.tile <= TILE_MAX:
+                    raise ValueError("tile must be in 1..%d" % TILE_MAX)
+                xy = np.asarray(gnn, np.float64).reshape(-1, 4)
+                phi = np.arctan2(xy[:, 1], xy[:, 0])
+                idx = np.arange(d.size, dtype=np.int64)
+                o1 = np.lexsort((idx, phi, idx // sort_window))
+                tid = np.empty(d.size, np.int64)
+                tid[o1] = np.arange(d.size) // self.tile
+                order = np.lexsort((np.argsort(o1), rank, tid))
                 self._tiles = (tid[order], rank[order])
             else:
                 order = np.argsort(rank, kind="stable")
@@ -123,7 +131,7 @@ class ParabolicKL:
         if self.tile > 0:   # one block record per wavefront (gtf_kl_graph.blk)
             blk = self._block_table(d, pair_ptr)
             self.blk = t(blk)
-            self.n_blk = int(blk.size // 8)
+            self.n_blk = int(blk.size // 12)
             self._g = nat.GtfKlGraph(self.n_nodes, self.n_slots, _ptr(self.slot_ptr), _ptr(self.slot_src),
                                      _ptr(self.gnn), _ptr(self.truth), _ptr(self.pair_ptr),
                                      (ctypes.c_void_p * 4)(), (ctypes.c_int32 * 4)(), (ctypes.c_int32 * 4)(), 0, 2,
@@ -142,31 +150,24 @@ class ParabolicKL:
                                      (ctypes.c_void_p * 4)(*[x.data_ptr() if x.numel() else None for x in self.lists]),
                                      (ctypes.c_int32 * 4)(*[x.numel() for x in self.lists]), gnn_stride=2)
 
-    def _block_table(self, d, pair_ptr, block=64):
-        """gtf_kl_graph.blk of the tiled layout: per tile (in node order) the blocks of its
-        > 8-edge nodes (one per block), 5..8-edge nodes (8 per block), 3..4-edge nodes (64)
-        and one- / two-edge nodes (64; one-edge first), each record (q, first node, count,
-        one-edge count, first slot, first pair lo / hi, 0)"""
+    def _block_table(self, d, pair_ptr):
+        """gtf_kl_graph.blk of the tiled layout: one record of 12 int32 per tile (first node,
+        bucket-0 count, its one-edge count, bucket 1 / 2 / 3 counts, bucket 0's first slot,
+        its first pair lo / hi, the window [previous tile's first node, next tile's end), 0)"""
         tid, rank = self._tiles
         sp = self.slot_ptr_host
-        recs = []
         nt = int(tid.max()) + 1 if tid.size else 0
         bounds = np.searchsorted(tid, np.arange(nt + 1))
+        recs = np.zeros((nt, 12), np.int64)
         for t_ in range(nt):
             a, b = int(bounds[t_]), int(bounds[t_ + 1])
-            r = rank[a:b]
-            cut = a + np.searchsorted(r, np.arange(7))      # rank runs inside the tile
-            for q, (r0, r1), per in ((3, (4, 5), 1), (2, (3, 4), block // 8), (1, (2, 3), block), (0, (0, 2), block)):
-                s0, s1 = int(cut[r0]), int(cut[r1])
-                n1_all = int(cut[1] - cut[0]) if q == 0 else 0
-                for v0 in range(s0, s1, per):
-                    cnt = min(per, s1 - v0)
-                    n1 = max(0, min(cnt, n1_all - (v0 - s0))) if q == 0 else 0
-                    pr = int(pair_ptr[v0 + n1]) if q == 0 and n1 < cnt else 0
-                    recs.append((q, v0, cnt, n1, int(sp[v0]) if q == 0 else 0, pr & 0xFFFFFFFF, pr >> 32, 0))
-        a = np.asarray(recs, np.int64).reshape(-1, 8)
-        a[:, 5] = np.where(a[:, 5] >= 2**31, a[:, 5] - 2**32, a[:, 5])   # the low word as int32 bits
-        return a.astype(np.int32).reshape(-1)
+            cut = a + np.searchsorted(rank[a:b], np.arange(6))      # rank runs inside the tile
+            n1, n0 = int(cut[1] - cut[0]), int(cut[2] - cut[0])
+            pr = int(pair_ptr[a + n1]) if n1 < n0 else 0
+            recs[t_] = (a, n0, n1, cut[3] - cut[2], cut[4] - cut[3], cut[5] - cut[4], sp[a],
+                        pr & 0xFFFFFFFF, pr >> 32, bounds[max(t_ - 1, 0)], bounds[min(t_ + 2, nt)], 0)
+        recs = np.where(recs >= 2**31, recs - 2**32, recs)   # low words as int32 bits
+        return recs.astype(np.int32).reshape(-1)
 
     def replica(self, gnn=None):
         """An independent copy of this batch in its own device buffers (same structure):

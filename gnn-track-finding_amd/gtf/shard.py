@@ -119,18 +119,26 @@ class ShardPlan:
         own = own[np.diff(g.out_ptr.astype(np.int64))[own] > 0]
         return np.unique(np.concatenate([halo.astype(np.int64), own])).astype(np.int32)
 
-    def schedule(self, r: int):
+    def schedule(self, r: int, widen: int = 0):
         """(sched, [n_g4, n_g8, n_g16, n_g32, n_g64], n_big, n_g2) of the owned receivers:
-        slot-count buckets in node order, the <= 2-slot nodes first in the <= 4 bucket"""
+        slot-count buckets in node order, the <= 2-slot nodes first in the <= 4 bucket.
+        widen = k > 0: every node in the bucket k sizes up (2**k times the lanes, capped at
+        64; no 2-lane groups) -- a rank's small share then runs each node's op chain on more
+        lanes (fewer pair rounds) where the GPU has lanes to spare"""
         deg = np.diff(self._g.slot_ptr.astype(np.int64))
         idx = np.arange(self.node_lo[r], self.node_hi[r], dtype=np.int32)
         d = deg[idx]
-        buckets = [idx[(d >= lo) & (d <= hi)] for lo, hi in BUCKETS]
+        q = np.full(d.size, -1, np.int64)
+        for j, (lo, hi) in enumerate(BUCKETS):
+            q[(d >= lo) & (d <= hi)] = j
+        q = np.where(q >= 0, np.minimum(q + widen, len(BUCKETS) - 1), -1)
+        buckets = [idx[q == j] for j in range(len(BUCKETS))]
         d0 = deg[buckets[0]]
-        buckets[0] = np.concatenate([buckets[0][d0 <= 2], buckets[0][d0 > 2]])
+        n2 = int((d0 <= 2).sum()) if widen == 0 else 0
+        if widen == 0:
+            buckets[0] = np.concatenate([buckets[0][d0 <= 2], buckets[0][d0 > 2]])
         big = idx[d > 64]
-        return (np.concatenate(buckets + [big]).astype(np.int32), [int(b.size) for b in buckets], int(big.size),
-                int((d0 <= 2).sum()))
+        return (np.concatenate(buckets + [big]).astype(np.int32), [int(b.size) for b in buckets], int(big.size), n2)
 
     def sender_schedule(self, r: int):
         """the rank's senders as (u, out_ptr[u], out_ptr[u+1], 0) quadruples bucketed by
@@ -233,7 +241,7 @@ class ShardedDeviceGraph:
     pass for its receivers and exchanges the halo with the other ranks after each pass."""
 
     def __init__(self, g: TrackGraph, rank: int, world: int, device="cuda", backend="nccl", group=None,
-                 tile: int = None):
+                 tile: int = None, widen: int = None):
         import torch
         from .device import DeviceGraph, TILE, sched_segments, sender_lanes
         self.torch = torch
@@ -249,7 +257,10 @@ class ShardedDeviceGraph:
         vp = lambda t: ctypes.c_void_p(t.data_ptr() if t.numel() else 0)  # noqa: E731
         pl = self.plan
         self.senders = up(pl.senders(rank))
-        sched, n_g, n_big, n_g2 = pl.schedule(rank)
+        if widen is None:
+            import os
+            widen = int(os.environ.get("GTF_SHARD_WIDEN", "0"))
+        sched, n_g, n_big, n_g2 = pl.schedule(rank, widen)
         self.sched = up(sched)
         self.sched_seg = up(sched_segments(gd.slot_ptr, sched))
         osched, n_o = pl.sender_schedule(rank)

@@ -462,14 +462,13 @@ typedef struct gtf_kl_graph {
                                  the kernel reads only x and y, so half the gathered bytes) */
     int64_t slot0;
     int64_t pair0;
-    /* tiled layout (gtf.parabolic.ParabolicKL(tile=T)): nodes in tiles of consecutive nodes,
-     * each tile ordered by bucket like the ordered layout, so a node's neighbours -- the
-     * same event's hits -- sit in its own tile and the neighbour gathers hit the L2 the
-     * tile's own reads filled. One record of 8 int32 per block (one wavefront):
-     * (bucket q, first node, node count, one-edge nodes among them (q = 0), first slot
-     * (q = 0), first pair (q = 0, low and high 32 bits), 0); a block takes count <= 64
-     * nodes of one tile's bucket q (8 per block for q = 2, 1 for q = 3). blk != NULL
-     * overrides list / first / count. The blocks run in XCD-contiguous order. */
+    /* tiled layout (gtf.parabolic.ParabolicKL(tile=T)): the nodes in tiles of <= 256 consecutive
+     * nodes cut from an azimuth-sorted order, each tile ordered by bucket (one- then two-edge,
+     * 3..4, 5..8, > 8 in-edges, then the unlisted nodes). One block per tile record of 12 int32:
+     * (first node, bucket-0 count, its one-edge count, bucket 1 / 2 / 3 counts, bucket 0's first
+     * slot, its first pair low / high 32 bits, window [lo, hi) of at most 768 nodes holding the
+     * tile's neighbours, 0); the block copies the window's x, y and truth ids into LDS and reads
+     * the neighbours there. blk != NULL overrides list / first / count. */
     const int32_t* blk;       /* [8 * n_blk] or NULL */
     int32_t n_blk;
     int32_t pad_blk_;

@@ -271,3 +271,36 @@ def test_sharded_pass_equals_single_gpu_pass():
         for f in ("has_merged", "merged_state", "merged_cov"):
             assert np.array_equal(res[r]["replica"][f], ref.node[f], equal_nan=True), (r, f)
         assert np.array_equal(res[r]["act"], ref.slot["act"]), r
+
+
+@pytest.mark.parametrize("widen", [1, 2, 5])
+def test_widened_schedule_covers_every_receiver_once(widen):
+    g = _event()
+    pl = ShardPlan(g, 3)
+    deg = np.diff(g.slot_ptr)
+    sizes = (4, 8, 16, 32, 64)
+    for r in range(3):
+        sched, n_g, n_big, n_g2 = pl.schedule(r, widen)
+        assert sorted(sched.tolist()) == list(range(pl.node_lo[r], pl.node_hi[r])) and n_g2 == 0
+        at = 0
+        for G, n in zip(sizes, n_g):
+            assert (deg[sched[at:at + n]] <= G).all()     # every node fits its group
+            at += n
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("widen", [1, 2])
+def test_widened_shard_pass_equals_single_gpu_pass(widen):
+    """one rank (no exchange) with every node on 2x / 4x the lanes: the pass is the same
+    bit for bit"""
+    from gtf.params import Params
+    from gtf.shard import ShardedDeviceGraph
+    g, ref = _reference_passes()
+    sd = ShardedDeviceGraph(g, 0, 1, "cuda:0", backend="gloo", tile=256, widen=widen)
+    for _ in range(PASSES):
+        sd.step(Params())
+    h = sd.d.download(g.copy())
+    for f in OUT_NODE:
+        assert np.array_equal(h.node[f], ref.node[f], equal_nan=True), f
+    for f in OUT_SLOT:
+        assert np.array_equal(h.slot[f], ref.slot[f], equal_nan=h.slot[f].dtype.kind == "f"), f

@@ -1,4 +1,4 @@
-"""GPU box: one rank's share of the edge-sharded C4 pass at N = 1, 2, 4, 8 on one GPU
+"""GPU box (GTF_SHARD_WIDEN=k: the widened lane-group schedule): one rank's share of the edge-sharded C4 pass at N = 1, 2, 4, 8 on one GPU
 (rank 0's wedge; no exchange): device time per pass (events around K back-to-back
 passes) and host time per pass_() call -- the compute side of the N > 1 bench step."""
 import os

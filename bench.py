@@ -168,7 +168,7 @@ def dropin_stage_wall(params, reps=3):
                 "input": "vol-7 134 full load", "subgraphs": len(graphs), "edges": edges,
                 "wall_s": med["wall_s"], "edges_per_s": edges / med["wall_s"], "workers": med["workers"],
                 "read_pack_s": med["read_pack_s"], "device_s": med["device_s"],
-                "unpack_write_s": med["unpack_write_s"],
+                "unpack_write_s": med["unpack_write_s"], "worker_max_s": med.get("worker_max_s"),
                 "reference_as_is_edges_per_s": 788, "reference_prints_stubbed_edges_per_s": 5367}
     finally:
         shutil.rmtree(tmp, ignore_errors=True)

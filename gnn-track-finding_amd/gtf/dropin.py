@@ -105,6 +105,11 @@ def run_dir(input_dir: str, output_dir: str, body: Callable, *, states=("tse", "
     files = glob.glob(input_dir + "*" + SUBGRAPH_SUFFIX)        # the reference's glob order
     workers = workers or default_workers()
     chunks = _chunks(len(files), workers)
+    if files:
+        # import what the pickles need (networkx, GNN_Measurement) here, once, before the
+        # fork: otherwise every worker imports networkx (~0.2 s) on its first load
+        with open(files[0], "rb") as fh:
+            pickle.load(fh)
     ctx = mp.get_context("fork")   # no exec: this process may hold the GPU (bench)
     procs, conns = [], []
     for lo, hi in chunks:

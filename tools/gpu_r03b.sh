@@ -1,8 +1,7 @@
 #!/bin/bash
 # round 3: GPU suite (incl. the 800' real-data parity and the sharded C4 test), then the
 # rocprofv3 kernel trace of the default bench, PMC passes of the C4 pass and of the cold
-# config-5 rotation, one bench line, and (if the profiler offers it) PC sampling of the
-# C4 pass loop. Stops at the first failing GPU step.
+# config-5 rotation, one bench line, . Stops at the first failing GPU step.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=gpurun_out/r03b
@@ -18,7 +17,3 @@ for i in 1 2; do
   GTF_NO_OUTIDX=1 timeout -k 10 120 python tools/pass_loop.py 150 >> $O/ab_outidx.jsonl || exit 1
   timeout -k 10 120 python tools/pass_loop.py 150 >> $O/ab_outidx.jsonl || exit 1
 done
-cd /tmp && export TMPDIR=/tmp
-timeout -k 10 60 rocprofv3 -L > $R/$O/rocprof_list.txt 2>&1
-timeout -k 10 120 rocprofv3 --pc-sampling-beta-enabled --pc-sampling-method stochastic --pc-sampling-unit cycles --pc-sampling-interval 65536 -d $R/$O/pcs -o run --output-format csv -- python3 $R/tools/pass_loop.py 200 > $R/$O/pcs.log 2>&1
-echo pcs rc $?

@@ -1,5 +1,5 @@
 """GPU box (GTF_SHARD_WIDEN=k: the widened lane-group schedule): one rank's share of the edge-sharded C4 pass at N = 1, 2, 4, 8 on one GPU
-(rank 0's wedge; no exchange): device time per pass (events around K back-to-back
+(rank 0's wedge; no exchange; argv: the world sizes, default 1 2 4 8): device time per pass (events around K back-to-back
 passes) and host time per pass_() call -- the compute side of the N > 1 bench step."""
 import os
 import sys
@@ -16,7 +16,8 @@ from gtf.shard import ShardedDeviceGraph  # noqa: E402
 g = synth.workload("c4", seed=0)
 p = Params()
 K = 50
-for world in (1, 2, 4, 8):
+worlds = [int(a) for a in sys.argv[1:]] or [1, 2, 4, 8]
+for world in worlds:
     sd = ShardedDeviceGraph(g, 0, world, "cuda:0", backend="gloo")
     snap = sd.d.snapshot(DeviceGraph.PASS_INPUTS)
     sd.d.stage_inputs(K)

@@ -484,7 +484,31 @@ def bench_sharded(workload, rank, world, dev, steps, warmup, params, backend="nc
 # the fused node kernel: priors, side norm, reweights, update and KL clustering of every
 # receiver in one launch (gtf_pass.hip run_pass)
 NODE_KERNEL = "k_node_multi<update+cluster> (KL-distance kernel)"
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02_v5", "pmc_c4.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r03", "c4", "pmc_c4.json")
+# per-launch SQ instruction counters of the pass kernels (tools/gpu_sqmix.sh, same event)
+SQ_SUMMARY = os.path.join(ROOT, "profiles", "r03", "sqmix", "sqmix.json")
+SQ_NAMES = {"k_sender+k_extrapolate": ("k_sender_sched", "k_extrapolate"),
+            NODE_KERNEL: ("k_node_multi<11, 1, 3, 4, 3, 4, 5, 6, 2, 3, 4, 10, 5, 8, 3>",)}
+
+
+def committed_valu(kernel, ms, workload, layout, tile):
+    """The VALU-issue roofline of `kernel` beside the HBM one: the committed SQ counters'
+    VALU instructions per launch at full issue rate on every SIMD (gtf.roofline
+    valu_issue_floor_s) against the measured launch time; None off the profiled C4 config."""
+    from gtf import roofline as rf
+    if (workload, layout, tile) != ("c4", "tiled", 4096) or kernel not in SQ_NAMES:
+        return None
+    try:
+        with open(SQ_SUMMARY) as f:
+            allc = json.load(f)
+        cs = [allc[n] for n in SQ_NAMES[kernel]]
+    except (OSError, KeyError, ValueError):
+        return None
+    floor = sum(rf.valu_issue_floor_s(c) for c in cs)
+    return {"bound": "valu_issue", "valu_insts_per_launch": sum(c["SQ_INSTS_VALU"] for c in cs),
+            "f64_insts_per_launch": sum(c.get(k, 0.0) for c in cs for k in rf.F64_COUNTERS),
+            "issue_floor_us": floor * 1e6, "frac": floor / (ms * 1e-3),
+            "source": os.path.relpath(SQ_SUMMARY, ROOT)}
 
 
 def committed_traffic(workload, kernel, layout, tile, edges, nodes):
@@ -681,7 +705,9 @@ def main():
                       "frac": v[1] / (v[0] * 1e-3) / 1e9 / rf.HBM_PEAK_GBS,
                       "builder_model_bytes": builder.get(k),
                       "builder_model_frac": builder[k] / (v[0] * 1e-3) / 1e9 / rf.HBM_PEAK_GBS if k in builder else None,
-                      "traffic_bytes": committed_traffic(args.workload, k, args.layout, args.tile, g.n_edges, g.n_nodes)} for k, v in cands.items()}
+                      "traffic_bytes": committed_traffic(args.workload, k, args.layout, args.tile, g.n_edges, g.n_nodes),
+                      "valu_roofline": committed_valu(k, v[0], args.workload, args.layout, args.tile)}
+                  for k, v in cands.items()}
     achieved = nbytes / (ms * 1e-3) / 1e9
     traffic = committed_traffic(args.workload, name, args.layout, args.tile, g.n_edges, g.n_nodes)
     pass_b = rf.pass_bytes(g.n_edges, g.n_nodes)
@@ -742,7 +768,8 @@ def main():
                          "kl_eligible_nodes": int(elig.sum()), "kl_eligible_in_edges": e_elig,
                          "byte_model": "SURVEY §8d (fused node kernel 89 B/edge + 186 B/node)",
                          "builder_model_bytes_per_launch": builder.get(name),
-                         "builder_model_frac": per_kernel[name]["builder_model_frac"]},
+                         "builder_model_frac": per_kernel[name]["builder_model_frac"],
+                         "valu_roofline": per_kernel[name]["valu_roofline"]},
             "pass_roofline": {"bound": "hbm", "algorithmic_bytes_per_step": pass_b,
                               "byte_model": "SURVEY §8d B_alg = 183 E + 290 N",
                               "achieved": pass_b / (elapsed / K) / 1e9, "peak": rf.HBM_PEAK_GBS, "unit": "GB/s",

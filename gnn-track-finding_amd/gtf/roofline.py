@@ -74,3 +74,21 @@ def pass_bytes(n_edges, n_nodes):
 def parabolic_kl_bytes(n_nodes, n_listed, n_slots, n_pairs, dtype="f64"):
     return (PKL_PER_NODE * n_nodes + PKL_PER_LISTED * n_listed + PKL_PER_SLOT * n_slots
             + PKL_PER_PAIR[dtype] * n_pairs)
+
+
+# VALU issue roofline (the bound of the fp64 node-local work beside HBM): gfx950 has 256
+# CUs x 4 SIMDs at ~2.4 GHz; a wave64 VALU instruction issues in 2 cycles on a 32-lane
+# SIMD (MI355X_MICROARCH.md), an fp64 add / mul / fma / transcendental in 4 (fp64 runs at
+# half the fp32 lane rate: 78.6 TFLOP/s).
+SIMDS, CLOCK_HZ = 1024, 2.4e9
+VALU_CYC, VALU_F64_CYC = 2, 4
+F64_COUNTERS = ("SQ_INSTS_VALU_ADD_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_FMA_F64",
+                "SQ_INSTS_VALU_TRANS_F64")
+
+
+def valu_issue_floor_s(counters: dict) -> float:
+    """Seconds the launch's VALU instructions need at full issue rate on every SIMD, from
+    its SQ counters (per launch): fp64 instructions at 4 cycles, every other at 2."""
+    f64 = sum(float(counters.get(k, 0.0)) for k in F64_COUNTERS)
+    other = float(counters["SQ_INSTS_VALU"]) - f64
+    return (f64 * VALU_F64_CYC + other * VALU_CYC) / (SIMDS * CLOCK_HZ)

@@ -140,8 +140,9 @@ def dropin_stage_wall(params, reps=3):
     drop-in runner gtf.dropin.run_dir: the per-file pickle reading / packing and unpacking /
     writing on worker processes, message passing + priors / reweight x2 + degree in one
     device call), on the full-load volume-7 134 network (14,766 directed edges), median of
-    reps. Timed in a fresh child process (python -m gtf.dropin), whose workers fork before
-    it touches the GPU; interpreter start and imports excluded, worker start-up included.
+    reps after the first. Timed in a fresh child process (python -m gtf.dropin), whose
+    worker pool forks before it touches the GPU; interpreter start and imports excluded;
+    the first directory's wall time (pool start-up, GPU context) reported beside.
     BASELINE.md times the reference's own stage on this input at 788 edges/s as is
     (18.7 s) and 5,367 edges/s with its prints stubbed."""
     import shutil
@@ -162,13 +163,18 @@ def dropin_stage_wall(params, reps=3):
                            capture_output=True, text=True, timeout=600)
         if r.returncode != 0:
             return {"error": r.stderr[-400:]}
-        runs = json.loads(r.stdout)["runs"]
+        out = json.loads(r.stdout)
+        runs = out["runs"]
         med = sorted(runs, key=lambda x: x["wall_s"])[len(runs) // 2]
         return {"stage": "extrapolate (drop-in runner gtf.dropin.run_dir, child process)",
                 "input": "vol-7 134 full load", "subgraphs": len(graphs), "edges": edges,
                 "wall_s": med["wall_s"], "edges_per_s": edges / med["wall_s"], "workers": med["workers"],
                 "read_pack_s": med["read_pack_s"], "device_s": med["device_s"],
                 "unpack_write_s": med["unpack_write_s"], "worker_max_s": med.get("worker_max_s"),
+                "device_phases_s": med.get("device_phases_s"),
+                "first_run_wall_s": out["first"]["wall_s"],
+                "first_run_note": "the first directory of the process: forks the worker pool (after importing "
+                                  "what the pickles need), creates the GPU context, loads code; the CLI's case",
                 "reference_as_is_edges_per_s": 788, "reference_prints_stubbed_edges_per_s": 5367}
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
@@ -340,7 +346,36 @@ def bench_components(g, params, dev, reps=5):
     d.raise_errors()
     del d
     out["f_pipeline_vol7"] = bench_pipeline_vol7(params, dev)
+    out["f2_event_build_c4"] = bench_event_build(g, dev)
     return out
+
+
+def bench_event_build(g, dev, reps=3):
+    """SURVEY §8f #2 on a C4-sized edge list: the event's undirected edges as shuffled CSV
+    rows with random 40-bit node ids, built into the packed CSR by the host builder
+    (gtf_build_event_csr, C++) and on the GPU (gtf_build_event_csr_device; the call
+    includes uploading the columns and downloading the arrays), the same arrays bit for bit
+    (tests/test_gpu_build.py). Median of reps after a first call."""
+    from gtf import io
+    rng = np.random.default_rng(5)
+    dst = np.repeat(np.arange(g.n_nodes), np.diff(g.slot_ptr))
+    src = g.slot["slot_src"]
+    keep = (src >= 0) & (src < dst)
+    a, b = src[keep], dst[keep]
+    perm = rng.permutation(a.size)
+    ids = rng.choice(2 ** 40, size=g.n_nodes, replace=False).astype(np.int64)
+    a, b = ids[a[perm]], ids[b[perm]]
+    res = {"nodes": int(g.n_nodes), "rows": int(a.size)}
+    for name, device in (("host_cpp_s", None), ("device_s", dev)):
+        ts = []
+        for _ in range(reps + 1):
+            t0 = time.perf_counter()
+            o, e, nsub = io.csr_from_rows(ids, a, b, device)
+            ts.append(time.perf_counter() - t0)
+        res[name] = float(np.median(ts[1:]))
+        res["directed_edges"], res["subgraphs"] = e, nsub
+    res["speedup"] = res["host_cpp_s"] / res["device_s"]
+    return res
 
 
 def bench_pipeline_vol7(params, dev):

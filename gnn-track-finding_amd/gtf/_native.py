@@ -144,6 +144,7 @@ SYMBOLS = ["gtf_workspace_bytes", "gtf_clear_errors", "gtf_read_errors", "gtf_ex
            "gtf_shard_chunk_bytes", "gtf_shard_pack", "gtf_shard_unpack", "gtf_halo_pack", "gtf_halo_unpack",
            "gtf_extract_workspace_bytes",
            "gtf_extract_candidates", "gtf_build_event_csr", "gtf_candidate_order",
+           "gtf_build_event_device_workspace_bytes", "gtf_build_event_csr_device",
            "gtf_updated_state_pair_counts", "gtf_updated_state_distances", "gtf_set_diagnostics",
            "gtf_last_error",
            "gtf_version"]
@@ -198,6 +199,9 @@ def lib():
     L.gtf_track_state_estimates.argtypes = [G, S, ctypes.POINTER(GtfTseExtra), PR, P]
     L.gtf_parabolic_kl.argtypes = [ctypes.POINTER(GtfKlGraph), I32, ctypes.POINTER(GtfKlOut), P]
     L.gtf_build_event_csr.argtypes = [ctypes.POINTER(GtfEventCsr)]
+    L.gtf_build_event_device_workspace_bytes.restype = ctypes.c_size_t
+    L.gtf_build_event_device_workspace_bytes.argtypes = [ctypes.c_int64, ctypes.c_int64]
+    L.gtf_build_event_csr_device.argtypes = [ctypes.POINTER(GtfEventCsr), P, ctypes.c_size_t, P]
     L.gtf_candidate_order.argtypes = [ctypes.POINTER(GtfCandidateGraph), P]
     L.gtf_updated_state_pair_counts.argtypes = [G, N, S, E, P, P]
     L.gtf_updated_state_distances.argtypes = [G, N, S, E, P, P, ctypes.POINTER(GtfPairOut), P]
@@ -208,7 +212,7 @@ def lib():
                "gtf_tag_prepare", "gtf_tag_sweep", "gtf_parabolic_kl", "gtf_track_state_estimates", "gtf_pass_shard", "gtf_shard_pack",
                "gtf_shard_unpack", "gtf_halo_pack", "gtf_halo_unpack", "gtf_extract_candidates", "gtf_build_event_csr",
                "gtf_candidate_order", "gtf_updated_state_pair_counts", "gtf_updated_state_distances",
-               "gtf_set_diagnostics"):
+               "gtf_set_diagnostics", "gtf_build_event_csr_device"):
         getattr(L, fn).restype = ctypes.c_int
     _lib = L
     return L

@@ -17,7 +17,8 @@ time"). Here the files are split into contiguous chunks, one per worker process:
 
 Subgraphs are independent (no edge crosses two of them), so the concatenated stage
 equals the stage on all subgraphs together: same values, same file numbering. The
-workers are forked before this process initialises the GPU and never touch it; only
+workers are a pool forked once per process, at its first directory (in a CLI before the
+GPU is initialised), and reused by later directories; they never touch the GPU, and only
 numpy arrays cross the pipes. Reference exceptions raised on the device are re-raised
 as the reference's exception class before any output is written (the reference loses
 the stage's output too).
@@ -55,43 +56,112 @@ def _chunks(n_files: int, workers: int):
     return [(int(bounds[i]), int(bounds[i + 1])) for i in range(w)]
 
 
-def _worker(conn, files, first_index, out_dir, states, merged):
-    """read + pack, wait for the stage's arrays, unpack + write"""
+def _job(conn, files, first_index, out_dir, states, merged):
+    """one directory share: read + pack, wait for the stage's arrays, unpack + write"""
+    t = [time.perf_counter()]
+    subs = []
+    for f in files:
+        with open(f, "rb") as fh:
+            subs.append(pickle.load(fh))
+    t.append(time.perf_counter())
+    g = pack(subs)
+    t.append(time.perf_counter())
+    conn.send(g)
+    t.append(time.perf_counter())
+    msg = conn.recv()
+    t.append(time.perf_counter())
+    if msg is None:            # the stage raised: write nothing
+        conn.send(("ok", 0, {}))
+        return
+    node, slot = msg
+    g.node.update(node)
+    g.slot.update(slot)
+    if g.n_nodes:
+        unpack(g, subs, states=states, merged=merged)
+    t.append(time.perf_counter())
+    for i, s in enumerate(subs):
+        with open(os.path.join(out_dir, "%d%s" % (first_index + i, SUBGRAPH_SUFFIX)), "wb") as fh:
+            pickle.dump(s, fh, pickle.HIGHEST_PROTOCOL)
+    t.append(time.perf_counter())
+    d = np.diff(t)
+    conn.send(("ok", len(subs), {"start": t[0], "load": d[0], "pack": d[1], "send": d[2], "wait": d[3],
+                                 "unpack": d[4], "dump": d[5]}))
+
+
+def _serve(conn):
+    """a pool worker: one job (a directory share) after another until None"""
     import gc
     gc.disable()    # the pickles are trees of many small objects: no cycles to collect here (2-3x faster loads)
-    try:
-        t = [time.perf_counter()]
-        subs = []
-        for f in files:
-            with open(f, "rb") as fh:
-                subs.append(pickle.load(fh))
-        t.append(time.perf_counter())
-        g = pack(subs)
-        t.append(time.perf_counter())
-        conn.send(g)
-        t.append(time.perf_counter())
-        msg = conn.recv()
-        t.append(time.perf_counter())
-        if msg is None:            # the stage raised: write nothing
-            conn.send(("ok", 0, {}))
+    while True:
+        job = conn.recv()
+        if job is None:
             return
-        node, slot = msg
-        g.node.update(node)
-        g.slot.update(slot)
-        if g.n_nodes:
-            unpack(g, subs, states=states, merged=merged)
-        t.append(time.perf_counter())
-        for i, s in enumerate(subs):
-            with open(os.path.join(out_dir, "%d%s" % (first_index + i, SUBGRAPH_SUFFIX)), "wb") as fh:
-                pickle.dump(s, fh, pickle.HIGHEST_PROTOCOL)
-        t.append(time.perf_counter())
-        d = np.diff(t)
-        conn.send(("ok", len(subs), {"start": t[0], "load": d[0], "pack": d[1], "send": d[2], "wait": d[3],
-                                     "unpack": d[4], "dump": d[5]}))
-    except BaseException as e:     # reported to the main process
-        conn.send(("error", repr(e)))
-    finally:
-        conn.close()
+        try:
+            _job(conn, *job)
+        except BaseException as e:     # reported to the main process, which drops the pool
+            conn.send(("error", repr(e)))
+            return
+        gc.collect()    # the job's graphs (networkx views hold cycles), after its reply
+
+
+class _Pool:
+    """Worker processes forked once per process, at the first directory: in a drop-in CLI
+    before this process initialises the GPU (forking a process that holds a GPU context
+    costs ~10 ms per worker, and the COW-shared pages slow its later host-to-device
+    copies), and reused by every later directory of a long-running caller."""
+
+    def __init__(self, n, warm_file):
+        import multiprocessing as mp
+        if warm_file:
+            # import what the pickles need (networkx, GNN_Measurement) here, once, before the
+            # fork: otherwise every worker imports networkx (~0.2 s) on its first load
+            with open(warm_file, "rb") as fh:
+                pickle.load(fh)
+        ctx = mp.get_context("fork")   # no exec: this process may hold the GPU
+        self.n, self.procs, self.conns = n, [], []
+        for _ in range(n):
+            a, b = ctx.Pipe()
+            p = ctx.Process(target=_serve, args=(b,), daemon=True)
+            p.start()
+            b.close()
+            self.procs.append(p)
+            self.conns.append(a)
+
+    def alive(self):
+        return all(p.is_alive() for p in self.procs)
+
+    def close(self):
+        for c in self.conns:
+            try:
+                c.send(None)
+                c.close()
+            except OSError:
+                pass
+        for p in self.procs:
+            p.join(10)
+            if p.is_alive():
+                p.kill()
+
+
+_POOL = None
+
+
+def _get_pool(n, warm_file):
+    global _POOL
+    if _POOL is not None and (_POOL.n != n or not _POOL.alive()):
+        _drop_pool()
+    if _POOL is None:
+        import atexit
+        _POOL = _Pool(n, warm_file)
+        atexit.register(_drop_pool)
+    return _POOL
+
+
+def _drop_pool():
+    global _POOL
+    if _POOL is not None:
+        _POOL.close()
+        _POOL = None
 
 
 def run_dir(input_dir: str, output_dir: str, body: Callable, *, states=("tse", "uts"), merged=True,
@@ -100,26 +170,15 @@ def run_dir(input_dir: str, output_dir: str, body: Callable, *, states=("tse", "
     stage's device calls (e.g. ``lambda d: d.extrapolate(p)``). Returns counts and the
     host / device split of the wall time. ``host_stage(TrackGraph) -> flags`` replaces the
     device (tests run the CPU checker through the same worker machinery)."""
-    import multiprocessing as mp
     t0 = time.perf_counter()
     files = glob.glob(input_dir + "*" + SUBGRAPH_SUFFIX)        # the reference's glob order
     workers = workers or default_workers()
     chunks = _chunks(len(files), workers)
-    if files:
-        # import what the pickles need (networkx, GNN_Measurement) here, once, before the
-        # fork: otherwise every worker imports networkx (~0.2 s) on its first load
-        with open(files[0], "rb") as fh:
-            pickle.load(fh)
-    ctx = mp.get_context("fork")   # no exec: this process may hold the GPU (bench)
-    procs, conns = [], []
-    for lo, hi in chunks:
-        a, b = ctx.Pipe()
-        p = ctx.Process(target=_worker, args=(b, files[lo:hi], lo, output_dir, states, merged), daemon=True)
-        p.start()
-        b.close()
-        procs.append(p)
-        conns.append(a)
+    pool = _get_pool(workers, files[0] if files else None)
+    conns = pool.conns[:len(chunks)]
     try:
+        for c, (lo, hi) in zip(conns, chunks):
+            c.send((files[lo:hi], lo, output_dir, tuple(states), merged))
         from multiprocessing.connection import wait
         parts = [None] * len(conns)
         pending = {c: i for i, c in enumerate(conns)}
@@ -133,19 +192,26 @@ def run_dir(input_dir: str, output_dir: str, body: Callable, *, states=("tse", "
         nonempty = [g for g in parts if g.n_nodes]
         flags = 0
         out_node, out_slot = None, None
+        phases = {}
         if nonempty and host_stage is not None:
             g = concat(nonempty)
             flags = int(host_stage(g) or 0)
             out_node, out_slot = g.node, g.slot
         elif nonempty:
             from .device import DeviceGraph
+            tp = [time.perf_counter()]
             g = concat(nonempty)
+            tp.append(time.perf_counter())
             d = DeviceGraph(g)
+            tp.append(time.perf_counter())
             d.clear_errors()
             body(d)
             flags = d.errors()
+            tp.append(time.perf_counter())
             d.download(g)
+            tp.append(time.perf_counter())
             out_node, out_slot = g.node, g.slot
+            phases = dict(zip(("concat", "upload", "stage", "download"), np.diff(tp).tolist()))
         t2 = time.perf_counter()
         if flags:
             for c in conns:
@@ -171,33 +237,31 @@ def run_dir(input_dir: str, output_dir: str, body: Callable, *, states=("tse", "
             written += m[1]
             wt.append(m[2])
         t3 = time.perf_counter()
-        # the slowest worker's phases (seconds) and the latest worker start after t0
-        worker = {k: max(w[k] for w in wt) for k in ("load", "pack", "send", "unpack", "dump")} if wt else {}
-        worker["last_start"] = max(w["start"] for w in wt) - t0 if wt else 0.0
-        return {"files": len(files), "written": written, "workers": len(chunks),
-                "edges": int(sum(p.n_edges for p in parts)), "read_pack_s": t1 - t0, "device_s": t2 - t1,
-                "unpack_write_s": t3 - t2, "wall_s": t3 - t0, "worker_max_s": worker}
-    finally:
-        for c in conns:
-            c.close()
-        for p in procs:
-            p.join(30)
-            if p.is_alive():
-                p.kill()
+    except BaseException:
+        _drop_pool()     # workers may be mid-job: start clean next time
+        raise
+    # the slowest worker's phases (seconds) and the latest worker start after t0
+    wt = [w for w in wt if w]
+    worker = {k: max(w[k] for w in wt) for k in ("load", "pack", "send", "unpack", "dump")} if wt else {}
+    worker["last_start"] = max(w["start"] for w in wt) - t0 if wt else 0.0
+    return {"files": len(files), "written": written, "workers": len(chunks),
+            "edges": int(sum(p.n_edges for p in parts)), "read_pack_s": t1 - t0, "device_s": t2 - t1,
+            "unpack_write_s": t3 - t2, "wall_s": t3 - t0, "worker_max_s": worker, "device_phases_s": phases}
 
 
 def _time_extrapolate(argv):
     """python -m gtf.dropin IN/ OUT/ REPS: the drop-in extrapolation stage (reference flags
     -c 2.0 -e 0.3 -z 0.4 -m 0.6 -b 550) over IN/, REPS + 1 times in this fresh process (the
-    first run loads the code objects), printing the wall time of each as JSON. bench.py's
-    dropin_stage runs it as a child process: its workers are forked before this process
-    touches the GPU."""
+    first run loads the code objects, forks the worker pool and initialises the GPU),
+    printing the wall time of each as JSON. bench.py's dropin_stage runs it as a child
+    process: its workers are forked before this process touches the GPU."""
     import json
     import sys
     from .params import Params
     ind, outd, reps = argv[0], argv[1], int(argv[2])
     p = Params()
     runs = [run_dir(ind, outd, lambda d: d.extrapolate(p)) for _ in range(reps + 1)]
+    _drop_pool()
     json.dump({"runs": runs[1:], "first": runs[0]}, sys.stdout)
 
 

@@ -109,30 +109,53 @@ def build_networkx(event_prefix: str, min_volume: int, max_volume: int, truth_cs
     return [G.subgraph(c).copy() for c in nx.weakly_connected_components(G)]
 
 
-def build_event_csr(event_prefix: str, min_volume: int, max_volume: int):
-    """Event conversion's graph straight to the packed CSR (gtf_build_event_csr):
-    the same TrackGraph as pack() of build_networkx's subgraphs with their
-    track_state_estimates keys in the reference's set order, without networkx.
-    Returns (graph with empty states -- every edge active, has_tse set, tse_rank in
-    dict order -- and vivl [N, 2] = (volume_id, in_volume_layer_id))."""
+def csr_from_rows(ids, a, b, device=None):
+    """The packed CSR of an event from its columns (node ids in CSV order; edge rows
+    add_edge(a, b) then add_edge(b, a)): gtf_build_event_csr on the host, or
+    gtf_build_event_csr_device on ``device`` (the build on the GPU, the same arrays bit
+    for bit). Returns (outputs dict of host arrays, n_edges, n_subgraphs)."""
     import ctypes
     from . import _native as nat
+    N, R = int(ids.size), int(a.size)
+    ids = np.ascontiguousarray(ids, np.int64)
+    a, b = np.ascontiguousarray(a, np.int64), np.ascontiguousarray(b, np.int64)
+    shapes = {"order": max(N, 1), "sub_id": max(N, 1), "slot_ptr": N + 1, "out_ptr": N + 1,
+              "slot_src": max(2 * R, 1), "tse_rank": max(2 * R, 1), "out_slot": max(2 * R, 1)}
+    names = ("order", "sub_id", "slot_ptr", "slot_src", "tse_rank", "out_ptr", "out_slot")
+    if device is None:
+        o = {k: np.zeros(n, np.int32) for k, n in shapes.items()}
+        vp = lambda t: ctypes.c_void_p(t.ctypes.data)  # noqa: E731
+        ev = nat.GtfEventCsr(N, R, vp(ids) if N else None, vp(a) if R else None, vp(b) if R else None,
+                             *[vp(o[k]) for k in names], 0, 0, 0)
+        nat.check(nat.lib().gtf_build_event_csr(ctypes.byref(ev)))
+        return o, int(ev.n_edges), int(ev.n_subgraphs)
+    import torch
+    L = nat.lib()
+    t_ids, t_a, t_b = (torch.from_numpy(x).to(device) for x in (ids, a, b))
+    o = {k: torch.zeros(n, dtype=torch.int32, device=device) for k, n in shapes.items()}
+    ws_bytes = int(L.gtf_build_event_device_workspace_bytes(N, R))
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=device)
+    vp = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    ev = nat.GtfEventCsr(N, R, vp(t_ids) if N else None, vp(t_a) if R else None, vp(t_b) if R else None,
+                         *[vp(o[k]) for k in names], 0, 0, 0)
+    stream = ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+    nat.check(L.gtf_build_event_csr_device(ctypes.byref(ev), vp(ws), ws_bytes, stream))
+    return {k: v.cpu().numpy() for k, v in o.items()}, int(ev.n_edges), int(ev.n_subgraphs)
+
+
+def build_event_csr(event_prefix: str, min_volume: int, max_volume: int, device=None):
+    """Event conversion's graph straight to the packed CSR (gtf_build_event_csr, or on
+    the GPU with ``device``: gtf_build_event_csr_device): the same TrackGraph as pack()
+    of build_networkx's subgraphs with their track_state_estimates keys in the
+    reference's set order, without networkx. Returns (graph with empty states -- every
+    edge active, has_tse set, tse_rank in dict order -- and vivl [N, 2] = (volume_id,
+    in_volume_layer_id))."""
     from .graph import NODE_FIELDS, SLOT_FIELDS, check_layout, empty_arrays
     ids, x, y, z, r, layer = read_nodes(event_prefix + "nodes.csv", min_volume, max_volume)
     n2, n1 = read_edges(event_prefix + "edges.csv")
-    N, R = int(ids.size), int(n1.size)
+    N = int(ids.size)
     ids = np.ascontiguousarray(ids, np.int64)
-    a, b = np.ascontiguousarray(n1, np.int64), np.ascontiguousarray(n2, np.int64)
-    o = {"order": np.zeros(max(N, 1), np.int32), "sub_id": np.zeros(max(N, 1), np.int32),
-         "slot_ptr": np.zeros(N + 1, np.int32), "out_ptr": np.zeros(N + 1, np.int32),
-         "slot_src": np.zeros(max(2 * R, 1), np.int32), "tse_rank": np.zeros(max(2 * R, 1), np.int32),
-         "out_slot": np.zeros(max(2 * R, 1), np.int32)}
-    vp = lambda t: ctypes.c_void_p(t.ctypes.data)  # noqa: E731
-    ev = nat.GtfEventCsr(N, R, vp(ids) if N else None, vp(a) if R else None, vp(b) if R else None,
-                         vp(o["order"]), vp(o["sub_id"]), vp(o["slot_ptr"]), vp(o["slot_src"]), vp(o["tse_rank"]),
-                         vp(o["out_ptr"]), vp(o["out_slot"]), 0, 0, 0)
-    nat.check(nat.lib().gtf_build_event_csr(ctypes.byref(ev)))
-    E = int(ev.n_edges)
+    o, E, n_sub = csr_from_rows(ids, n1, n2, device)
     order = o["order"][:N].astype(np.int64)
     node, slot = empty_arrays(NODE_FIELDS, N), empty_arrays(SLOT_FIELDS, E)
     gnn = np.stack([x, y, z, r], axis=1)[order]
@@ -150,8 +173,7 @@ def build_event_csr(event_prefix: str, min_volume: int, max_volume: int):
     slot["rev_edge"][:] = 1
     slot["act"][:] = 1
     slot["tse_rank"] = o["tse_rank"][:E].copy()
-    g = TrackGraph(N, E, o["slot_ptr"].copy(), o["out_ptr"].copy(), o["out_slot"][:E].copy(), node, slot,
-                   int(ev.n_subgraphs))
+    g = TrackGraph(N, E, o["slot_ptr"].copy(), o["out_ptr"].copy(), o["out_slot"][:E].copy(), node, slot, n_sub)
     check_layout(g)
     lay = layer[order]
     vivl = np.stack([(lay / 1000).astype(np.int64), lay % 100], 1).astype(np.float64)

@@ -62,13 +62,16 @@ def event_layout(event_prefix: str, min_volume: int, max_volume: int, builder: s
     active (helper.initialize_edge_activation). Returns (graph, vivl[N, 2]).
 
     builder "native": gtf_build_event_csr (C++, CSV rows -> CSR, CPython set orders
-    reproduced); "networkx": the reference's own construction through networkx and
+    reproduced); "device": gtf_build_event_csr_device (the same build on the GPU, the
+    same arrays); "networkx": the reference's own construction through networkx and
     pack() (gtf.io.build_networkx) -- the slow path the native one is tested against."""
     from . import io
     if builder == "native":
         return io.build_event_csr(event_prefix, min_volume, max_volume)
+    if builder == "device":
+        return io.build_event_csr(event_prefix, min_volume, max_volume, device="cuda")
     if builder != "networkx":
-        raise ValueError("builder must be 'native' or 'networkx'")
+        raise ValueError("builder must be 'native', 'device' or 'networkx'")
     import networkx as nx
     subs = io.build_networkx(event_prefix, min_volume, max_volume)
     for G in subs:

@@ -518,6 +518,16 @@ typedef struct gtf_event_csr {
 
 int gtf_build_event_csr(gtf_event_csr* ev);
 
+/* The same build on the GPU (SURVEY §8f #2 "graph build on device"; gtf_build_dev.hip):
+ * every pointer of `ev` a DEVICE array of the sizes above, the outputs equal to
+ * gtf_build_event_csr's bit for bit (radix sorts for the id lookup and networkx's
+ * successor insertion order, hook + pointer jumping for the weakly connected components,
+ * CPython 3.10 set tables in the workspace for the set orders). Synchronises `stream`
+ * (n_edges / n_subgraphs are returned in `ev`). Replaces helper.construct_graph
+ * (helper.py:465-521) and event_conversion.py:63-84 like the host builder. */
+size_t gtf_build_event_device_workspace_bytes(int64_t n_nodes, int64_t n_rows);
+int gtf_build_event_csr_device(gtf_event_csr* ev, void* workspace, size_t workspace_bytes, gtf_stream_t stream);
+
 /* Member order of every extraction candidate as the reference builds it: CCA over the
  * active edges of each subgraph (extract_track_candidates.py:332-346) -- networkx
  * weakly connected components, each copied as subGraph.subgraph(component) (set order

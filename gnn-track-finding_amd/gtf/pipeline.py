@@ -56,7 +56,7 @@ class Iteration:
     remaining_vivl: Optional[np.ndarray] = None
 
 
-def event_layout(event_prefix: str, min_volume: int, max_volume: int, builder: str = "native"):
+def event_layout(event_prefix: str, min_volume: int, max_volume: int, builder: str = "native", device="cuda"):
     """Host half of event conversion: the packed network in the reference's orders,
     with empty track_state_estimates dicts keyed in their set order and every edge
     active (helper.initialize_edge_activation). Returns (graph, vivl[N, 2]).
@@ -69,7 +69,7 @@ def event_layout(event_prefix: str, min_volume: int, max_volume: int, builder: s
     if builder == "native":
         return io.build_event_csr(event_prefix, min_volume, max_volume)
     if builder == "device":
-        return io.build_event_csr(event_prefix, min_volume, max_volume, device="cuda")
+        return io.build_event_csr(event_prefix, min_volume, max_volume, device=device)
     if builder != "networkx":
         raise ValueError("builder must be 'native', 'device' or 'networkx'")
     import networkx as nx
@@ -86,12 +86,14 @@ def event_layout(event_prefix: str, min_volume: int, max_volume: int, builder: s
 
 
 def build_event(event_prefix: str, min_volume: int, max_volume: int, p: Params = None, device="cuda",
-                builder: str = "native"):
+                builder: str = "device"):
     """event_conversion.py:53-101: CSVs -> packed network with track_state_estimates,
-    activation 1, priors, mixture weights and degrees. Returns (graph, vivl[N, 2])."""
+    activation 1, priors, mixture weights and degrees, all on the GPU (the graph build by
+    gtf_build_event_csr_device; builder "native" for the host C++ one, the same arrays).
+    Returns (graph, vivl[N, 2])."""
     from .device import DeviceGraph
     p = p or Params()
-    g, vivl = event_layout(event_prefix, min_volume, max_volume, builder)
+    g, vivl = event_layout(event_prefix, min_volume, max_volume, builder, device)
     if g.n_nodes == 0:
         return g, vivl
     d = DeviceGraph(g, device)

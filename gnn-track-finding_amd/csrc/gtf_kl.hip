@@ -75,11 +75,15 @@ __device__ __forceinline__ double gy(const gtf_kl_graph& g, int v) { return g.gn
 
 // where a kernel reads neighbour coordinates and truth ids: global memory, or a block's
 // LDS window of consecutive nodes [lo, hi) with global memory beyond it
-struct GSrc {
-    const gtf_kl_graph* g;
-    __device__ __forceinline__ double x(int u) const { return gx(*g, u); }
-    __device__ __forceinline__ double y(int u) const { return gy(*g, u); }
-    __device__ __forceinline__ long long t(int u) const { return g->truth[u]; }
+struct GSrc {   // the fields themselves, not a pointer to the kernel-argument struct
+    const double* gnn;
+    int64_t stride;
+    const int64_t* truth;
+    __device__ __forceinline__ explicit GSrc(const gtf_kl_graph& g)
+        : gnn(g.gnn), stride(g.gnn_stride ? g.gnn_stride : 4), truth(g.truth) {}
+    __device__ __forceinline__ double x(int u) const { return gnn[stride * u]; }
+    __device__ __forceinline__ double y(int u) const { return gnn[stride * u + 1]; }
+    __device__ __forceinline__ long long t(int u) const { return truth[u]; }
 };
 struct WSrc {
     const gtf_kl_graph* g;
@@ -272,7 +276,7 @@ __device__ __forceinline__ void pkl_node(const gtf_kl_graph& g, const gtf_kl_out
     const int gi = (bid * BLOCK + (int)threadIdx.x) / G;
     if (gi >= count) return;  // group-uniform
     const int v = list ? list[gi] : first + gi;   // (ordered layout: the bucket is a node range)
-    pkl_node_body<T, G, STATES>(g, o, GSrc{&g}, v, threadIdx.x & (G - 1),
+    pkl_node_body<T, G, STATES>(g, o, GSrc(g), v, threadIdx.x & (G - 1),
                                 (KlStage<T, G>*)smem + (int)threadIdx.x / G);
 }
 
@@ -491,7 +495,7 @@ __device__ __forceinline__ void pkl_node4(const gtf_kl_graph& g, const gtf_kl_ou
                                           int bid, int first) {
     const int gi = bid * BLOCK + (int)threadIdx.x;
     if (gi >= count) return;
-    pkl_node4_body<T, STATES>(g, o, GSrc{&g}, list ? list[gi] : first + gi);
+    pkl_node4_body<T, STATES>(g, o, GSrc(g), list ? list[gi] : first + gi);
 }
 
 struct KlBuckets {

@@ -1,9 +1,14 @@
 #!/bin/bash
-# A/B of config-5 gtf_parabolic_kl builds on one box: tools/gpu_kl_ab.sh LIB... (file
-# names under gnn-track-finding_amd/gtf; "libgtf.so" is the default build), two rounds.
-set -e
-for r in 1 2; do
-  for lib in "$@"; do
-    GTF_LIB=$PWD/gnn-track-finding_amd/gtf/$lib timeout -k 10 200 python -u tools/pkl_time.py 50 2>/dev/null | sed "s/^/$lib r$r /" | cut -c1-200
+# config-5 KL kernel: this build against the round-2 kernel source (gtf/ab/libgtf_r02kl.so),
+# hot (one batch relaunched) and cold (8 batches rotated), alternating
+set -o pipefail
+O=gpurun_out/kl_ab
+mkdir -p $O
+for i in 1 2; do
+  for lib in default gnn-track-finding_amd/gtf/ab/libgtf_r02kl.so; do
+    if [ $lib = default ]; then unset GTF_LIB; else export GTF_LIB=$PWD/$lib; fi
+    timeout -k 10 120 python tools/pkl_time.py 48 --hot >> $O/ab.jsonl || exit 1
+    timeout -k 10 120 python tools/pkl_time.py 48 >> $O/ab.jsonl || exit 1
   done
 done
+cat $O/ab.jsonl

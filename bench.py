@@ -269,7 +269,9 @@ def bench_components(g, params, dev, reps=5):
     gtf_updated_state_distances: pair counts, scan, pair kernel) and tag propagation
     (tag_propagation.py:97-164, Jacobi max sweeps until flips / processed <= 10 %, the flip
     count read back after each sweep as the script's stop test needs), initial tag = node
-    index, radius = r. Wall times with the device synchronised, median of reps."""
+    index, radius = r. Wall times with the device synchronised, median of reps; a15 / a2
+    outputs left in the device layout's node order (host_order=False: no reordering
+    gathers, as a device-resident caller consumes them)."""
     import torch
     from gtf.device import DeviceGraph
     from gtf import roofline as rf
@@ -281,7 +283,7 @@ def bench_components(g, params, dev, reps=5):
     for _ in range(reps + 1):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        ptr, cols = d.updated_state_distances()
+        ptr, cols = d.updated_state_distances(host_order=False)
         torch.cuda.synchronize()
         ts.append(time.perf_counter() - t0)
     npairs = int(cols["chi2"].numel())
@@ -328,7 +330,7 @@ def bench_components(g, params, dev, reps=5):
     # a2: the initial per-edge states of event conversion (helper.py:238-452 + priors,
     # mixture weights, degree; pipeline.build_event's device half) on the same event
     def tse():
-        d.track_state_estimates(params)
+        d.track_state_estimates(params, host_order=False)
         d.node_ops(["priors_tse", "mw_tse", "degree"], params)
     tse()
     torch.cuda.synchronize()

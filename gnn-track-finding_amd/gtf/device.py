@@ -343,12 +343,14 @@ class DeviceGraph:
                                            ctypes.byref(self.cuts), ctypes.byref(self.ce), ctypes.byref(cp),
                                            self.ptr("ws"), self.stream, arr))
 
-    def track_state_estimates(self, p: Params):
+    def track_state_estimates(self, p: Params, host_order: bool = True):
         """helper.compute_track_state_estimates (helper.py:238-452) for every key of the
         nodes' track_state_estimates dicts (tse_rank >= 0, dict order as given): writes
         tse_sv / tse_cov / tse_tau / tse_xyzr / tse_theta / tse_var_ms on the device and
         returns the per-node attributes (xy/zr_edge_gradient_mean_var,
-        angle_of_rotation, translation) as device tensors."""
+        angle_of_rotation, translation) as device tensors -- in host node order, or with
+        host_order=False in the device layout's order (no gathers: what a caller that keeps
+        the event on the device consumes)."""
         self._natural_only("track_state_estimates")
         torch = self.torch
         N = self.n_nodes
@@ -363,19 +365,20 @@ class DeviceGraph:
         cp = self.cparams(p)
         nat.check(self.lib.gtf_track_state_estimates(ctypes.byref(self.cg_sched), ctypes.byref(self.ctse),
                                                      ctypes.byref(ex), ctypes.byref(cp), self.stream))
-        if self.order is not None:   # per-node outputs in host node order
+        if self.order is not None and host_order:   # per-node outputs in host node order
             inv = self._inv_order()
             x = {k: v[inv] for k, v in x.items()}
         return x
 
     # ------------------------------------------ a15: distances between updated states
-    def updated_state_distances(self, truth=None):
+    def updated_state_distances(self, truth=None, host_order: bool = True):
         """calculate_distance_between_updated_track_states.py (:27-104 over the pair loop
         :134-195) on the current updated_track_states: every pair i > j of the dict entries
         of each node with the dict and more than one active in-edge. Returns (pair_ptr [N+1]
         int64, {"chi2", "avg_tau", "avg_theta", "delta_theta"[, "truth"]}) as device
         tensors, pairs of node v at [pair_ptr[v], pair_ptr[v+1]) in the reference's loop
-        order. truth: [N] truth_particle per node (host or device), or None."""
+        order. truth: [N] truth_particle per node (host or device), or None. host_order=False:
+        the node segments in the device layout's node order (no reordering gathers)."""
         self._natural_only("updated_state_distances")
         torch = self.torch
         dev = self.device
@@ -409,7 +412,7 @@ class DeviceGraph:
             raise ValueError("updated-state distances: " +
                              "; ".join(m for b, m in nat.ERR_FLAGS.items() if f & b))
         cols = {k: v[:P] for k, v in out.items()}
-        if self.order is not None and N:   # node segments of pairs in host node order
+        if self.order is not None and N and host_order:   # node segments of pairs in host node order
             inv = self._inv_order()
             cnt = counts[:N][inv]
             hptr = torch.zeros(N + 1, dtype=torch.int64, device=dev)

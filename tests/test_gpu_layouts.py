@@ -63,3 +63,24 @@ def test_tag_propagation_layout_equivariant(layout):
     (ta, fa), (tb, fb) = res
     assert np.array_equal(ta, tb) and fa == fb and len(fa) >= 1
     torch.cuda.synchronize()
+
+
+def test_device_order_outputs_are_the_host_order_ones_renumbered():
+    """host_order=False (the bench's device-resident timing): the same a2 node attributes
+    and a15 pair segments, in the tiled layout's node order"""
+    g = _event()
+    d = DeviceGraph(g.copy(), layout="tiled", tile=512)
+    xh = {k: v.cpu().numpy() for k, v in d.track_state_estimates(Params()).items()}
+    xd = {k: v.cpu().numpy() for k, v in d.track_state_estimates(Params(), host_order=False).items()}
+    order = d.order   # device node i is host node order[i]
+    for k in xh:
+        assert np.array_equal(xd[k], xh[k][order], equal_nan=True), k
+    d.full_pass(Params())
+    ph, ch = d.updated_state_distances()
+    pd_, cd = d.updated_state_distances(host_order=False)
+    ph, pd_ = ph.cpu().numpy(), pd_.cpu().numpy()
+    ch, cd = {k: v.cpu().numpy() for k, v in ch.items()}, {k: v.cpu().numpy() for k, v in cd.items()}
+    assert ph[-1] == pd_[-1] > 0
+    seg = np.concatenate([np.arange(ph[h], ph[h + 1]) for h in order])
+    for k in ch:
+        assert np.array_equal(cd[k], ch[k][seg], equal_nan=True), k

@@ -3,9 +3,10 @@
 reference's own stages run subgraph by subgraph (tests/golden/make_golden_800.py).
 
 The inputs are built on the GPU exactly as a user would build them: the committed CSVs
-(tests/golden/kat800) -> gtf_build_event_csr (C++, the reference's node / successor /
-set orders: the structure digest equals the reference's packed network) ->
-gtf_track_state_estimates + priors / weights / degree on the device. Then:
+(tests/golden/kat800) -> gtf_build_event_csr_device (the graph build on the GPU, the
+reference's node / successor / set orders: the structure digest equals the reference's
+packed network) -> gtf_track_state_estimates + priors / weights / degree on the device.
+Then:
 
 * iteration 1, clustering on track_state_estimates (-c 1.0 -k 2.0,
   run_gnn_trackml_mod.sh:89): the reference raises ValueError in 2 of the 1,909 subgraphs

@@ -73,6 +73,28 @@ __device__ __forceinline__ int64_t gnn_row(const gtf_kl_graph& g, int v) {
 __device__ __forceinline__ double gx(const gtf_kl_graph& g, int v) { return g.gnn[gnn_row(g, v)]; }
 __device__ __forceinline__ double gy(const gtf_kl_graph& g, int v) { return g.gnn[gnn_row(g, v) + 1]; }
 
+// cache policy of the once-touched streams (GTF_KL_NT bits, diagnostics builds): 1 the
+// outputs stored non-temporal, 2 the in-edge sender lists loaded non-temporal, 4 the node's
+// own coordinates and truth id too (they are also other nodes' sender gathers)
+#ifndef GTF_KL_NT
+#define GTF_KL_NT 0
+#endif
+template <typename T>
+__device__ __forceinline__ void st_out(T* p, T v) {
+    if (GTF_KL_NT & 1) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+template <typename T>
+__device__ __forceinline__ T ld_list(const T* p) {
+    if (GTF_KL_NT & 2) return __builtin_nontemporal_load(p);
+    return *p;
+}
+template <typename T>
+__device__ __forceinline__ T ld_own(const T* p) {
+    if (GTF_KL_NT & 4) return __builtin_nontemporal_load(p);
+    return *p;
+}
+
 // where a kernel reads neighbour coordinates and truth ids: global memory, or a block's
 // LDS window of consecutive nodes [lo, hi) with global memory beyond it
 struct GSrc {   // the fields themselves, not a pointer to the kernel-argument struct
@@ -237,8 +259,8 @@ __device__ __forceinline__ void pkl_node_body(const gtf_kl_graph& g, const gtf_k
         }
         vs = grp_sum<G>(vs);
         if (gl == 0) {
-            if (o.emp_var) o.emp_var[v] = vs / (double)d;
-            if (o.emp_mean) o.emp_mean[v] = mean;
+            if (o.emp_var) st_out(o.emp_var + (v), (double)(vs / (double)d));
+            if (o.emp_mean) st_out(o.emp_mean + (v), (double)(mean));
         }
     }
     gtf::wave_lds_sync();
@@ -265,8 +287,8 @@ __device__ __forceinline__ void pkl_node_body(const gtf_kl_graph& g, const gtf_k
             b = pstate<T>(f, src.x(uj), src.y(uj), s, nullptr, nullptr);
             if (o.truth) { ti = src.t(ui); tj = src.t(uj); }
         }
-        kl[base + t] = pkl<T>(a, b);
-        if (o.truth) o.truth[base + t] = (int8_t)(tv == ti && ti == tj && tv == tj);  // (:84-95)
+        st_out(kl + (base + t), (T)(pkl<T>(a, b)));
+        if (o.truth) st_out(o.truth + (base + t), (int8_t)(tv == ti && ti == tj && tv == tj));  // (:84-95)
     }
 }
 
@@ -298,10 +320,10 @@ __device__ __forceinline__ void pkl_node1_ordered(const gtf_kl_graph& g, const g
     const bool two = gi >= g.n_d1;
     const int64_t l = g.slot0 + (two ? g.n_d1 + 2 * (int64_t)(gi - g.n_d1) : gi);
     const int64_t pp = g.pair0 + (gi - g.n_d1);
-    const double xv = gx(g, v), yv = gy(g, v);
-    const long long tv = (o.truth && g.truth) ? g.truth[v] : 0;
-    const int u0 = g.slot_src[l];
-    const int u1 = two ? g.slot_src[l + 1] : u0;
+    const double xv = ld_own(g.gnn + gnn_row(g, v)), yv = ld_own(g.gnn + gnn_row(g, v) + 1);
+    const long long tv = (o.truth && g.truth) ? ld_own(g.truth + v) : 0;
+    const int u0 = ld_list(g.slot_src + l);
+    const int u1 = two ? ld_list(g.slot_src + l + 1) : u0;
     const double x0 = gx(g, u0), y0 = gy(g, u0);
     const double x1 = gx(g, u1), y1 = gy(g, u1);
     long long t0 = 0, t1 = 0;
@@ -316,11 +338,11 @@ __device__ __forceinline__ void pkl_node1_ordered(const gtf_kl_graph& g, const g
     const double g1 = two ? (f.y - y1) / (f.x - x1) : g0;
     // / 2 and / 1 as exact scalings
     const double mean = two ? (g0 + g1) * 0.5 : g0;
-    if (o.emp_var) o.emp_var[v] = two ? ((g0 - mean) * (g0 - mean) + (g1 - mean) * (g1 - mean)) * 0.5 : 0.0 * (g0 - mean);
-    if (o.emp_mean) o.emp_mean[v] = mean;
+    if (o.emp_var) st_out(o.emp_var + (v), (double)(two ? ((g0 - mean) * (g0 - mean) + (g1 - mean) * (g1 - mean)) * 0.5 : 0.0 * (g0 - mean)));
+    if (o.emp_mean) st_out(o.emp_mean + (v), (double)(mean));
     if (two) {
-        ((T*)o.kl)[pp] = pkl<T>(b, a);   // pair (i, j) = (1, 0)
-        if (o.truth) o.truth[pp] = (int8_t)(tv == t1 && t1 == t0 && tv == t0);
+        st_out((T*)o.kl + (pp), (T)(pkl<T>(b, a)));   // pair (i, j) = (1, 0)
+        if (o.truth) st_out(o.truth + (pp), (int8_t)(tv == t1 && t1 == t0 && tv == t0));
     }
 }
 
@@ -346,11 +368,11 @@ __device__ __forceinline__ void pkl_b0_body(const gtf_kl_graph& g, const gtf_kl_
     const double g0 = (f.y - y0) / (f.x - x0);
     const double g1 = two ? (f.y - y1) / (f.x - x1) : g0;
     const double mean = two ? (g0 + g1) * 0.5 : g0;   // / 2 and / 1 as exact scalings
-    if (o.emp_var) o.emp_var[v] = two ? ((g0 - mean) * (g0 - mean) + (g1 - mean) * (g1 - mean)) * 0.5 : 0.0 * (g0 - mean);
-    if (o.emp_mean) o.emp_mean[v] = mean;
+    if (o.emp_var) st_out(o.emp_var + (v), (double)(two ? ((g0 - mean) * (g0 - mean) + (g1 - mean) * (g1 - mean)) * 0.5 : 0.0 * (g0 - mean)));
+    if (o.emp_mean) st_out(o.emp_mean + (v), (double)(mean));
     if (two) {
-        ((T*)o.kl)[pp] = pkl<T>(b, a);   // pair (i, j) = (1, 0)
-        if (o.truth) o.truth[pp] = (int8_t)(tv == t1 && t1 == t0 && tv == t0);
+        st_out((T*)o.kl + (pp), (T)(pkl<T>(b, a)));   // pair (i, j) = (1, 0)
+        if (o.truth) st_out(o.truth + (pp), (int8_t)(tv == t1 && t1 == t0 && tv == t0));
     }
 }
 
@@ -474,8 +496,8 @@ __device__ __forceinline__ void pkl_node4_body(const gtf_kl_graph& g, const gtf_
 #pragma unroll
         for (int q = 1; q < 4; q++)
             if (q < d) vs = vs + (gr[q] - mean) * (gr[q] - mean);
-        if (o.emp_var) o.emp_var[v] = vs / (double)d;
-        if (o.emp_mean) o.emp_mean[v] = mean;
+        if (o.emp_var) st_out(o.emp_var + (v), (double)(vs / (double)d));
+        if (o.emp_mean) st_out(o.emp_mean + (v), (double)(mean));
     }
     T* kl = (T*)o.kl;
     int t = 0;
@@ -484,8 +506,8 @@ __device__ __forceinline__ void pkl_node4_body(const gtf_kl_graph& g, const gtf_
 #pragma unroll
         for (int j = 0; j < i; j++)
             if (i < d) {
-                kl[base + t] = pkl<T>(st[i], st[j]);
-                if (o.truth) o.truth[base + t] = (int8_t)(tv == tu[i] && tu[i] == tu[j] && tv == tu[j]);
+                st_out(kl + (base + t), (T)(pkl<T>(st[i], st[j])));
+                if (o.truth) st_out(o.truth + (base + t), (int8_t)(tv == tu[i] && tu[i] == tu[j] && tv == tu[j]));
                 t++;
             }
 }

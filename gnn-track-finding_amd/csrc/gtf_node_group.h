@@ -788,6 +788,29 @@ __device__ __forceinline__ bool ops_have_fresh(const NodeOps& ops) {
     return false;
 }
 
+// Diagnostics build GTF_OP_TIMING=1: lane 0 of every wavefront (up to
+// GTF_OP_TIMING_WAVES) records the shader clock at its start, after its loads, after every
+// op of the sequence and after its stores (row of 24 words per wave; word 23 = G), read
+// back by gtf_op_timing (tools/op_timing.py); words 20 / 21 = the chip-wide real-time
+// clock at the start / end (the shader clocks of different XCDs are not aligned)
+#ifndef GTF_OP_TIMING
+#define GTF_OP_TIMING 0
+#endif
+#if GTF_OP_TIMING
+#define GTF_OP_TIMING_WAVES 65536
+__device__ uint64_t g_op_time[GTF_OP_TIMING_WAVES * 24];
+template <int G, int OP, typename Stage>
+__device__ __forceinline__ void node_op_timed(NodeCtx<G>& c, const gtf_graph& g, gtf_nodes& n, gtf_states& tse,
+                                              gtf_states& uts, const gtf_params& p, const Ws& w, double* sval,
+                                              Stage* stg, double chi2_thr, double kl_thr, bool has_tse, bool has_uts,
+                                              uint64_t* tb, int& ti) {
+    node_op<G, OP, Stage>(c, g, n, tse, uts, p, w, sval, stg, chi2_thr, kl_thr, has_tse, has_uts);
+    const uint64_t t = __builtin_readcyclecounter();
+    if (tb && ti < 20) tb[ti] = t;
+    ti++;
+}
+#endif
+
 // compile-time op sequence for one group size: dead ops are compiled out.
 // `bid` is the block index inside this bucket's range of the launch.
 template <int G, int... OPS>
@@ -799,7 +822,20 @@ __device__ __forceinline__ void node_seq_body(const gtf_graph& g, gtf_nodes& n, 
     using Stage = StageT<G>;
     NodeCtx<G> c;
     const int gi = (bid * NBLOCK + (int)threadIdx.x) / G;
+#if GTF_OP_TIMING
+    const uint64_t t_start = __builtin_readcyclecounter();
+    const uint64_t rt_start = __builtin_amdgcn_s_memrealtime();   // chip-wide constant-rate clock
+    const int wave = (int)((blockIdx.x * NBLOCK + threadIdx.x) / 64);
+    uint64_t* tb = ((threadIdx.x & 63) == 0 && wave < GTF_OP_TIMING_WAVES) ? g_op_time + 24 * (int64_t)wave : nullptr;
+    int ti = 2;
+#endif
     if (!node_load(c, g, n, tse, uts, e, list, seg, count, gi, Q::need, ar)) return;
+#if GTF_OP_TIMING
+    {
+        const uint64_t t = __builtin_readcyclecounter();
+        if (tb) { tb[0] = t_start; tb[1] = t; tb[20] = rt_start; tb[23] = (uint64_t)G; }
+    }
+#endif
     double* sval = (double*)smem + (threadIdx.x & ~63);
     Stage* stg = (Stage*)(smem + NBLOCK * sizeof(double)) + (Q::cluster ? (int)threadIdx.x / G : 0);
 #if GTF_EARLY_STAGE
@@ -820,10 +856,21 @@ __device__ __forceinline__ void node_seq_body(const gtf_graph& g, gtf_nodes& n, 
 #if GTF_ABLATE == 4
     // diagnostics build: the node's loads and stores only (every field marked dirty)
     if (has_tse || has_uts) { c.uts.dirty = c.tse.dirty = D_RANK | D_MW | D_PRIOR; c.uts_dirty_lr = true; c.edge_mw_dirty = true; }
+#elif GTF_OP_TIMING
+    (node_op_timed<G, OPS, Stage>(c, g, n, tse, uts, p, w, sval, stg, chi2_thr, kl_thr, has_tse, has_uts, tb, ti),
+     ...);
 #else
     (node_op<G, OPS, Stage>(c, g, n, tse, uts, p, w, sval, stg, chi2_thr, kl_thr, has_tse, has_uts), ...);
 #endif
     node_store(c, n, tse, uts, e);
+#if GTF_OP_TIMING
+    {
+        const uint64_t t = __builtin_readcyclecounter();
+        const uint64_t rt = __builtin_amdgcn_s_memrealtime();
+        if (tb && ti < 20) tb[ti] = t;
+        if (tb) tb[21] = rt;
+    }
+#endif
 }
 
 struct Buckets {

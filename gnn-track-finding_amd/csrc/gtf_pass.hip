@@ -1083,6 +1083,18 @@ int gtf_pass(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts,
     return gtf_pass_ev(g, n, tse, uts, e, p, ws, stream, nullptr);
 }
 
+#if GTF_OP_TIMING
+// diagnostics build only: the node kernel's per-wave op timestamps (g_op_time), reset / read
+int gtf_op_timing(uint64_t* host, int32_t n_words, int32_t reset) {
+    void* a = nullptr;
+    if (hipGetSymbolAddress(&a, HIP_SYMBOL(g_op_time)) != hipSuccess) return -1;
+    const size_t cap = sizeof(uint64_t) * (size_t)GTF_OP_TIMING_WAVES * 24;
+    const size_t nb = n_words < 0 ? 0 : (size_t)n_words * sizeof(uint64_t);
+    if (reset) return hipMemset(a, 0, cap) == hipSuccess ? 0 : -1;
+    return hipMemcpy(host, a, nb < cap ? nb : cap, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
+
 const char* gtf_last_error(void) { return g_err; }
 const char* gtf_version(void) { return "gtf 0.1.0 (gfx950)"; }
 

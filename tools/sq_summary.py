@@ -18,7 +18,7 @@ for f in glob.glob(d + "/sq*/**/*counter_collection.csv", recursive=True):
             continue
         n = n.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
         acc[n][r["Counter_Name"]] += float(r["Counter_Value"])
-        disp[(n, r["Counter_Name"])].add(r["Dispatch_Id"])
+        disp[(n, r["Counter_Name"])].add((f, r["Dispatch_Id"]))   # ids restart in every pass
 out = {}
 for n, cs in acc.items():
     out[n] = {c: v / max(len(disp[(n, c)]), 1) for c, v in sorted(cs.items())}

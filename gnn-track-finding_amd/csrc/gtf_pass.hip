@@ -211,22 +211,64 @@ __device__ __forceinline__ void sender_bucket_lanes(const gtf_graph& g, gtf_node
     sender_scan_lane<G>(g, n, e, p, w, en.x, en.y, kv.x, kv.y, t & (G - 1));
 }
 
-__global__ void __launch_bounds__(BLOCK) k_sender_sched(gtf_graph g, gtf_nodes n, gtf_edges e, gtf_params p, Ws w,
-                                                        SendBuckets sb) {
+// All arguments of k_sender_sched in one by-value struct, read through a laundered copy of
+// the kernarg-segment address (as the node kernel's NodeKArgs, gtf_node_group.h): each
+// bucket path loads only the pointers it uses. Passed as separate structs the scan kept
+// ~100 SGPRs live, which admits 6 blocks of 256 threads per CU (SGPR budget 800 /
+// (ceil(sgpr / 16) * 16 + 16)) where its 58 VGPRs allow 8.
+struct SendKArgs {
+    gtf_graph g;
+    gtf_nodes n;
+    gtf_edges e;
+    gtf_params p;
+    Ws w;
+    SendBuckets sb;
+};
+typedef const __attribute__((address_space(4))) SendKArgs* SendKArgPtr;
+__device__ __forceinline__ SendKArgPtr send_kargs() {
+    uint64_t a = (uint64_t)(uintptr_t)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(a));
+    return (SendKArgPtr)a;
+}
+
+#ifndef GTF_SEND_KARGS
+#define GTF_SEND_KARGS 1
+#endif
+#ifndef GTF_SEND_NUM_SGPR
+#define GTF_SEND_NUM_SGPR 72
+#endif
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(GTF_SEND_NUM_SGPR))) k_sender_sched(SendKArgs args) {
+#if GTF_SEND_KARGS
+    (void)args;
+    const SendKArgPtr A = send_kargs();
+#define GTF_SA(f) (*(decltype(args.f)*)&A->f)
+#else
+#define GTF_SA(f) (args.f)
+#endif
     int b = blockIdx.x;
-    if (b < sb.blocks[0]) {
-        if (sb.lanes[0]) sender_bucket_lanes<4>(g, n, e, p, w, sb.list[0], sb.lanes[0], sb.count[0], b, sb.blocks[0]);
-        else sender_bucket<4>(g, n, e, p, w, sb.list[0], sb.count[0], b, sb.blocks[0]);
+    const int b0 = GTF_SA(sb).blocks[0];
+    if (b < b0) {
+        const SendBuckets& sb = GTF_SA(sb);
+        if (sb.lanes[0])
+            sender_bucket_lanes<4>(GTF_SA(g), GTF_SA(n), GTF_SA(e), GTF_SA(p), GTF_SA(w), sb.list[0], sb.lanes[0],
+                                   sb.count[0], b, b0);
+        else sender_bucket<4>(GTF_SA(g), GTF_SA(n), GTF_SA(e), GTF_SA(p), GTF_SA(w), sb.list[0], sb.count[0], b, b0);
         return;
     }
-    b -= sb.blocks[0];
-    if (b < sb.blocks[1]) {
-        if (sb.lanes[1]) sender_bucket_lanes<8>(g, n, e, p, w, sb.list[1], sb.lanes[1], sb.count[1], b, sb.blocks[1]);
-        else sender_bucket<8>(g, n, e, p, w, sb.list[1], sb.count[1], b, sb.blocks[1]);
+    b -= b0;
+    const int b1 = GTF_SA(sb).blocks[1];
+    if (b < b1) {
+        const SendBuckets& sb = GTF_SA(sb);
+        if (sb.lanes[1])
+            sender_bucket_lanes<8>(GTF_SA(g), GTF_SA(n), GTF_SA(e), GTF_SA(p), GTF_SA(w), sb.list[1], sb.lanes[1],
+                                   sb.count[1], b, b1);
+        else sender_bucket<8>(GTF_SA(g), GTF_SA(n), GTF_SA(e), GTF_SA(p), GTF_SA(w), sb.list[1], sb.count[1], b, b1);
         return;
     }
-    b -= sb.blocks[1];
-    sender_bucket<16>(g, n, e, p, w, sb.list[2], sb.count[2], b, sb.blocks[2]);
+    b -= b1;
+    const SendBuckets& sb = GTF_SA(sb);
+    sender_bucket<16>(GTF_SA(g), GTF_SA(n), GTF_SA(e), GTF_SA(p), GTF_SA(w), sb.list[2], sb.count[2], b, sb.blocks[2]);
+#undef GTF_SA
 }
 
 // ---------------------------------------------------------------------------
@@ -772,7 +814,7 @@ int launch_extrap_edges(const gtf_graph* g, gtf_nodes* n, gtf_states* uts, gtf_e
                 total += sb.blocks[q];
             }
             if (total > 0)
-                hipLaunchKernelGGL(k_sender_sched, dim3(total), dim3(BLOCK), 0, st, *g, *n, *e, *p, w, sb);
+                hipLaunchKernelGGL(k_sender_sched, dim3(total), dim3(BLOCK), 0, st, SendKArgs{*g, *n, *e, *p, w, sb});
         } else {
             hipLaunchKernelGGL(k_sender, dim3((count + BLOCK / SG - 1) / (BLOCK / SG)), dim3(BLOCK), 0, st, *g, *n,
                                *e, *p, w, list, count);

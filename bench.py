@@ -498,12 +498,15 @@ def bench_sharded(workload, rank, world, dev, steps, warmup, params, backend="nc
                 sd.step(params)
             else:
                 sd.pass_(params)
+        t_issue = time.perf_counter() - t0     # host time to enqueue the K steps
         torch.cuda.synchronize()
         dist.barrier()
         torch.cuda.synchronize()
         sd.d.use_inputs(None)
+        issue[exchange] = reduce_scalar(t_issue, dist.ReduceOp.MAX, dev, backend)
         return reduce_scalar(time.perf_counter() - t0, dist.ReduceOp.MAX, dev, backend)
 
+    issue = {}
     el = run(True)
     el_pass = run(False)
     flags = int(reduce_scalar(sd.d.errors(), dist.ReduceOp.MAX, dev, backend))
@@ -512,6 +515,9 @@ def bench_sharded(workload, rank, world, dev, steps, warmup, params, backend="nc
     return {"scaling": "strong", "n_gpus": world, "edges": g.n_edges, "nodes": g.n_nodes,
             "ms_per_step": el / steps * 1e3, "edges_per_s": g.n_edges * steps / el,
             "pass_ms_no_exchange": el_pass / steps * 1e3,
+            "host_issue_ms_per_step": issue[True] / steps * 1e3,
+            "host_issue_ms_per_step_no_exchange": issue[False] / steps * 1e3,
+            "host_issue_note": "host time to enqueue the steps (max over ranks); close to ms_per_step = host-bound",
             "halo_bytes_per_rank_max": hb, "owned_slots_max": pl.cap_slots,
             "owned_slots_min": int((pl.slot_hi - pl.slot_lo).min()),
             "collective": "all_to_all_single of per-destination halo segments (RCCL over xGMI)",

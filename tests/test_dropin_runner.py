@@ -68,3 +68,32 @@ def test_run_dir_empty_directory(tmp_path):
     os.makedirs(ind)
     info = run_dir(ind, ind, None, workers=4, host_stage=lambda g: 0)
     assert info["files"] == info["written"] == 0
+
+
+def test_pool_survives_a_bad_file_and_is_reused(tmp_path):
+    """the worker pool is forked once and reused by later directories; a file a worker
+    cannot read raises in the caller, the pool is dropped, and the next directory runs on a
+    fresh pool with the same results"""
+    from gtf import dropin
+    d = _load("extrapolate")
+    p = Params(**{k: d["args"][k] for k in ("sigma0xy", "sigma0rz", "sigma0rz2", "endcap_boundary", "chi2_cut")})
+    good, bad = str(tmp_path / "good") + "/", str(tmp_path / "bad") + "/"
+    _write(d["in"], good)
+    _write(d["in"][:5], bad)
+    with open(bad + "2_subgraph.gpickle", "wb") as fh:
+        fh.write(b"not a pickle")
+    outs = [str(tmp_path / ("out%d" % i)) + "/" for i in range(3)]
+    for o in outs:
+        os.makedirs(o)
+    run_dir(good, outs[0], None, workers=3, host_stage=_oracle_extrapolate(p))
+    pool = dropin._POOL
+    assert pool is not None and pool.alive()
+    run_dir(good, outs[1], None, workers=3, host_stage=_oracle_extrapolate(p))
+    assert dropin._POOL is pool                      # reused, not re-forked
+    with pytest.raises(RuntimeError, match="drop-in worker"):
+        run_dir(bad, outs[2], None, workers=3, host_stage=_oracle_extrapolate(p))
+    assert dropin._POOL is None                      # dropped after the failure
+    run_dir(good, outs[2], None, workers=3, host_stage=_oracle_extrapolate(p))
+    for o in outs:
+        assert graphs_equal(_read(o), d["out"]) == []
+    dropin._drop_pool()

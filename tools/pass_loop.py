@@ -14,7 +14,13 @@ from gtf.params import Params  # noqa: E402
 
 K = int(sys.argv[1]) if len(sys.argv) > 1 else 100
 g = synth.workload("c4", seed=0)
-d = DeviceGraph(g, "cuda:0", layout="tiled")
+W = int(os.environ.get("GTF_WEDGES", "0"))   # diagnostics: azimuthal wedges (one per XCD) before the tiles
+if W > 1:
+    from gtf.shard import shard_layout
+    gd, _, _, _ = shard_layout(g, W, int(os.environ.get("GTF_WEDGE_TILE", "4096")))
+    d = DeviceGraph(gd, "cuda:0", layout="natural")
+else:
+    d = DeviceGraph(g, "cuda:0", layout="tiled")
 snap = d.snapshot(DeviceGraph.PASS_INPUTS)
 S = min(K, 50)
 d.stage_inputs(S)

@@ -341,11 +341,23 @@ class ShardedDeviceGraph:
         """the halo: what the other ranks' next pass reads, one all-to-all"""
         if self.world == 1:
             return
-        d = self.d
         _, st, sbuf, rbuf, sview, rview = self._io()
-        nat.check(d.lib.gtf_halo_pack(ctypes.byref(d.cn), ctypes.byref(d.ce), ctypes.byref(self.halo_send), sbuf, st))
+        self.halo_pack()
         alltoall_bytes(sview, rview, self.send_sizes, self.recv_sizes, self.backend, self.group)
-        nat.check(d.lib.gtf_halo_unpack(ctypes.byref(d.cn), ctypes.byref(d.ce), ctypes.byref(self.halo_recv), rbuf,
+        self.halo_unpack(rbuf)
+
+    def halo_pack(self):
+        """this rank's halo segments into its send buffer (on its stream)"""
+        d = self.d
+        _, st, sbuf = self._io()[:3]
+        nat.check(d.lib.gtf_halo_pack(ctypes.byref(d.cn), ctypes.byref(d.ce), ctypes.byref(self.halo_send), sbuf, st))
+
+    def halo_unpack(self, buf):
+        """the received halo segments (device buffer address `buf`, receive layout) into this
+        rank's replica (on its stream)"""
+        d = self.d
+        st = self._io()[1]
+        nat.check(d.lib.gtf_halo_unpack(ctypes.byref(d.cn), ctypes.byref(d.ce), ctypes.byref(self.halo_recv), buf,
                                         st))
 
     def sync(self):
@@ -374,3 +386,111 @@ class ShardedDeviceGraph:
     def owned_host_slots(self) -> np.ndarray:
         r = self.rank
         return self.d.slot_perm[self.plan.slot_lo[r]:self.plan.slot_hi[r]]
+
+
+class SplitDeviceGraph:
+    """One event's pass on ONE GPU as two receiver wedges run concurrently on two HIP
+    streams (the tail of each half's kernels overlaps the other's): two replicas of the
+    sharded layout (ShardedDeviceGraph with world 2) in this process, each on its own
+    stream; after both halves, each half's halo goes to the other through device memory
+    (the sender's halo_pack buffer is the receiver's unpack input -- for two parts the
+    send layout of one is the receive layout of the other), and the streams join. The
+    results equal the one-stream pass bit for bit (tests/test_gpu_split.py); each half's
+    owned receivers are final in its own replica (download() merges them).
+
+    Measured on C4 (tools/overlap_probe.py): two halves on two streams 129-136 us against
+    147-152 us for the one-stream pass; three parts no better, four slower."""
+
+    PARTS = 2
+
+    def __init__(self, g: TrackGraph, device="cuda"):
+        import torch
+        self.torch = torch
+        self.streams = [torch.cuda.Stream(device) for _ in range(self.PARTS)]
+        self.parts = []
+        for r in range(self.PARTS):
+            with torch.cuda.stream(self.streams[r]):
+                sd = ShardedDeviceGraph(g, r, self.PARTS, device, backend="local")
+                sd._io()                        # fixes the part's stream: streams[r]
+                self.parts.append(sd)
+        self._ev = [[torch.cuda.Event() for _ in range(self.PARTS)] for _ in range(2)]   # packed, done
+        self.n_edges, self.n_nodes = g.n_edges, g.n_nodes
+
+    # ------------------------------------------------------------------ staging
+    def snapshot(self):
+        from .device import DeviceGraph
+        return [sd.d.snapshot(DeviceGraph.PASS_INPUTS) for sd in self.parts]
+
+    def stage_inputs(self, k: int):
+        for r, sd in enumerate(self.parts):
+            with self.torch.cuda.stream(self.streams[r]):
+                sd.d.stage_inputs(k)
+
+    def fill_inputs(self, snaps):
+        for r, sd in enumerate(self.parts):
+            with self.torch.cuda.stream(self.streams[r]):
+                sd.d.fill_inputs(snaps[r])
+
+    def use_inputs(self, i):
+        for sd in self.parts:
+            sd.d.use_inputs(i)
+
+    def clear_errors(self):
+        for r, sd in enumerate(self.parts):
+            with self.torch.cuda.stream(self.streams[r]):
+                sd.d.clear_errors()
+
+    def errors(self) -> int:
+        f = 0
+        for r, sd in enumerate(self.parts):
+            with self.torch.cuda.stream(self.streams[r]):
+                f |= sd.d.errors()
+        return f
+
+    # ------------------------------------------------------------------ the pass
+    def step(self, p, exchange=True, join=True):
+        """the pass of the whole event: both halves concurrently, then the halo exchange
+        through device memory, then the two streams join (every later call on either
+        stream sees the whole pass). exchange / join False: diagnostics timings only."""
+        (a, b), (sa, sb) = self.parts, self.streams
+        packed, done = self._ev
+        for r, sd in enumerate(self.parts):
+            sd.pass_(p)
+            if exchange:
+                sd.halo_pack()
+                packed[r].record(self.streams[r])
+        if exchange:
+            sa.wait_event(packed[1])
+            a.halo_unpack(ctypes.c_void_p(b.send_buf.data_ptr()))
+            sb.wait_event(packed[0])
+            b.halo_unpack(ctypes.c_void_p(a.send_buf.data_ptr()))
+        if join:
+            for r in range(self.PARTS):
+                done[r].record(self.streams[r])
+            sa.wait_event(done[1])   # the next pack on one stream must not overwrite a buffer the
+            sb.wait_event(done[0])   # other is still unpacking
+
+    def join(self, stream=None):
+        """make `stream` (default: the current one) wait for both halves"""
+        torch = self.torch
+        s = stream or torch.cuda.current_stream()
+        for r in range(self.PARTS):
+            e = torch.cuda.Event()
+            e.record(self.streams[r])
+            s.wait_event(e)
+
+    def download(self, g: TrackGraph) -> TrackGraph:
+        """every half's owned receivers (and their slots) from its replica, host order"""
+        from .graph import SLOT_FIELDS
+        from .device import MUTABLE_NODE, STATIC_SLOT
+        self.torch.cuda.synchronize()
+        for sd in self.parts:
+            h = sd.d.download(g.copy())
+            nodes, slots = sd.owned_host_nodes(), sd.owned_host_slots()
+            for f in MUTABLE_NODE:
+                g.node[f][nodes] = h.node[f][nodes]
+            for f in SLOT_FIELDS:
+                if f in STATIC_SLOT or f == "slot_key":
+                    continue
+                g.slot[f][slots] = h.slot[f][slots]
+        return g

@@ -44,7 +44,7 @@ inline int grid(int64_t n) { return (int)((n + BLOCK - 1) / BLOCK); }
 inline size_t al(size_t x) { return (x + 255) & ~size_t(255); }
 
 constexpr uint64_t NONE = ~uint64_t(0);
-constexpr int32_t ERR_DUP = 1, ERR_RANGE = 2, ERR_ASYM = 4;
+constexpr int32_t ERR_DUP = 1, ERR_RANGE = 2, ERR_ASYM = 4, ERR_OVER = 8;
 
 // final table size of a CPython 3.10 set after n distinct insertions (start 8, resize when
 // fill * 5 >= mask * 3 to the next power of two above 4 * fill, 2 * fill past 50000)
@@ -68,13 +68,18 @@ struct DevSet {
     int64_t* b;
     int64_t mask;
     int64_t fill;
+    int64_t cap;        // entries of each table (a resize beyond it sets `over` and stops)
+    bool over;
 
-    __device__ void init(int64_t* t0, int64_t* t1) {
+    __device__ void init(int64_t* t0, int64_t* t1, int64_t capacity) {
         a = t0;
         b = t1;
         mask = 7;
         fill = 0;
-        for (int i = 0; i < 8; i++) a[i] = -1;
+        cap = capacity;
+        over = capacity < 8;
+        if (!over)
+            for (int i = 0; i < 8; i++) a[i] = -1;
     }
     __device__ void insert_clean(int64_t key) {
         uint64_t perturb = (uint64_t)key;
@@ -91,6 +96,7 @@ struct DevSet {
     __device__ void resize(int64_t minused) {
         int64_t ns = 8;
         while (ns <= minused) ns <<= 1;
+        if (ns > cap) { over = true; return; }   // more distinct keys than the table was sized for
         int64_t* old = a;
         const int64_t om = mask;
         a = b;
@@ -101,6 +107,7 @@ struct DevSet {
             if (old[i] >= 0) insert_clean(old[i]);
     }
     __device__ void add(int64_t key) {
+        if (over) return;
         uint64_t perturb = (uint64_t)key;
         int64_t i = key & mask;
         for (;;) {
@@ -254,14 +261,14 @@ __global__ void k_comp_words(const int32_t* size, int32_t n_sub, int64_t n, int6
 __global__ void k_comp_order(const int32_t* memb, const int32_t* coff, const int32_t* size, int32_t n_sub, int64_t n,
                              const int32_t* gptr, const uint64_t* gkey, const int32_t* gdst, const int64_t* node_id,
                              const uint64_t* ids, const int32_t* idx, const int64_t* toff, int64_t* tbl,
-                             int32_t* queue, uint8_t* seen, int32_t* order) {
+                             int32_t* queue, uint8_t* seen, int32_t* order, int32_t* err) {
     const int32_t c = blockIdx.x * BLOCK + threadIdx.x;
     if (c >= n_sub || 2 * (int64_t)size[c] >= n) return;
     const int32_t lo = coff[c], sz = size[c];
     const int64_t cap = set_capacity(sz);
     int64_t* t = tbl + toff[c];
     DevSet s;
-    s.init(t, t + cap);
+    s.init(t, t + cap, cap);
     const int32_t root = memb[lo];
     int32_t head = lo, tail = lo;
     seen[root] = 1;
@@ -281,9 +288,10 @@ __global__ void k_comp_order(const int32_t* memb, const int32_t* coff, const int
     (void)gkey;
     DevSet shown;
     int64_t* spare = (s.a == t) ? t + cap : t;   // the first set's spare table
-    shown.init(spare, t + 2 * cap);
+    shown.init(spare, t + 2 * cap, cap);
     for (int64_t i = 0; i <= s.mask; i++)
         if (s.a[i] >= 0) shown.add(s.a[i]);
+    if (s.over || shown.over) { atomicOr(err, ERR_OVER); return; }
     int32_t r = lo;
     for (int64_t i = 0; i <= shown.mask; i++)
         if (shown.a[i] >= 0) order[r++] = find_id(ids, idx, (int32_t)n, shown.a[i]);
@@ -343,12 +351,13 @@ __global__ void k_tse_rank(const int32_t* order, int64_t n, const int32_t* slot_
     const int32_t b = slot_ptr[p], e = slot_ptr[p + 1], u = order[p];
     const int64_t cap = set_capacity(e - b);
     DevSet s;
-    s.init(tbl + toff[p], tbl + toff[p] + cap);
+    s.init(tbl + toff[p], tbl + toff[p] + cap, cap);
     for (int32_t k = b; k < e; k++) {
         s.add(node_id[order[slot_src[k]]]);
         tse_rank[k] = -1;
     }
     for (int32_t j = gptr[u]; j < gptr[u + 1]; j++) s.add(node_id[gdst[j]]);
+    if (s.over) { atomicOr(err, ERR_OVER); return; }
     int32_t r = 0;
     for (int64_t i = s.mask; i >= 0; i--) {   // reversed iteration order
         if (s.a[i] < 0) continue;
@@ -541,7 +550,7 @@ int gtf_build_event_csr_device(gtf_event_csr* ev, void* workspace, size_t worksp
     if ((size_t)words > w.tbl_words) return fail("gtf_build_event_csr_device: set tables exceed the workspace bound");
     GTF_CK(hipMemsetAsync(w.seen, 0, N, st), "memset");
     hipLaunchKernelGGL(k_comp_order, dim3(grid(n_sub)), dim3(BLOCK), 0, st, w.memb, w.coff, w.size, n_sub, N, w.gptr,
-                       gkey, gdst, ev->node_id, w.ids, w.idx, w.toff, w.tbl, w.queue, w.seen, ev->order);
+                       gkey, gdst, ev->node_id, w.ids, w.idx, w.toff, w.tbl, w.queue, w.seen, ev->order, w.scal);
     hipLaunchKernelGGL(k_pos, dim3(grid(N)), dim3(BLOCK), 0, st, ev->order, w.comp, N, w.pos, ev->sub_id);
     // 5. slots: (packed receiver, packed sender) in order; the out-lists; the key orders
     GTF_CK(hipMemsetAsync(w.rdeg, 0, 4 * (N + 1), st), "memset");
@@ -570,6 +579,10 @@ int gtf_build_event_csr_device(gtf_event_csr* ev, void* workspace, size_t worksp
     GTF_CK(hipGetLastError(), "launch");
     GTF_CK(hipMemcpyAsync(scal, w.scal, 4, hipMemcpyDeviceToHost, st), "read");
     GTF_CK(hipStreamSynchronize(st), "sync");
+    if (scal[0] & ERR_OVER) {
+        gtf::set_error("gtf_build_event_csr_device: a set held more keys than its table was sized for");
+        return -1;
+    }
     if (scal[0] & ERR_ASYM) {
         gtf::set_error("gtf_build_event_csr_device: neighbour without an in-edge (graph not symmetric)");
         return -1;

@@ -166,6 +166,23 @@ def dropin_stage_wall(params, reps=3):
         out = json.loads(r.stdout)
         runs = out["runs"]
         med = sorted(runs, key=lambda x: x["wall_s"])[len(runs) // 2]
+        # the CLI as run_gnn_trackml_mod.sh calls it: one fresh process per stage, whole
+        # wall time (interpreter, imports, worker pool, GPU context, stage, exit); the lean
+        # runtime (no torch, gtf.devmem) vs the same CLI made to hold torch
+        cli = [sys.executable, os.path.join(ROOT, "gnn-track-finding_amd", "extrapolate", "extrapolate_merged_states.py"),
+               "-i", ind, "-o", outd, "-c", str(params.chi2_cut), "-e", str(params.sigma0xy), "-z",
+               str(params.sigma0rz), "-m", str(params.sigma0rz2), "-b", str(params.endcap_boundary)]
+        cli_s = {}
+        for mem, n in (("hip", 3), ("torch", 1)):
+            ts = []
+            for _ in range(n):
+                t0 = time.perf_counter()
+                rc = subprocess.run(cli, env=dict(env, GTF_DROPIN_MEM=mem), cwd=ROOT, capture_output=True,
+                                    text=True, timeout=600)
+                ts.append(time.perf_counter() - t0)
+                if rc.returncode != 0:
+                    return {"error": "CLI (%s): %s" % (mem, rc.stderr[-400:])}
+            cli_s[mem] = sorted(ts)[len(ts) // 2]
         return {"stage": "extrapolate (drop-in runner gtf.dropin.run_dir, child process)",
                 "input": "vol-7 134 full load", "subgraphs": len(graphs), "edges": edges,
                 "wall_s": med["wall_s"], "edges_per_s": edges / med["wall_s"], "workers": med["workers"],
@@ -174,7 +191,12 @@ def dropin_stage_wall(params, reps=3):
                 "device_phases_s": med.get("device_phases_s"),
                 "first_run_wall_s": out["first"]["wall_s"],
                 "first_run_note": "the first directory of the process: forks the worker pool (after importing "
-                                  "what the pickles need), creates the GPU context, loads code; the CLI's case",
+                                  "what the pickles need), creates the GPU context, loads code",
+                "cli_process_wall_s": cli_s["hip"], "cli_edges_per_s": edges / cli_s["hip"],
+                "cli_process_wall_s_with_torch": cli_s["torch"],
+                "cli_note": "extrapolate_merged_states.py -i -o -c -e -z -m -b in a fresh process, whole wall time "
+                            "(median of 3); its device arrays come from libgtf (gtf.devmem), no torch in the process; "
+                            "_with_torch: the same CLI holding torch tensors (GTF_DROPIN_MEM=torch)",
                 "reference_as_is_edges_per_s": 788, "reference_prints_stubbed_edges_per_s": 5367}
     finally:
         shutil.rmtree(tmp, ignore_errors=True)

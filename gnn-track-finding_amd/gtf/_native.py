@@ -146,6 +146,8 @@ SYMBOLS = ["gtf_workspace_bytes", "gtf_clear_errors", "gtf_read_errors", "gtf_ex
            "gtf_extract_candidates", "gtf_build_event_csr", "gtf_candidate_order",
            "gtf_build_event_device_workspace_bytes", "gtf_build_event_csr_device",
            "gtf_updated_state_pair_counts", "gtf_updated_state_distances", "gtf_set_diagnostics",
+           "gtf_device_init", "gtf_malloc", "gtf_free", "gtf_memcpy_htod", "gtf_memcpy_dtoh", "gtf_memcpy_dtod",
+           "gtf_memset", "gtf_stream_synchronize",
            "gtf_last_error",
            "gtf_version"]
 
@@ -153,20 +155,33 @@ OPS = {"ranks": 1, "priors_tse": 2, "priors_uts": 3, "reweight_uts": 4, "degree"
        "mw_uts": 8, "cluster_tse": 9, "cluster_uts": 10, "fresh": 11}
 
 _lib = None
+_lean = False   # loaded without torch (lean=True): only gtf.devmem allocations may be used
 
 
-def lib():
-    """Load libgtf.so once; raise loudly if it is missing (no fallback path)."""
-    global _lib
+def lib(lean: bool = False):
+    """Load libgtf.so once; raise loudly if it is missing (no fallback path).
+
+    lean=False (default): torch is imported first, so its bundled libamdhip64 (SONAME
+    libamdhip64.so.7) satisfies libgtf's NEEDED entry and the process holds ONE HIP
+    runtime, which torch tensors and libgtf share. Loaded the other way round, torch
+    pulls a second runtime and libgtf's calls see no device.
+    lean=True (the drop-in CLIs, gtf.devmem): torch is not imported; libgtf binds the
+    system HIP runtime and every allocation comes from gtf_malloc. A process that loaded
+    libgtf this way cannot use torch device tensors with it afterwards (lib() raises)."""
+    global _lib, _lean
     if _lib is not None:
+        if _lean and not lean:
+            raise RuntimeError("libgtf was loaded without torch (gtf.devmem, the drop-in CLIs' lean runtime); "
+                               "torch device tensors cannot share it in this process")
         return _lib
     if not os.path.exists(LIB_PATH):
         raise RuntimeError("libgtf.so not built at %s -- run __graft_entry__.build() "
                            "(hipcc --offload-arch=gfx950); there is no CPU fallback" % LIB_PATH)
-    # torch first: its bundled libamdhip64 (SONAME libamdhip64.so.7) then satisfies
-    # libgtf's NEEDED entry, so the process holds ONE HIP runtime. Loaded the other way
-    # round, torch pulls a second runtime and libgtf's calls see no device.
-    import torch  # noqa: F401
+    import sys
+    if lean and "torch" not in sys.modules:
+        _lean = True
+    else:
+        import torch  # noqa: F401
     L = ctypes.CDLL(LIB_PATH)
     L.gtf_workspace_bytes.restype = ctypes.c_size_t
     L.gtf_workspace_bytes.argtypes = [I32, I32]
@@ -205,6 +220,13 @@ def lib():
     L.gtf_candidate_order.argtypes = [ctypes.POINTER(GtfCandidateGraph), P]
     L.gtf_updated_state_pair_counts.argtypes = [G, N, S, E, P, P]
     L.gtf_updated_state_distances.argtypes = [G, N, S, E, P, P, ctypes.POINTER(GtfPairOut), P]
+    L.gtf_device_init.argtypes = [I32]
+    L.gtf_malloc.argtypes = [ctypes.POINTER(P), ctypes.c_size_t]
+    L.gtf_free.argtypes = [P]
+    for fn in ("gtf_memcpy_htod", "gtf_memcpy_dtoh", "gtf_memcpy_dtod"):
+        getattr(L, fn).argtypes = [P, P, ctypes.c_size_t, P]
+    L.gtf_memset.argtypes = [P, I32, ctypes.c_size_t, P]
+    L.gtf_stream_synchronize.argtypes = [P]
     L.gtf_last_error.restype = ctypes.c_char_p
     L.gtf_version.restype = ctypes.c_char_p
     for fn in ("gtf_clear_errors", "gtf_read_errors", "gtf_extrapolate", "gtf_update", "gtf_cluster", "gtf_pass",
@@ -212,7 +234,8 @@ def lib():
                "gtf_tag_prepare", "gtf_tag_sweep", "gtf_parabolic_kl", "gtf_track_state_estimates", "gtf_pass_shard", "gtf_shard_pack",
                "gtf_shard_unpack", "gtf_halo_pack", "gtf_halo_unpack", "gtf_extract_candidates", "gtf_build_event_csr",
                "gtf_candidate_order", "gtf_updated_state_pair_counts", "gtf_updated_state_distances",
-               "gtf_set_diagnostics", "gtf_build_event_csr_device"):
+               "gtf_set_diagnostics", "gtf_build_event_csr_device", "gtf_device_init", "gtf_malloc", "gtf_free",
+               "gtf_memcpy_htod", "gtf_memcpy_dtoh", "gtf_memcpy_dtod", "gtf_memset", "gtf_stream_synchronize"):
         getattr(L, fn).restype = ctypes.c_int
     _lib = L
     return L
@@ -220,4 +243,4 @@ def lib():
 
 def check(rc):
     if rc != 0:
-        raise RuntimeError("libgtf: %s (rc=%d)" % (lib().gtf_last_error().decode(), rc))
+        raise RuntimeError("libgtf: %s (rc=%d)" % ((_lib or lib()).gtf_last_error().decode(), rc))

@@ -126,8 +126,14 @@ class DeviceGraph:
     stage methods are layout-independent (the pass is equivariant under renumber)."""
 
     def __init__(self, g: TrackGraph, device: str = "cuda", schedule: bool = True, layout: str = "natural",
-                 pack: bool = False, tile: int = TILE):
-        torch = _torch()
+                 pack: bool = False, tile: int = TILE, mem: str = "torch"):
+        """mem "torch": the arrays are torch tensors (every method). mem "hip": plain
+        allocations from libgtf (gtf.devmem, no torch in the process): the stage methods,
+        clear_errors / errors and download only -- the drop-in CLIs' path."""
+        if mem not in ("torch", "hip"):
+            raise ValueError("mem must be 'torch' or 'hip'")
+        self.mem = mem
+        torch = _torch() if mem == "torch" else None
         self.layout = layout
         self.order = self.slot_perm = None
         self.pad_plan = None
@@ -140,8 +146,13 @@ class DeviceGraph:
             raise ValueError("layout must be 'natural', 'schedule', 'tiled' or 'padded'")
         self.slot_ptr_host = g.slot_ptr
         self.torch = torch
-        self.device = torch.device(device)
-        self.lib = nat.lib()
+        if torch is not None:
+            self.device = torch.device(device)
+            self.lib = nat.lib()
+        else:
+            self.device = device
+            self.lib = nat.lib(lean=True)
+            nat.check(self.lib.gtf_device_init(int(device.split(":")[1]) if ":" in device else 0))
         self.n_nodes, self.n_slots, self.n_edges = g.n_nodes, g.n_slots, g.n_edges
         self.t = {}
         up = self._up
@@ -149,7 +160,8 @@ class DeviceGraph:
         up("out_ptr", g.out_ptr.astype(np.int32))
         up("out_slot", g.out_slot.astype(np.int32))
         up("slot_dst", g.slot_dst().astype(np.int32))
-        up("out_dst", g.slot_dst()[g.out_slot].astype(np.int32) if g.n_edges else np.zeros(0, np.int32))
+        out_dst = g.slot_dst()[g.out_slot].astype(np.int32) if g.n_edges else np.zeros(0, np.int32)
+        up("out_dst", out_dst)
         src = g.slot["slot_src"].astype(np.int64)
         up("slot_layer", np.where(src >= 0, g.node["layer"][np.maximum(src, 0)] if g.n_nodes else np.nan,
                                   np.nan).astype(np.float64))
@@ -186,7 +198,7 @@ class DeviceGraph:
         up("sched_seg", sched_segments(g.slot_ptr, sched))
         osched, self.n_o = sender_schedule(g.out_ptr)
         up("out_sched", osched)
-        up("out_lanes", sender_lanes(g.out_slot, self.t["out_dst"].cpu().numpy(), osched, self.n_o))
+        up("out_lanes", sender_lanes(g.out_slot, out_dst, osched, self.n_o))
         self.n_pack_waves = 0
         if pack:   # the packed lane segments are built only when asked for
             pent, pwave = pack_schedule(g.slot_ptr)
@@ -203,10 +215,18 @@ class DeviceGraph:
             if f in ("slot_key",):
                 continue
             up(f, g.slot[f])
-        self._make_arena(self.PASS_INPUTS)
         self._staged, self._resident = [], None   # stage_inputs() copies
         ws_bytes = int(self.lib.gtf_workspace_bytes(g.n_nodes, g.n_slots))
-        self.t["ws"] = torch.zeros(ws_bytes, dtype=torch.uint8, device=self.device)
+        if torch is not None:
+            self._make_arena(self.PASS_INPUTS)
+            self.t["ws"] = torch.zeros(ws_bytes, dtype=torch.uint8, device=self.device)
+        else:   # (no arena: snapshots and staged inputs are benchmark tools, torch only)
+            from .devmem import HipArray
+            self.arena = None
+            self.t["ws"] = HipArray.zeros(ws_bytes, np.uint8)
+            nat.check(self.lib.gtf_stream_synchronize(None))   # the uploads' host buffers may go
+            for t in self.t.values():
+                t._pending = None
         self._build_structs(pack)
 
     # ---------------------------------------------------------------- memory
@@ -231,8 +251,21 @@ class DeviceGraph:
 
     def _up(self, name, arr):
         arr = np.ascontiguousarray(arr)
+        if self.torch is None:
+            from .devmem import HipArray
+            self.t[name] = HipArray.from_numpy(arr)
+            return
         t = self.torch.from_numpy(arr.reshape(-1) if arr.size else arr.reshape(0)).to(self.device)
         self.t[name] = t
+
+    def _np(self, t):
+        """host copy of a device array (synchronises)"""
+        return t.numpy() if self.torch is None else t.cpu().numpy()
+
+    def _need_torch(self, what):
+        if self.torch is None:
+            raise NotImplementedError("%s needs DeviceGraph(mem='torch'); mem='hip' carries the stage methods, "
+                                      "errors and download only" % what)
 
     def ptr(self, name):
         t = self.t[name]
@@ -274,6 +307,8 @@ class DeviceGraph:
 
     @property
     def stream(self):
+        if self.torch is None:
+            return ctypes.c_void_p(0)   # mem "hip": the default stream
         return ctypes.c_void_p(self.torch.cuda.current_stream(self.device).cuda_stream)
 
     @staticmethod
@@ -352,6 +387,7 @@ class DeviceGraph:
         host_order=False in the device layout's order (no gathers: what a caller that keeps
         the event on the device consumes)."""
         self._natural_only("track_state_estimates")
+        self._need_torch("track_state_estimates")
         torch = self.torch
         N = self.n_nodes
         nan = float("nan")
@@ -380,6 +416,7 @@ class DeviceGraph:
         order. truth: [N] truth_particle per node (host or device), or None. host_order=False:
         the node segments in the device layout's node order (no reordering gathers)."""
         self._natural_only("updated_state_distances")
+        self._need_torch("updated_state_distances")
         torch = self.torch
         dev = self.device
         N = self.n_nodes
@@ -427,6 +464,7 @@ class DeviceGraph:
     def tag_propagation(self, tags, radius, threshold=0.1, max_sweeps=100000):
         """Jacobi sweeps until flips / processed <= threshold (tag_propagation.py:137)."""
         self._natural_only("tag_propagation")
+        self._need_torch("tag_propagation")
         torch = self.torch
         dev = self.device
         E = self.n_edges
@@ -464,6 +502,7 @@ class DeviceGraph:
         extrapolated edge (the values extrapolate_merged_states.py:134-172 prints to CSV).
         Off by default and never on the benchmark's path; set_diagnostics(False, False)
         unregisters them."""
+        self._need_torch("set_diagnostics")
         torch = self.torch
         self.diag_t = {}
         if node_err:
@@ -513,7 +552,7 @@ class DeviceGraph:
         nm = None if self.order is None else self.order >= 0          # (padded: not a dummy node)
         sm = None if self.slot_perm is None else self.slot_perm >= 0  # (padded: not a padding slot)
         for f in MUTABLE_NODE:
-            a = self.t[f].cpu().numpy().reshape((-1,) + g.node[f].shape[1:])
+            a = self._np(self.t[f]).reshape((-1,) + g.node[f].shape[1:])
             if self.order is None:
                 g.node[f][...] = a
             else:
@@ -521,7 +560,7 @@ class DeviceGraph:
         for f in SLOT_FIELDS:
             if f in STATIC_SLOT or f == "slot_key":
                 continue
-            a = self.t[f].cpu().numpy().reshape((-1,) + g.slot[f].shape[1:])
+            a = self._np(self.t[f]).reshape((-1,) + g.slot[f].shape[1:])
             if self.slot_perm is None:
                 g.slot[f][...] = a
             else:
@@ -554,6 +593,7 @@ class DeviceGraph:
     def snapshot(self, names=None):
         """device-side copy of mutable arrays (default: every one). The pass inputs
         (PASS_INPUTS) live in one arena and snapshot as a single buffer."""
+        self._need_torch("snapshot")
         if names is not None and tuple(names) == tuple(self.PASS_INPUTS):
             return {"__arena__": self.arena.clone()}
         names = names or [k for k in self.t if k in MUTABLE_NODE or
@@ -575,6 +615,7 @@ class DeviceGraph:
         a restore copy between them: use_inputs(i) points every stage method at copy i
         (None: the arrays of this graph). The arrays outside the arena (state values,
         degree) are shared: a pass overwrites every value it reads back."""
+        self._need_torch("stage_inputs")
         if self._resident is None:
             self._resident = (self.cn, self.cuts, self.ctse, self.ce)
         self.use_inputs(None)

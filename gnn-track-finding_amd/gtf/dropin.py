@@ -11,7 +11,9 @@ time"). Here the files are split into contiguous chunks, one per worker process:
 
   worker w: unpickle its files -> pack them (gtf.graph.pack) -> send the packed arrays
   main:     concatenate the chunks (gtf.graph.concat) -> one device stage call ->
-            send each worker the mutable arrays of its node / slot range
+            send each worker the mutable arrays of its node / slot range (device
+            arrays from libgtf's own allocator, gtf.devmem, unless the process already
+            holds torch: device_memory())
   worker w: write them back into its graphs (gtf.graph.unpack) -> pickle each graph to
             the output directory under its global glob index
 
@@ -48,6 +50,33 @@ def default_workers() -> int:
         n = os.cpu_count() or 1
     env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
     return max(1, min(n, env) if env else min(n, 16))
+
+
+def device_memory() -> str:
+    """DeviceGraph's allocator for a directory: "hip" (gtf.devmem, libgtf's own runtime,
+    no torch) unless this process already imported torch, whose runtime libgtf then shares
+    ("torch"). A drop-in CLI never imports torch: bringing it up costs 1.9-2.0 s of the
+    extrapolation CLI's 2.3 s on the MI355X box (tools/cold_start.py).
+    GTF_DROPIN_MEM=torch|hip overrides."""
+    import sys
+    m = os.environ.get("GTF_DROPIN_MEM", "")
+    if m in ("torch", "hip"):
+        return m
+    return "torch" if "torch" in sys.modules else "hip"
+
+
+def _warm_device():
+    """load libgtf lean and create the device context (one small allocation)"""
+    import ctypes
+    from . import _native as nat
+    try:
+        L = nat.lib(lean=True)
+        if L.gtf_device_init(0) == 0:
+            p = ctypes.c_void_p()
+            if L.gtf_malloc(ctypes.byref(p), 256) == 0:
+                L.gtf_free(p)
+    except Exception:   # DeviceGraph reports any failure itself
+        pass
 
 
 def _chunks(n_files: int, workers: int):
@@ -176,6 +205,13 @@ def run_dir(input_dir: str, output_dir: str, body: Callable, *, states=("tse", "
     chunks = _chunks(len(files), workers)
     pool = _get_pool(workers, files[0] if files else None)
     conns = pool.conns[:len(chunks)]
+    warm = None
+    if host_stage is None and files and device_memory() == "hip":
+        # bring the HIP runtime up while the workers read (after the fork: a fork of a
+        # process that holds a GPU context slows its later copies, _Pool)
+        import threading
+        warm = threading.Thread(target=_warm_device, daemon=True)
+        warm.start()
     try:
         for c, (lo, hi) in zip(conns, chunks):
             c.send((files[lo:hi], lo, output_dir, tuple(states), merged))
@@ -199,10 +235,12 @@ def run_dir(input_dir: str, output_dir: str, body: Callable, *, states=("tse", "
             out_node, out_slot = g.node, g.slot
         elif nonempty:
             from .device import DeviceGraph
+            if warm is not None:
+                warm.join()
             tp = [time.perf_counter()]
             g = concat(nonempty)
             tp.append(time.perf_counter())
-            d = DeviceGraph(g)
+            d = DeviceGraph(g, mem=device_memory())
             tp.append(time.perf_counter())
             d.clear_errors()
             body(d)

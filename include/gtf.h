@@ -549,6 +549,21 @@ typedef struct gtf_candidate_graph {
 
 int gtf_candidate_order(const gtf_candidate_graph* cg, int32_t* order_key);
 
+/* Device memory for a host without a framework allocator (csrc/gtf_mem.hip): the drop-in
+ * stage CLIs (extrapolate_merged_states.py:521-572, clustering.py:380-415,
+ * remove_state_metadata.py:11-57 -- one process per stage and iteration) allocate and
+ * copy through the HIP runtime libgtf is linked against instead of loading a framework
+ * (gtf/devmem.py). Copies are stream-ordered; gtf_memcpy_dtoh synchronises the stream.
+ * gtf_malloc(…, 0) returns a valid 256-byte allocation (never a null pointer). */
+int gtf_device_init(int32_t device);
+int gtf_malloc(void** ptr, size_t bytes);
+int gtf_free(void* ptr);
+int gtf_memcpy_htod(void* dst, const void* src, size_t bytes, gtf_stream_t stream);
+int gtf_memcpy_dtoh(void* dst, const void* src, size_t bytes, gtf_stream_t stream);
+int gtf_memcpy_dtod(void* dst, const void* src, size_t bytes, gtf_stream_t stream);
+int gtf_memset(void* dst, int32_t value, size_t bytes, gtf_stream_t stream);
+int gtf_stream_synchronize(gtf_stream_t stream);
+
 const char* gtf_last_error(void);
 const char* gtf_version(void);
 

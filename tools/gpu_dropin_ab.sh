@@ -1,7 +1,7 @@
 #!/bin/bash
 # drop-in stage timing (bench.dropin_stage_wall), twice
 set -o pipefail
-O=gpurun_out/dropin_ab2
+O=gpurun_out/dropin_ab3
 mkdir -p $O
 for i in 1 2; do
   timeout -k 10 200 python -u -c "

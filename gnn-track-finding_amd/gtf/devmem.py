@@ -19,6 +19,17 @@ import numpy as np
 from . import _native as nat
 
 
+def default_mem() -> str:
+    """the allocator a stage entry point picks when the caller gives none: "hip" in a
+    process that has not imported torch (a drop-in CLI), else "torch", whose HIP runtime
+    libgtf then shares. GTF_DROPIN_MEM=torch|hip overrides."""
+    import os
+    m = os.environ.get("GTF_DROPIN_MEM", "")
+    if m in ("torch", "hip"):
+        return m
+    return "torch" if "torch" in sys.modules else "hip"
+
+
 class HipArray:
     """a 1-D device array: an owning allocation, or a view into one (arena members)"""
 

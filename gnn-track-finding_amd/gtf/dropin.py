@@ -58,11 +58,8 @@ def device_memory() -> str:
     ("torch"). A drop-in CLI never imports torch: bringing it up costs 1.9-2.0 s of the
     extrapolation CLI's 2.3 s on the MI355X box (tools/cold_start.py).
     GTF_DROPIN_MEM=torch|hip overrides."""
-    import sys
-    m = os.environ.get("GTF_DROPIN_MEM", "")
-    if m in ("torch", "hip"):
-        return m
-    return "torch" if "torch" in sys.modules else "hip"
+    from .devmem import default_mem
+    return default_mem()
 
 
 def _warm_device():

@@ -44,11 +44,10 @@ def run(g: TrackGraph, vivl, params: Params, order_key=None, device="cuda", d=No
     if params.numhits < 3:
         raise ValueError("numhits must be >= 3 (rotate_track reads three hits)")
     if d is None:
-        d = DeviceGraph(g, device)
+        from .devmem import default_mem
+        d = DeviceGraph(g, device, mem=default_mem())
     elif d.n_nodes != g.n_nodes or d.n_slots != g.n_slots:
         raise ValueError("DeviceGraph does not hold this graph")
-    torch = d.torch
-    dev = d.device
     N = g.n_nodes
     sub = g.node["sub_id"].astype(np.int32)
     if N and (np.any(np.diff(sub) < 0) or sub[0] != 0 or np.any(np.diff(sub) > 1)):
@@ -56,17 +55,18 @@ def run(g: TrackGraph, vivl, params: Params, order_key=None, device="cuda", d=No
                          "as pack() numbers them")
     n_sub = int(sub.max()) + 1 if N else 0
     sub_ptr = np.searchsorted(sub, np.arange(n_sub + 1)).astype(np.int32)
-    up = lambda a, dt=None: torch.from_numpy(np.ascontiguousarray(a if dt is None else a.astype(dt))).to(dev)  # noqa
+    n1 = max(N, 1)
+    up = lambda a, dt=None: _up(d, np.asarray(a) if dt is None else np.asarray(a).astype(dt))  # noqa: E731
     t = {"xyzr": up(g.node["xyzr"], np.float64), "vivl": up(np.asarray(vivl), np.float64), "sub": up(sub),
          "sub_ptr": up(sub_ptr), "gnn": up(g.node["gnn"], np.float64),
          "order": up(np.asarray(order_key), np.int32) if order_key is not None else None,
-         "label": torch.empty(max(N, 1), dtype=torch.int32, device=dev),
-         "status": torch.full((max(N, 1),), -1, dtype=torch.int8, device=dev),
-         "pxy": torch.full((max(N, 1),), float("nan"), dtype=torch.float64, device=dev),
-         "pzr": torch.full((max(N, 1),), float("nan"), dtype=torch.float64, device=dev),
-         "ext": torch.zeros(max(N, 1), dtype=torch.uint8, device=dev),
-         "ncand": torch.zeros(1, dtype=torch.int32, device=dev)}
-    ws = torch.zeros(int(d.lib.gtf_extract_workspace_bytes(N, n_sub)), dtype=torch.uint8, device=dev)
+         "label": up(np.zeros(n1, np.int32)),
+         "status": up(np.full(n1, -1, np.int8)),
+         "pxy": up(np.full(n1, np.nan)),
+         "pzr": up(np.full(n1, np.nan)),
+         "ext": up(np.zeros(n1, np.uint8)),
+         "ncand": up(np.zeros(1, np.int32))}
+    ws = _zeros(d, int(d.lib.gtf_extract_workspace_bytes(N, n_sub)))
     vp = lambda x: ctypes.c_void_p(x.data_ptr() if x is not None and x.numel() else 0)  # noqa: E731
     io = nat.GtfExtractIO(vp(t["xyzr"]), vp(t["vivl"]), vp(t["sub"]), vp(t["sub_ptr"]), n_sub, 0, vp(t["order"]),
                           vp(t["gnn"]), vp(t["label"]), vp(t["status"]), vp(t["pxy"]), vp(t["pzr"]),
@@ -74,10 +74,26 @@ def run(g: TrackGraph, vivl, params: Params, order_key=None, device="cuda", d=No
     cp = params.c()
     nat.check(d.lib.gtf_extract_candidates(ctypes.byref(d.cg), ctypes.byref(d.ce), ctypes.byref(io),
                                            ctypes.byref(cp), vp(ws), d.stream))
-    out = {k: t[k][:N].cpu().numpy() for k in ("label", "status", "pxy", "pzr", "ext")}
-    out["gnn"] = t["gnn"].cpu().numpy().reshape(-1, 4)[:N]
-    out["n_candidates"] = int(t["ncand"].item())
+    out = {k: d._np(t[k])[:N] for k in ("label", "status", "pxy", "pzr", "ext")}
+    out["gnn"] = d._np(t["gnn"]).reshape(-1, 4)[:N]
+    out["n_candidates"] = int(d._np(t["ncand"])[0])
     return out
+
+
+def _up(d, a):
+    """a host array as a device array of d's allocator (torch tensor or gtf.devmem)"""
+    a = np.ascontiguousarray(a).reshape(-1)
+    if d.torch is None:
+        from .devmem import HipArray
+        return HipArray.from_numpy(a)
+    return d.torch.from_numpy(a).to(d.device)
+
+
+def _zeros(d, nbytes):
+    if d.torch is None:
+        from .devmem import HipArray
+        return HipArray.zeros(nbytes, np.uint8)
+    return d.torch.zeros(nbytes, dtype=d.torch.uint8, device=d.device)
 
 
 def candidate_order(g: TrackGraph) -> np.ndarray:
@@ -94,7 +110,7 @@ def candidate_order(g: TrackGraph) -> np.ndarray:
     cg = nat.GtfCandidateGraph(N, g.n_slots, g.n_edges, 0, vp(a["slot_ptr"]), vp(a["slot_src"]), vp(a["is_edge"]),
                                vp(a["act"]), vp(a["out_ptr"]), vp(a["out_slot"]), vp(a["sub_id"]), vp(a["node_id"]))
     out = np.zeros(max(N, 1), np.int32)
-    nat.check(nat.lib().gtf_candidate_order(ctypes.byref(cg), vp(out)))
+    nat.check(nat.lib(lean=True).gtf_candidate_order(ctypes.byref(cg), vp(out)))   # host code: no torch needed
     return out[:N]
 
 

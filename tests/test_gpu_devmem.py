@@ -98,3 +98,38 @@ def test_clustering_cli_without_torch(tmp_path):
                   str(tmp_path))
     errs = graphs_equal(_read(str(tmp_path / "out")), d["out"])
     assert errs == [], "\n".join(errs[:20])
+
+
+def test_extract_cli_without_torch(tmp_path):
+    """the extraction CLI (GPU CCA + fits) in a torch-free process: the reference's
+    candidate, remaining and fragment files (counts and node lists; test_dropin.py checks
+    every attribute of the same run on the default path)"""
+    import pickle
+    d = _load("extract")
+    a = d["args"]
+    dirs = {k: str(tmp_path / k) + "/" for k in ("in", "cand", "rem", "frag")}
+    for v in dirs.values():
+        os.makedirs(v)
+    for i, s in enumerate(d["input"]):
+        with open(dirs["in"] + "%d_subgraph.gpickle" % i, "wb") as f:
+            pickle.dump(s, f, pickle.HIGHEST_PROTOCOL)
+    _cli_no_torch("extract/extract_track_candidates.py",
+                  ["-i", dirs["in"], "-c", dirs["cand"], "-r", dirs["rem"], "-f", dirs["frag"], "-p", str(a["p"]),
+                   "-n", str(a["n"]), "-s", str(a["s"]), "-t", str(a["t"]), "-a", str(a["a"]),
+                   "-e", str(d["P"]["sigma0xy"]), "-z", str(d["P"]["sigma0rz"]), "-b", str(d["P"]["endcap_boundary"])],
+                  str(tmp_path))
+    for key, dd in (("candidates", "cand"), ("remaining", "rem"), ("fragments", "frag")):
+        got = _read_numbered(dirs[dd])
+        assert len(got) == len(d[key]), key
+        for gs, es in zip(got, d[key]):
+            assert list(gs.nodes) == list(es.nodes), key
+
+
+def _read_numbered(dd):
+    import pickle
+    out, i = [], 0
+    while os.path.isfile(dd + "%d_subgraph.gpickle" % i):
+        with open(dd + "%d_subgraph.gpickle" % i, "rb") as f:
+            out.append(pickle.load(f))
+        i += 1
+    return out

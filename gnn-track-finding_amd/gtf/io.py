@@ -12,7 +12,8 @@ is assembled vectorised. Semantics kept:
   (helper.py:537-543); both directions are added when both ends are kept
   (helper.py:512-518).
 
-Truth joins (particle ids, module ids) are not on the hot path and are not built.
+Truth joins (particle ids, module ids) are not on the packed path; build_networkx adds
+them to the networkx graph the drop-in event conversion writes.
 """
 from __future__ import annotations
 
@@ -29,8 +30,19 @@ def read_nodes(path: str, min_volume: int, max_volume: int):
     lid = a["layer_id"].to_numpy()
     keep = (lid >= lo) & (lid <= hi)
     x, y, z = (a[c].to_numpy(np.float64)[keep] for c in ("x", "y", "z"))
-    return (a["node_idx"].to_numpy(np.int64)[keep], x, y, z, np.sqrt(x**2 + y**2),
-            lid[keep].astype(np.int64))
+    return (a["node_idx"].to_numpy(np.int64)[keep], x, y, z, edge_length_xy(x, y), lid[keep].astype(np.int64))
+
+
+def edge_length_xy(x, y):
+    """helper.edge_length_xy (helper.py:12-13) as the reference evaluates it, on numpy
+    float64 scalars of a DataFrame row: ``row.x**2`` is the C library's pow(x, 2), which
+    differs from x * x in the last bit for some x (6 of the 8,748 vol-7 hits), where numpy's
+    array power squares; so the squares go through math.pow (the same pow)."""
+    import math
+    sq = np.frompyfunc(math.pow, 2, 1)
+    x2 = sq(np.asarray(x, np.float64), 2.0).astype(np.float64)
+    y2 = sq(np.asarray(y, np.float64), 2.0).astype(np.float64)
+    return np.sqrt(x2 + y2)
 
 
 def read_edges(path: str):
@@ -81,25 +93,92 @@ def read_truth(path: str, node_ids: np.ndarray) -> np.ndarray:
     return out
 
 
-def build_networkx(event_prefix: str, min_volume: int, max_volume: int, truth_csv: str = None):
+def aggregate_truth(event_path: str, truth_event_path: str, truth_event_file: str) -> None:
+    """helper.load_save_truth (helper.py:548-582) without its per-row pandas lookups: one
+    row per nodes_to_hits row (its order), with the hit's particle (truth.csv) and its
+    volume / layer / module (hits.csv) -- each hit must occur exactly once in those files,
+    where the reference's ``.item()`` raises ValueError otherwise -- and the particle's
+    nhits from particles.csv, 0.0 where the particle is absent or listed twice (the
+    reference's ``except ValueError``). Written as the reference writes it (nhits float)."""
+    import pandas as pd
+    hits_particles = pd.read_csv(truth_event_path + "truth.csv")
+    particles_nhits = pd.read_csv(truth_event_path + "particles.csv")
+    hits_module_id = pd.read_csv(truth_event_path + "hits.csv")
+    nodes_hits = pd.read_csv(event_path + "nodes_to_hits.csv")
+    hit = nodes_hits["hit_id"]
+
+    def lookup(df, col):
+        cnt = hit.map(df["hit_id"].value_counts()).fillna(0)
+        if (cnt != 1).any():
+            raise ValueError("can only convert an array of size 1 to a Python scalar (hit_id %d)"
+                             % int(hit[cnt != 1].iloc[0]))
+        return hit.map(df.drop_duplicates("hit_id").set_index("hit_id")[col])
+
+    truth = pd.DataFrame({"node_idx": nodes_hits["node_idx"], "hit_id": hit,
+                          "particle_id": lookup(hits_particles, "particle_id"),
+                          "volume_id": lookup(hits_module_id, "volume_id"),
+                          "layer_id": lookup(hits_module_id, "layer_id"),
+                          "module_id": lookup(hits_module_id, "module_id")})
+    pid = truth["particle_id"]
+    once = pid.map(particles_nhits["particle_id"].value_counts()).fillna(0) == 1
+    nh = pid.map(particles_nhits.drop_duplicates("particle_id").set_index("particle_id")["nhits"])
+    truth["nhits"] = np.where(once, nh, 0).astype(np.float64)
+    truth.to_csv(truth_event_file, index=False)
+
+
+def truth_joins(truth):
+    """construct_graph's truth joins (helper.py:468-481) on the mapping DataFrame: per
+    node_idx, its particles (first = truth_particle), hits and modules, each distinct in
+    row order, and every hit's particle (a hit listed twice makes the reference's
+    ``.item()`` raise ValueError). Returns {node_idx: (truth_particle, module_ids,
+    hit_ids, [particle per hit])}."""
+    hit_n = truth["hit_id"].value_counts()
+    pid_of_hit = truth.drop_duplicates("hit_id").set_index("hit_id")["particle_id"]
+    out = {}
+    for n, grp in truth.groupby("node_idx", sort=True):
+        hits = grp["hit_id"].unique()
+        if (hit_n[hits] != 1).any():
+            raise ValueError("can only convert an array of size 1 to a Python scalar (hit_id %d)"
+                             % int(hits[(hit_n[hits] != 1).to_numpy()][0]))
+        out[int(n)] = (grp["particle_id"].unique()[0].item(), grp["module_id"].unique(), hits,
+                       [pid_of_hit[h].item() for h in hits])
+    return out
+
+
+def build_networkx(event_prefix: str, min_volume: int, max_volume: int, truth_csv: str = None, truth=None):
     """The reference's event_conversion graph (event_conversion.py:53-88): construct_graph
     (helper.py:465-521) -- nodes in CSV order with GNN_Measurement, xy, zr, xyzr,
-    volume/layer ids, truth_particle and tags; both directions of every CSV edge in row
-    order -- then nx.DiGraph and the weakly connected subgraphs, copied. Returns the
-    list of subgraphs (no state estimates yet). module_id / hit_dissociation (truth-file
-    joins used only by extraction diagnostics) are not built."""
+    volume/layer ids, module_id, truth_particle, hit_dissociation and tags, with the
+    reference's value types (numpy float64 coordinates and ids from its row Series); both
+    directions of every CSV edge in row order -- then nx.DiGraph and the weakly connected
+    subgraphs, copied. Returns the list of subgraphs (no state estimates yet).
+    truth: the full mapping DataFrame (node_idx, hit_id, particle_id, ..., module_id), as
+    event_conversion reads it: every construct_graph attribute. truth_csv: a two-column
+    node_idx -> particle_id extract instead (truth_particle only; no module_id /
+    hit_dissociation, which only extraction's node merging and the efficiency read)."""
     import networkx as nx
     from GNN_Measurement.GNN_Measurement import GNN_Measurement
     ids, x, y, z, r, layer = read_nodes(event_prefix + "nodes.csv", min_volume, max_volume)
-    truth = read_truth(truth_csv, ids) if truth_csv else np.full(ids.size, -1, np.int64)
+    joins = truth_joins(truth) if truth is not None else None
+    tp = read_truth(truth_csv, ids) if truth_csv else np.full(ids.size, -1, np.int64)
     G = nx.DiGraph()
     for i in range(ids.size):
         n = int(ids[i])
-        xi, yi, zi, ri = float(x[i]), float(y[i]), float(z[i]), float(r[i])
-        vol, lay = int(layer[i] / 1000), int(layer[i] % 100)
-        G.add_node(n, GNN_Measurement=GNN_Measurement(xi, yi, zi, ri, truth_particle=int(truth[i]), n=n),
-                   xy=(xi, yi), zr=(zi, ri), xyzr=(xi, yi, zi, ri), volume_id=vol, in_volume_layer_id=lay,
-                   vivl_id=(vol, lay), truth_particle=int(truth[i]), tags=[n])
+        xi, yi, zi, ri = x[i], y[i], z[i], r[i]
+        vol, lay = np.float64(int(layer[i] / 1000)), np.float64(int(layer[i] % 100))
+        if joins is not None:
+            if n not in joins:   # grouped_pid.loc[...].item() of no row
+                raise ValueError("can only convert an array of size 1 to a Python scalar (node %d)" % n)
+            t, modules, hits, hit_pids = joins[n]
+            G.add_node(n, GNN_Measurement=GNN_Measurement(xi, yi, zi, ri, truth_particle=t, n=n),
+                       xy=(xi, yi), zr=(zi, ri), xyzr=(xi, yi, zi, ri), volume_id=vol, in_volume_layer_id=lay,
+                       vivl_id=(vol, lay), module_id=modules, truth_particle=t,
+                       hit_dissociation={"hit_id": hits, "particle_id": hit_pids}, tags=[n])
+        else:
+            t = int(tp[i])
+            G.add_node(n, GNN_Measurement=GNN_Measurement(xi, yi, zi, ri, truth_particle=t, n=n),
+                       xy=(xi, yi), zr=(zi, ri), xyzr=(xi, yi, zi, ri), volume_id=vol, in_volume_layer_id=lay,
+                       vivl_id=(vol, lay), truth_particle=t, tags=[n])
     n2, n1 = read_edges(event_prefix + "edges.csv")
     for a, b in zip(n1.tolist(), n2.tolist()):
         if a in G and b in G:

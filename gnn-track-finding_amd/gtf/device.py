@@ -387,7 +387,8 @@ class DeviceGraph:
         host_order=False in the device layout's order (no gathers: what a caller that keeps
         the event on the device consumes)."""
         self._natural_only("track_state_estimates")
-        self._need_torch("track_state_estimates")
+        if self.torch is None:
+            return self._track_state_estimates_hip(p, host_order)
         torch = self.torch
         N = self.n_nodes
         nan = float("nan")
@@ -405,6 +406,26 @@ class DeviceGraph:
             inv = self._inv_order()
             x = {k: v[inv] for k, v in x.items()}
         return x
+
+    def _track_state_estimates_hip(self, p: Params, host_order: bool):
+        """mem "hip": the same call on gtf.devmem arrays; the per-node attributes come back
+        as host arrays"""
+        from .devmem import HipArray
+        N = self.n_nodes
+        shapes = {"xy_mean_var": (N, 2), "zr_mean_var": (N, 2), "angle_of_rotation": (N,), "translation": (N, 2)}
+        x = {k: HipArray.from_numpy(np.full(int(np.prod(sh)), np.nan)) for k, sh in shapes.items()}
+        vp = lambda t: ctypes.c_void_p(t.data_ptr() if t.numel() else 0)  # noqa: E731
+        ex = nat.GtfTseExtra(self.ptr("tse_theta"), self.ptr("tse_var_ms"), vp(x["xy_mean_var"]),
+                             vp(x["zr_mean_var"]), vp(x["angle_of_rotation"]), vp(x["translation"]))
+        cp = self.cparams(p)
+        nat.check(self.lib.gtf_track_state_estimates(ctypes.byref(self.cg_sched), ctypes.byref(self.ctse),
+                                                     ctypes.byref(ex), ctypes.byref(cp), self.stream))
+        out = {k: v.numpy().reshape(shapes[k]) for k, v in x.items()}
+        if self.order is not None and host_order:
+            inv = np.empty(self.order.size, np.int64)
+            inv[self.order] = np.arange(self.order.size)
+            out = {k: v[inv] for k, v in out.items()}
+        return out
 
     # ------------------------------------------ a15: distances between updated states
     def updated_state_distances(self, truth=None, host_order: bool = True):

@@ -131,17 +131,30 @@ def truth_joins(truth):
     node_idx, its particles (first = truth_particle), hits and modules, each distinct in
     row order, and every hit's particle (a hit listed twice makes the reference's
     ``.item()`` raise ValueError). Returns {node_idx: (truth_particle, module_ids,
-    hit_ids, [particle per hit])}."""
-    hit_n = truth["hit_id"].value_counts()
-    pid_of_hit = truth.drop_duplicates("hit_id").set_index("hit_id")["particle_id"]
+    hit_ids, [particle per hit])}. Vectorised: the distinct (node, value) pairs in row
+    order, grouped by node with a stable sort."""
+    import pandas as pd
+    node = truth["node_idx"].to_numpy(np.int64)
+    hit = truth["hit_id"].to_numpy(np.int64)
+    pid = truth["particle_id"].to_numpy(np.int64)
+    uh, first, cnt = np.unique(hit, return_index=True, return_counts=True)
+    if (cnt != 1).any():
+        raise ValueError("can only convert an array of size 1 to a Python scalar (hit_id %d)" % int(uh[cnt != 1][0]))
+
+    def distinct(col):
+        d = pd.DataFrame({"n": node, "v": truth[col].to_numpy(np.int64)}).drop_duplicates()
+        n, v = d["n"].to_numpy(), d["v"].to_numpy()
+        o = np.argsort(n, kind="stable")
+        un, start = np.unique(n[o], return_index=True)
+        return un, np.split(v[o], start[1:])
+
+    nodes, pids = distinct("particle_id")
+    _, modules = distinct("module_id")
+    _, hits = distinct("hit_id")
+    pid_of_hit = pid[first]                      # hits are unique: every hit's one row
     out = {}
-    for n, grp in truth.groupby("node_idx", sort=True):
-        hits = grp["hit_id"].unique()
-        if (hit_n[hits] != 1).any():
-            raise ValueError("can only convert an array of size 1 to a Python scalar (hit_id %d)"
-                             % int(hits[(hit_n[hits] != 1).to_numpy()][0]))
-        out[int(n)] = (grp["particle_id"].unique()[0].item(), grp["module_id"].unique(), hits,
-                       [pid_of_hit[h].item() for h in hits])
+    for n, p, m, h in zip(nodes.tolist(), pids, modules, hits):
+        out[n] = (int(p[0]), m, h, pid_of_hit[np.searchsorted(uh, h)].tolist())
     return out
 
 

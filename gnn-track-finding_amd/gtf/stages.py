@@ -33,10 +33,11 @@ def _raise_flags(flags: int):
 def _run(subGraphs, body, states=("tse", "uts"), merged=True):
     """pack -> device -> body(DeviceGraph) -> check flags -> unpack"""
     from .device import DeviceGraph
+    from .devmem import default_mem
     g = pack(subGraphs)
     if g.n_nodes == 0:
         return subGraphs
-    d = DeviceGraph(g)
+    d = DeviceGraph(g, mem=default_mem())
     d.clear_errors()
     body(d)
     flags = d.errors()
@@ -77,8 +78,9 @@ def compute_track_state_estimates(GraphList, sigma0xy, sigma0rz, sigma0rz2, endc
     if g.n_nodes == 0:
         return GraphList
     p = Params(sigma0xy=sigma0xy, sigma0rz=sigma0rz, sigma0rz2=sigma0rz2, endcap_boundary=endcap_boundary)
-    d = DeviceGraph(g)
-    x = {k: v.cpu().numpy() for k, v in d.track_state_estimates(p).items()}
+    from .devmem import default_mem
+    d = DeviceGraph(g, mem=default_mem())
+    x = {k: v if isinstance(v, np.ndarray) else v.cpu().numpy() for k, v in d.track_state_estimates(p).items()}
     d.download(g)
     S = g.slot
     vi = 0

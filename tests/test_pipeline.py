@@ -166,3 +166,70 @@ def test_gpu_pipeline_cli_and_resume(tmp_path):
     check(3)
     again = store.load_groups(os.path.join(out, "iteration_3", "candidates", "candidates.npz"))
     assert [list(a) for a in again[0]] == [list(a) for a in first[0]]
+
+
+@pytest.mark.gpu
+def test_gpu_run_script_with_dropin_clis(tmp_path):
+    """run_gnn_trackml_mod.sh (:61-146, START=1 END=3) with every stage a drop-in CLI in
+    its own process -- event conversion, clustering / extrapolation, extraction, update,
+    the script's directories and its nesting `cp -r` of the previous candidates -- on the
+    committed vol-7 event: each iteration's candidate, remaining and fragment files are
+    the reference run's (tests/golden/pipeline_vol7.npz)."""
+    import glob
+    import pickle
+    import subprocess
+    import sys
+    import pandas as pd
+    from test_event_conversion import _truth_frame
+    pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gnn-track-finding_amd")
+    root, net, tru = str(tmp_path / "output"), str(tmp_path / "net"), str(tmp_path / "truth")
+    for d in (net, tru):
+        os.makedirs(d)
+    for f in ("nodes.csv", "edges.csv"):
+        with open(PREFIX + f) as a, open(os.path.join(net, "event_1_filtered_graph_" + f), "w") as b:
+            b.write(a.read())
+    _truth_frame().to_csv(os.path.join(tru, "event000001000-full-mapping-minCurv-0.3-800.csv"), index=False)
+    SZ = ["-z", "0.4", "-m", "0.6", "-b", "550.0"]
+
+    def cli(module, *args):
+        r = subprocess.run([sys.executable, os.path.join(pkg, module)] + list(args), capture_output=True, text=True,
+                           timeout=600)
+        assert r.returncode == 0, (module, r.stderr[-3000:])
+
+    def read(d):
+        return [pickle.load(open(f, "rb")) for f in sorted(glob.glob(d + "*_subgraph.gpickle"))]
+
+    inp = root + "/track_sim/network/"
+    os.makedirs(inp)
+    cli("trackml_mod/event_conversion.py", "-o", inp, "-n", net, "-t", tru, "-a", "7", "-z", "7", "-e", "0.3",
+        "-r", "0.4", "-m", "0.6", "-b", "550.0")
+    exp = _fixture()
+    for i in (1, 2, 3):
+        out = root + "/iteration_%d/network/" % i
+        os.makedirs(out)
+        if i == 1:
+            cli("clustering/clustering.py", "-i", inp, "-o", out, "-d", "track_state_estimates", "-c", "1.0", "-k", "2.0",
+                "-l", "x.lut", "-t", str(i), *SZ)
+        elif i % 2 == 0:
+            cli("extrapolate/extrapolate_merged_states.py", "-i", inp, "-o", out, "-c", "2.0", "-e", "0.3", *SZ)
+        else:
+            cli("clustering/clustering.py", "-i", inp, "-o", out, "-d", "updated_track_states", "-c", "1000", "-k", "100",
+                "-l", "x.lut", "-t", str(i), *SZ)
+        cand, rem, frag = (root + "/iteration_%d/%s/" % (i, k) for k in ("candidates", "remaining", "fragments"))
+        for d in (cand, rem, frag):
+            os.makedirs(d)
+        if i > 1:   # the script's cp -r into an existing directory nests the copy one level down
+            subprocess.check_call(["cp", "-r", root + "/iteration_%d/candidates/" % (i - 1), cand])
+        cli("extract/extract_track_candidates.py", "-i", out, "-c", cand, "-r", rem, "-f", frag, "-p", "0.01", "-n", "4",
+            "-s", "10", "-t", "8.0", "-a", str(i), "-e", "0.3", "-z", "0.4", "-b", "550.0")
+        if i % 2 == 0:
+            cli("update/remove_state_metadata.py", "-r", rem)
+        inp = rem
+        pv = pd.read_csv(cand + "pvals.csv")
+        cands = [list(s.nodes) for s in read(cand)]
+        # files are numbered in the script's glob order; pvals.csv follows the extraction order
+        # of the same candidates, which are the first len(pv) files
+        ordered = [list(pickle.load(open(cand + "%d_subgraph.gpickle" % k, "rb")).nodes) for k in range(len(pv))]
+        assert len(cands) == len(ordered)
+        _check(i, ordered, pv["pvals_xy"].to_numpy(), pv["pvals_zr"].to_numpy(), [list(s.nodes) for s in read(rem)],
+               [list(s.nodes) for s in read(frag)], exp, 1e-7)

@@ -30,9 +30,15 @@ def main(path):
     sz = ["-z", "0.4", "-m", "0.6", "-b", "550.0"]
     stages = []
 
+    prof = os.environ.get("GTF_PROFILE_STAGE")   # e.g. it1_extract: cProfile that stage (top functions to stdout)
+
     def cli(name, module, *args):
         t = time.perf_counter()
-        subprocess.run([sys.executable, os.path.join(PKG, module)] + list(args), check=True, capture_output=True)
+        pre = ["-m", "cProfile", "-s", "cumulative"] if name == prof else []
+        r = subprocess.run([sys.executable] + pre + [os.path.join(PKG, module)] + list(args), check=True,
+                           capture_output=True, text=True)
+        if pre:
+            print("\n".join(r.stdout.splitlines()[:60]))
         stages.append((name, time.perf_counter() - t))
         print(name, "%.3f s" % stages[-1][1], flush=True)
 

@@ -485,35 +485,47 @@ class DeviceGraph:
     def tag_propagation(self, tags, radius, threshold=0.1, max_sweeps=100000):
         """Jacobi sweeps until flips / processed <= threshold (tag_propagation.py:137)."""
         self._natural_only("tag_propagation")
-        self._need_torch("tag_propagation")
-        torch = self.torch
-        dev = self.device
         E = self.n_edges
-        keep = torch.zeros(max(E, 1), dtype=torch.uint8, device=dev)
-        proc = torch.zeros(max(self.n_nodes, 1), dtype=torch.uint8, device=dev)
-        cnt = torch.zeros(2, dtype=torch.int32, device=dev)
-        r = torch.from_numpy(np.ascontiguousarray(self._to_dev_nodes(radius), dtype=np.float64)).to(dev)
-        ta = torch.from_numpy(np.ascontiguousarray(self._to_dev_nodes(tags), dtype=np.int64)).to(dev)
-        tb = torch.empty_like(ta)
+        keep = self._dev_zeros(max(E, 1), np.uint8)
+        proc = self._dev_zeros(max(self.n_nodes, 1), np.uint8)
+        cnt = self._dev_zeros(2, np.int32)
+        r = self._dev_from(np.ascontiguousarray(self._to_dev_nodes(radius), dtype=np.float64))
+        ta = self._dev_from(np.ascontiguousarray(self._to_dev_nodes(tags), dtype=np.int64))
+        tb = self._dev_zeros(max(self.n_nodes, 1), np.int64)
         vp = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
         nat.check(self.lib.gtf_tag_prepare(ctypes.byref(self.cg), vp(r), vp(keep), vp(proc), vp(cnt), self.stream))
-        total = int(cnt[0].item())
+        total = int(self._np(cnt)[0])
         flips_hist = []
         frac = 1.0
-        flips = cnt[1:2]
+        flips = cnt[1:2] if self.torch is not None else cnt.view(4, 1, np.int32)
         while frac > threshold and len(flips_hist) < max_sweeps:
             nat.check(self.lib.gtf_tag_sweep(ctypes.byref(self.cg), vp(keep), vp(proc), vp(ta), vp(tb), vp(flips),
                                              self.stream))
-            f = int(flips.item())
+            f = int(self._np(flips)[0])
             flips_hist.append(f)
             frac = f / total if total else 0.0
             ta, tb = tb, ta
-        out = ta.cpu().numpy()
+        out = self._np(ta)[:self.n_nodes]
         if self.order is not None:
             h = np.empty_like(out)
             h[self.order] = out
             out = h
         return out, flips_hist
+
+    def _dev_zeros(self, n, dtype):
+        """a zeroed device array of this graph's allocator"""
+        if self.torch is None:
+            from .devmem import HipArray
+            return HipArray.zeros(n, dtype)
+        return self.torch.zeros(n, dtype=getattr(self.torch, np.dtype(dtype).name), device=self.device)
+
+    def _dev_from(self, a):
+        """a host array on the device (this graph's allocator)"""
+        a = np.ascontiguousarray(a).reshape(-1)
+        if self.torch is None:
+            from .devmem import HipArray
+            return HipArray.from_numpy(a)
+        return self.torch.from_numpy(a).to(self.device)
 
     # ------------------------------------------------------------ diagnostics
     def set_diagnostics(self, node_err: bool = True, edge_chi2: bool = True, slot_cluster: bool = False):

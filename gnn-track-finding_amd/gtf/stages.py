@@ -175,7 +175,8 @@ def tag_propagation(G, threshold=0.1):
     Tags are written to the node attribute 'tags' (appended, as the script does)."""
     g = pack([G])
     from .device import DeviceGraph
-    d = DeviceGraph(g)
+    from .devmem import default_mem
+    d = DeviceGraph(g, mem=default_mem())
     radius = [G.nodes[n]["zr"][1] if "zr" in G.nodes[n] else G.nodes[n]["xyzr"][3] for n in G.nodes]
     tags, flips = d.tag_propagation(g.node["tag"], radius, threshold)
     out = {}

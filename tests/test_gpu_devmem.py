@@ -133,3 +133,15 @@ def _read_numbered(dd):
             out.append(pickle.load(f))
         i += 1
     return out
+
+
+def test_tag_propagation_hip_memory_equals_torch():
+    """tag propagation (k_tag_prepare + sweeps until the reference's stop test) on both
+    allocators: same final tags, same flips per sweep"""
+    g = synth.workload("tiny400", seed=3)
+    rng = np.random.default_rng(0)
+    tags = rng.integers(0, g.n_nodes, g.n_nodes)
+    radius = g.node["xyzr"][:, 3]
+    a = DeviceGraph(g, mem="torch").tag_propagation(tags, radius)
+    b = DeviceGraph(g, mem="hip").tag_propagation(tags, radius)
+    assert np.array_equal(a[0], b[0]) and a[1] == b[1] and len(a[1]) >= 1

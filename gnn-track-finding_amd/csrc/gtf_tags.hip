@@ -138,6 +138,36 @@ __global__ void __launch_bounds__(BLOCK) k_tag_sweep_sched(gtf_graph g, const ui
     const unsigned long long m = __ballot(flipped);
     if ((threadIdx.x & 63) == 0 && m) atomicAdd(flips, (int)__popcll(m));
 }
+
+// One rank's sweep of the sharded tag propagation: the owned nodes
+// [lo, hi) as k_tag_sweep computes them; every other node's word is INT64_MIN and this
+// rank's flip count goes to word n_nodes + rank (the other ranks' words stay 0), so an
+// all-reduce(MAX) of the n_nodes + nranks words is the whole next tag array on every rank
+// plus every rank's flip count: one collective per sweep, bit-exact (integer max).
+__global__ void __launch_bounds__(BLOCK) k_tag_sweep_owned(gtf_graph g, const uint8_t* keep, const uint8_t* processed,
+                                                           const int64_t* tin, int64_t* tout, int lo, int hi,
+                                                           unsigned long long* flips) {
+    const int u = gtf::xcd_local(blockIdx.x, gridDim.x) * BLOCK + threadIdx.x;
+    int flipped = 0;
+    if (u < g.n_nodes) {
+        int64_t t = INT64_MIN;
+        if (u >= lo && u < hi) {
+            const int64_t t0 = tin[u];
+            t = t0;
+            if (processed[u]) {
+                for (int i = g.out_ptr[u]; i < g.out_ptr[u + 1]; i++)
+                    if (keep[i]) {
+                        const int64_t tw = tin[g.out_dst ? g.out_dst[i] : g.slot_dst[g.out_slot[i]]];
+                        t = tw > t ? tw : t;
+                    }
+                flipped = (t != t0);
+            }
+        }
+        tout[u] = t;
+    }
+    const unsigned long long b = __ballot(flipped);
+    if ((threadIdx.x & 63) == 0 && b) atomicAdd(flips, (unsigned long long)__popcll(b));
+}
 }  // namespace
 
 extern "C" {
@@ -182,6 +212,25 @@ int gtf_tag_sweep(const gtf_graph* g, const uint8_t* keep, const uint8_t* proces
         hipLaunchKernelGGL(k_tag_sweep, dim3((g->n_nodes + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, st, *g, keep,
                            processed, tags_in, tags_out, flips);
     }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int gtf_tag_sweep_shard(const gtf_graph* g, const uint8_t* keep, const uint8_t* processed, const int64_t* tags_in,
+                        int64_t* tags_out, const gtf_shard* shard, int32_t rank, int32_t nranks,
+                        gtf_stream_t stream) {
+    if (int rc = gtf::check_abi(g, "gtf_tag_sweep_shard")) return rc;
+    if (!shard || rank < 0 || rank >= nranks || shard->node_lo < 0 || shard->node_hi < shard->node_lo ||
+        shard->node_hi > g->n_nodes) {
+        gtf::set_error("gtf_tag_sweep_shard: owned node range or rank out of bounds");
+        return -2;
+    }
+    hipStream_t st = (hipStream_t)stream;
+    int64_t* words = tags_out + g->n_nodes;   // the nranks flip-count words
+    if (hipMemsetAsync(words, 0, sizeof(int64_t) * (size_t)nranks, st) != hipSuccess) return -1;
+    if (g->n_nodes > 0)
+        hipLaunchKernelGGL(k_tag_sweep_owned, dim3((g->n_nodes + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, st, *g, keep,
+                           processed, tags_in, tags_out, shard->node_lo, shard->node_hi,
+                           reinterpret_cast<unsigned long long*>(words + rank));
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

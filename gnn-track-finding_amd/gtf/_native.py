@@ -140,7 +140,7 @@ ERR_FLAGS = {
 # exported symbols (must match include/gtf.h; tests check the .so exports all of them)
 SYMBOLS = ["gtf_workspace_bytes", "gtf_clear_errors", "gtf_read_errors", "gtf_extrapolate", "gtf_update",
            "gtf_message_passing", "gtf_node_ops",
-           "gtf_cluster", "gtf_pass", "gtf_pass_ev", "gtf_tag_prepare", "gtf_tag_sweep", "gtf_parabolic_kl", "gtf_track_state_estimates", "gtf_pass_shard",
+           "gtf_cluster", "gtf_pass", "gtf_pass_ev", "gtf_tag_prepare", "gtf_tag_sweep", "gtf_tag_sweep_shard", "gtf_parabolic_kl", "gtf_track_state_estimates", "gtf_pass_shard",
            "gtf_shard_chunk_bytes", "gtf_shard_pack", "gtf_shard_unpack", "gtf_halo_pack", "gtf_halo_unpack",
            "gtf_extract_workspace_bytes",
            "gtf_extract_candidates", "gtf_build_event_csr", "gtf_candidate_order",
@@ -204,6 +204,7 @@ def lib(lean: bool = False):
     L.gtf_extract_candidates.argtypes = [G, E, ctypes.POINTER(GtfExtractIO), ctypes.POINTER(GtfExtractParams), P, P]
     SH = ctypes.POINTER(GtfShard)
     L.gtf_pass_shard.argtypes = [G, N, S, S, E, PR, SH, P, P, ctypes.POINTER(P)]
+    L.gtf_tag_sweep_shard.argtypes = [G, P, P, P, P, SH, I32, I32, P]
     L.gtf_shard_chunk_bytes.restype = ctypes.c_size_t
     L.gtf_shard_chunk_bytes.argtypes = [I32, I32]
     L.gtf_shard_pack.argtypes = [N, E, SH, I32, I32, P, P]
@@ -231,7 +232,7 @@ def lib(lean: bool = False):
     L.gtf_version.restype = ctypes.c_char_p
     for fn in ("gtf_clear_errors", "gtf_read_errors", "gtf_extrapolate", "gtf_update", "gtf_cluster", "gtf_pass",
                "gtf_pass_ev", "gtf_message_passing", "gtf_node_ops",
-               "gtf_tag_prepare", "gtf_tag_sweep", "gtf_parabolic_kl", "gtf_track_state_estimates", "gtf_pass_shard", "gtf_shard_pack",
+               "gtf_tag_prepare", "gtf_tag_sweep", "gtf_tag_sweep_shard", "gtf_parabolic_kl", "gtf_track_state_estimates", "gtf_pass_shard", "gtf_shard_pack",
                "gtf_shard_unpack", "gtf_halo_pack", "gtf_halo_unpack", "gtf_extract_candidates", "gtf_build_event_csr",
                "gtf_candidate_order", "gtf_updated_state_pair_counts", "gtf_updated_state_distances",
                "gtf_set_diagnostics", "gtf_build_event_csr_device", "gtf_device_init", "gtf_malloc", "gtf_free",

@@ -236,6 +236,20 @@ def alltoall_bytes(send, recv, send_sizes, recv_sizes, backend: str, group=None)
     return recv
 
 
+def allreduce_max_i64(buf, backend: str, group=None):
+    """element-wise MAX all-reduce of an int64 buffer (the sharded tag sweep's exchange).
+    RCCL reduces the device buffer over xGMI; gloo stages through host memory."""
+    import torch.distributed as dist
+    if backend == "nccl":
+        dist.all_reduce(buf, op=dist.ReduceOp.MAX, group=group)
+        return buf
+    h = buf.cpu()
+    dist.all_reduce(h, op=dist.ReduceOp.MAX, group=group)
+    if h is not buf:
+        buf.copy_(h.to(buf.device))
+    return buf
+
+
 class ShardedDeviceGraph:
     """A DeviceGraph replica on this rank's GPU (wedge + tiled node order) that runs the
     pass for its receivers and exchanges the halo with the other ranks after each pass."""
@@ -377,6 +391,45 @@ class ShardedDeviceGraph:
     def step(self, p, events=None):
         self.pass_(p, events)
         self.exchange()
+
+    def tag_propagation(self, tags, radius, threshold=0.1, max_sweeps=100000):
+        """Tag propagation (tag_propagation/tag_propagation.py:97-164) on the edge-sharded
+        event: the keep mask and the processed count come from the replica
+        (gtf_tag_prepare over the whole event, no exchange); per sweep every rank computes
+        its owned nodes' next tags (gtf_tag_sweep_shard) and ONE all-reduce(MAX) of the
+        n_nodes + world int64 words gives every replica the whole next tag array and every
+        rank's flip count. Same stop rule (flips / processed <= threshold), sweeps and tags
+        as DeviceGraph.tag_propagation, bit for bit. Returns (tags in host node order,
+        flips per sweep) on every rank; tags / radius are host-order arrays."""
+        torch = self.torch
+        d = self.d
+        N, W = d.n_nodes, self.world
+        dev = d.device
+        vp = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        keep = torch.zeros(max(d.n_edges, 1), dtype=torch.uint8, device=dev)
+        proc = torch.zeros(max(N, 1), dtype=torch.uint8, device=dev)
+        cnt = torch.zeros(2, dtype=torch.int32, device=dev)
+        r = torch.from_numpy(np.ascontiguousarray(d._to_dev_nodes(radius), dtype=np.float64)).to(dev)
+        ta = torch.zeros(N + W, dtype=torch.int64, device=dev)
+        ta[:N] = torch.from_numpy(np.ascontiguousarray(d._to_dev_nodes(tags), dtype=np.int64)).to(dev)
+        tb = torch.zeros(N + W, dtype=torch.int64, device=dev)
+        st = d.stream
+        nat.check(d.lib.gtf_tag_prepare(ctypes.byref(self.cg), vp(r), vp(keep), vp(proc), vp(cnt), st))
+        total = int(cnt[0].item())
+        hist = []
+        frac = 1.0
+        while frac > threshold and len(hist) < max_sweeps:
+            nat.check(d.lib.gtf_tag_sweep_shard(ctypes.byref(self.cg), vp(keep), vp(proc), vp(ta), vp(tb),
+                                                ctypes.byref(self.shard), self.rank, W, st))
+            allreduce_max_i64(tb, self.backend, self.group)
+            f = int(tb[N:].sum().item())
+            hist.append(f)
+            frac = f / total if total else 0.0
+            ta, tb = tb, ta
+        out = ta[:N].cpu().numpy()
+        h = np.empty_like(out)
+        h[d.order] = out
+        return h, hist
 
     def owned_host_nodes(self) -> np.ndarray:
         """host indices of this rank's receivers (their results are final on this rank)"""

@@ -22,6 +22,7 @@
  *                       (run_gnn_trackml_mod.sh:101,138,112 stage order)
  *   gtf_tag_sweep    -> tag_propagation/tag_propagation.py:137-164 (one sweep)
  *   gtf_tag_prepare  -> tag_propagation/tag_propagation.py:97-110
+ *   gtf_tag_sweep_shard -> one sweep (:137-164) on an edge-sharded event
  *   gtf_updated_state_distances -> calculate_distance_between_updated_states/
  *                       calculate_distance_between_updated_track_states.py:27-104,134-195
  */
@@ -336,6 +337,17 @@ int gtf_tag_prepare(const gtf_graph* g, const double* radius, uint8_t* keep, uin
  * on the sender schedule's lane groups, otherwise one thread per node. */
 int gtf_tag_sweep(const gtf_graph* g, const uint8_t* keep, const uint8_t* processed,
                   const int64_t* tags_in, int64_t* tags_out, int32_t* flips, gtf_stream_t stream);
+/* One rank's sweep of tag propagation on an edge-sharded event (the sweep of
+ * tag_propagation.py:137-164 over the rank's owned nodes [shard->node_lo, shard->node_hi)
+ * of the replicated graph `g`). tags_in / tags_out: device int64 [n_nodes + nranks].
+ * Writes the owned nodes' next tags, INT64_MIN for every other node, this rank's flip count
+ * to tags_out[n_nodes + rank] and 0 to the other ranks' count words, so ONE all-reduce(MAX)
+ * of the n_nodes + nranks words gives every rank the whole next tag array and every
+ * rank's flip count (their sum is the sweep's flips). gtf_tag_prepare runs unsharded on
+ * the replica (its n_processed is the whole event's). */
+int gtf_tag_sweep_shard(const gtf_graph* g, const uint8_t* keep, const uint8_t* processed,
+                        const int64_t* tags_in, int64_t* tags_out, const gtf_shard* shard,
+                        int32_t rank, int32_t nranks, gtf_stream_t stream);
 
 /* ---- Distances between updated track states --------------------
  * calculate_distance_between_updated_states/calculate_distance_between_updated_track_states.py:

@@ -167,6 +167,41 @@ def test_exchange_alltoall_gloo_world2():
         assert (a == exp).all()
 
 
+def _gloo_tag_exchange_worker(rank, world, port, q):
+    """the sharded tag sweep's buffer protocol (gtf_tag_sweep_shard): owned tags, INT64_MIN
+    elsewhere, this rank's flip count at word n + rank, 0 in the other count words"""
+    import torch
+    import torch.distributed as dist
+    from gtf.shard import allreduce_max_i64
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    n = 1000
+    lo, hi = [0, 300, 1000][rank], [300, 1000, 1000][rank]
+    buf = torch.full((n + world,), torch.iinfo(torch.int64).min, dtype=torch.int64)
+    buf[lo:hi] = torch.arange(lo, hi, dtype=torch.int64) * 7 - 3000
+    buf[n:] = 0
+    buf[n + rank] = 11 * (rank + 1)
+    allreduce_max_i64(buf, "gloo")
+    q.put((rank, buf.numpy().copy()))
+    dist.destroy_process_group()
+
+
+def test_exchange_tag_allreduce_max_gloo_world2():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_gloo_tag_exchange_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(60)
+    exp = np.concatenate([np.arange(1000, dtype=np.int64) * 7 - 3000, [11, 22]])
+    for r in range(2):
+        assert np.array_equal(res[r], exp)
+
+
 # ---------------------------------------------------------------- GPU (2 ranks, 1 GPU)
 PASSES = 2
 OUT_NODE = ("has_merged", "merged_state", "merged_cov", "merged_prior", "has_uts", "degree")

@@ -46,7 +46,8 @@ def _worker(rank, world, port, which, outdir):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     g, tags, radius = _graph(which)
     sd = ShardedDeviceGraph(g, rank, world, "cuda:0", backend="gloo", tile=512)
-    out, flips = sd.tag_propagation(tags, radius)
+    # C4: sweep to convergence (the reference's 10 % stop ends after one sweep there)
+    out, flips = sd.tag_propagation(tags, radius, threshold=0.1 if which == "vol7" else 0.0)
     np.savez(os.path.join(outdir, "%s_w%d_r%d.npz" % (which, world, rank)), tags=out, flips=np.array(flips))
     dist.barrier()
     dist.destroy_process_group()
@@ -85,8 +86,8 @@ def test_sharded_tags_vol7_equal_reference(world, tmp_path):
 def test_sharded_tags_c4_equal_single_gpu(world, tmp_path):
     from gtf.device import DeviceGraph
     g, tags, radius = _graph("c4")
-    one, one_flips = DeviceGraph(g, layout="tiled").tag_propagation(tags, radius)
-    assert len(one_flips) > 1
+    one, one_flips = DeviceGraph(g, layout="tiled").tag_propagation(tags, radius, threshold=0.0)
+    assert len(one_flips) > 2 and one_flips[-1] == 0
     for z in _run("c4", world, tmp_path):
         assert list(z["flips"]) == list(one_flips)
         assert np.array_equal(z["tags"], one)

@@ -35,7 +35,7 @@ def _graph(which):
     return g, np.arange(g.n_nodes, dtype=np.int64), g.node["xyzr"][:, 3]
 
 
-def _worker(rank, world, port, which, outdir):
+def _worker(rank, world, port, which, outdir, backend="gloo"):
     import sys
     sys.path.insert(0, os.path.dirname(__file__))
     import torch
@@ -43,9 +43,12 @@ def _worker(rank, world, port, which, outdir):
     from gtf.shard import ShardedDeviceGraph
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda:0"))
+    else:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
     g, tags, radius = _graph(which)
-    sd = ShardedDeviceGraph(g, rank, world, "cuda:0", backend="gloo", tile=512)
+    sd = ShardedDeviceGraph(g, rank, world, "cuda:0", backend=backend, tile=512)
     # C4: sweep to convergence (the reference's 10 % stop ends after one sweep there)
     out, flips = sd.tag_propagation(tags, radius, threshold=0.1 if which == "vol7" else 0.0)
     np.savez(os.path.join(outdir, "%s_w%d_r%d.npz" % (which, world, rank)), tags=out, flips=np.array(flips))
@@ -53,11 +56,11 @@ def _worker(rank, world, port, which, outdir):
     dist.destroy_process_group()
 
 
-def _run(which, world, tmp_path):
+def _run(which, world, tmp_path, backend="gloo"):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, which, str(tmp_path))) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, which, str(tmp_path), backend)) for r in range(world)]
     for p in ps:
         p.start()
     for p in ps:
@@ -91,3 +94,13 @@ def test_sharded_tags_c4_equal_single_gpu(world, tmp_path):
     for z in _run("c4", world, tmp_path):
         assert list(z["flips"]) == list(one_flips)
         assert np.array_equal(z["tags"], one)
+
+
+def test_sharded_tags_vol7_rccl_world1(tmp_path):
+    """the RCCL all-reduce(MAX) path of the sweep exchange (one rank: the box has one GPU)"""
+    from fixtures import load
+    g, _, extra, _ = load("tags_vol7")
+    kept = extra["tags"] >= 0
+    (z,) = _run("vol7", 1, tmp_path, backend="nccl")
+    assert list(z["flips"]) == list(extra["flips"])
+    assert np.array_equal(z["tags"][kept], extra["tags"][kept])

@@ -505,23 +505,53 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
     int lt0 = 1 << 20, lt1 = 1 << 20;
     unsigned lmask = 0;
     bool lnan = false, lnz = false;
-    for (int t = c.grp.gl; t < npairs; t += c.grp.size()) {
-        int i, j;
-        pair_ij(t, i, j);
-        const int li = sb + stg->ord[sb + i], lj = sb + stg->ord[sb + j];
-        const double D = mahalanobis_geo(stg->a[li], stg->b[li], stage_cov(stg, li), stg->a[lj], stg->b[lj],
-                                         stage_cov(stg, lj), sza2, sra2, stage_geo(stg, li, szb2, srb2),
-                                         stage_geo(stg, lj, szb2, srb2));
-        if (D == 0.0) continue;  // zeros are excluded (np.nonzero)
+    // a lane's pairs in ascending t (the np.where order of its ties): fold one distance
+    auto fold = [&](double D, int t, int i, int j) {
+        if (D == 0.0) return;  // zeros are excluded (np.nonzero)
         lnz = true;
-        if (D != D) { lnan = true; continue; }
+        if (D != D) { lnan = true; return; }
         if (D < lmin) {
             lmin = D; lt0 = t; lt1 = 1 << 20; lmask = (1u << i) | (1u << j);
         } else if (D == lmin) {
             if (lt1 == (1 << 20)) lt1 = t;
             lmask |= (1u << i) | (1u << j);
         }
+    };
+    auto pair_d = [&](int i, int j) {
+        const int li = sb + stg->ord[sb + i], lj = sb + stg->ord[sb + j];
+        return mahalanobis_geo(stg->a[li], stg->b[li], stage_cov(stg, li), stg->a[lj], stg->b[lj],
+                               stage_cov(stg, lj), sza2, sra2, stage_geo(stg, li, szb2, srb2),
+                               stage_geo(stg, lj, szb2, srb2));
+    };
+#ifndef GTF_PAIR_UNROLL
+#define GTF_PAIR_UNROLL 1
+#endif
+#if GTF_PAIR_UNROLL > 1
+    // GTF_PAIR_UNROLL of the lane's pairs per iteration: their division chains (the 2x2
+    // inverse of the summed covariances, the tau term) are independent and overlap; folded
+    // in t order
+    constexpr int U = GTF_PAIR_UNROLL;
+    const int step = c.grp.size();
+    for (int t = c.grp.gl; t < npairs; t += U * step) {
+        double Dv[U];
+        int iv[U], jv[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const int tu = t + u * step;
+            pair_ij(tu < npairs ? tu : t, iv[u], jv[u]);
+            Dv[u] = pair_d(iv[u], jv[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            if (t + u * step < npairs) fold(Dv[u], t + u * step, iv[u], jv[u]);
     }
+#else
+    for (int t = c.grp.gl; t < npairs; t += c.grp.size()) {
+        int i, j;
+        pair_ij(t, i, j);
+        fold(pair_d(i, j), t, i, j);
+    }
+#endif
     if (!c.grp.any(lnz)) {
         if (c.grp.gl == 0) raise_node(err, c.v, GTF_ERR_ALL_ZERO_DIST);
         return;

@@ -8,7 +8,7 @@
 # tools/ab.sh.
 set -e
 cd "$(dirname "$0")/../gnn-track-finding_amd/csrc"
-SRC="gtf_pass.hip gtf_tags.hip gtf_kl.hip gtf_tse.hip gtf_shard.hip gtf_extract.hip gtf_a15.hip gtf_build.cpp"
+SRC="gtf_pass.hip gtf_tags.hip gtf_kl.hip gtf_tse.hip gtf_shard.hip gtf_extract.hip gtf_a15.hip gtf_build.cpp gtf_build_dev.hip gtf_mem.hip"
 CXX="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -shared"
 if [ -n "$1" ]; then
   name=$1; shift

@@ -215,6 +215,74 @@ int gtf_tag_sweep(const gtf_graph* g, const uint8_t* keep, const uint8_t* proces
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+static size_t tag_align(size_t x) { return (x + 255) & ~size_t(255); }
+
+size_t gtf_tag_workspace_bytes(int32_t n_nodes, int32_t n_edges) {
+    const size_t n = n_nodes > 0 ? (size_t)n_nodes : 1, e = n_edges > 0 ? (size_t)n_edges : 1;
+    return tag_align(2 * sizeof(int32_t)) + tag_align(e) + tag_align(n) + tag_align(sizeof(int64_t) * n);
+}
+
+// The whole stage behind one call: prepare, then sweeps until flips / processed <= the
+// threshold (the loop of tag_propagation.py:130-164, first sweep unconditional), the tag
+// arrays ping-ponging between `tags` and the workspace; one stream synchronisation per
+// sweep, where the stop rule reads the flip count.
+int gtf_tag_propagate(const gtf_graph* g, const double* radius, int64_t* tags, double flip_threshold,
+                      int32_t max_sweeps, int32_t* flips_out, int32_t* sweeps_out, void* workspace,
+                      size_t workspace_bytes, gtf_stream_t stream) {
+    if (int rc = gtf::check_abi(g, "gtf_tag_propagate")) return rc;
+    if (!sweeps_out || (g->n_nodes > 0 && (!tags || !radius)) || max_sweeps < 0) {
+        gtf::set_error("gtf_tag_propagate: null argument or negative max_sweeps");
+        return -2;
+    }
+    const int32_t n_edges = g->n_nodes > 0 ? g->n_edges : 0;
+    if (!workspace || workspace_bytes < gtf_tag_workspace_bytes(g->n_nodes, n_edges)) {
+        gtf::set_error("gtf_tag_propagate: workspace smaller than gtf_tag_workspace_bytes()");
+        return -2;
+    }
+    hipStream_t st = (hipStream_t)stream;
+    const size_t n = g->n_nodes > 0 ? (size_t)g->n_nodes : 1, e = n_edges > 0 ? (size_t)n_edges : 1;
+    char* w = static_cast<char*>(workspace);
+    int32_t* cnt = reinterpret_cast<int32_t*>(w);   // [0] processed, [1] flips
+    w += tag_align(2 * sizeof(int32_t));
+    uint8_t* keep = reinterpret_cast<uint8_t*>(w);
+    w += tag_align(e);
+    uint8_t* proc = reinterpret_cast<uint8_t*>(w);
+    w += tag_align(n);
+    int64_t* other = reinterpret_cast<int64_t*>(w);
+    *sweeps_out = 0;
+    if (int rc = gtf_tag_prepare(g, radius, keep, proc, cnt, stream)) return rc;
+    int32_t total = 0;
+    if (hipMemcpyAsync(&total, cnt, sizeof(int32_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess) {
+        gtf::set_error("gtf_tag_propagate: reading the processed count failed");
+        return -1;
+    }
+    int64_t* cur = tags;
+    int64_t* nxt = other;
+    double frac = 1.0;
+    int32_t s = 0;
+    while (frac > flip_threshold && s < max_sweeps) {
+        if (int rc = gtf_tag_sweep(g, keep, proc, cur, nxt, cnt + 1, stream)) return rc;
+        int32_t f = 0;
+        if (hipMemcpyAsync(&f, cnt + 1, sizeof(int32_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess) {
+            gtf::set_error("gtf_tag_propagate: reading the flip count failed");
+            return -1;
+        }
+        if (flips_out) flips_out[s] = f;
+        s++;
+        frac = total ? (double)f / (double)total : 0.0;
+        int64_t* t = cur;
+        cur = nxt;
+        nxt = t;
+    }
+    *sweeps_out = s;
+    if (cur != tags && g->n_nodes > 0 &&
+        hipMemcpyAsync(tags, cur, sizeof(int64_t) * (size_t)g->n_nodes, hipMemcpyDeviceToDevice, st) != hipSuccess)
+        return -1;
+    return 0;
+}
+
 int gtf_tag_sweep_shard(const gtf_graph* g, const uint8_t* keep, const uint8_t* processed, const int64_t* tags_in,
                         int64_t* tags_out, const gtf_shard* shard, int32_t rank, int32_t nranks,
                         gtf_stream_t stream) {

@@ -140,7 +140,7 @@ ERR_FLAGS = {
 # exported symbols (must match include/gtf.h; tests check the .so exports all of them)
 SYMBOLS = ["gtf_workspace_bytes", "gtf_clear_errors", "gtf_read_errors", "gtf_extrapolate", "gtf_update",
            "gtf_message_passing", "gtf_node_ops",
-           "gtf_cluster", "gtf_pass", "gtf_pass_ev", "gtf_tag_prepare", "gtf_tag_sweep", "gtf_tag_sweep_shard", "gtf_parabolic_kl", "gtf_track_state_estimates", "gtf_pass_shard",
+           "gtf_cluster", "gtf_pass", "gtf_pass_ev", "gtf_tag_prepare", "gtf_tag_sweep", "gtf_tag_sweep_shard", "gtf_tag_workspace_bytes", "gtf_tag_propagate", "gtf_parabolic_kl", "gtf_track_state_estimates", "gtf_pass_shard",
            "gtf_shard_chunk_bytes", "gtf_shard_pack", "gtf_shard_unpack", "gtf_halo_pack", "gtf_halo_unpack",
            "gtf_extract_workspace_bytes",
            "gtf_extract_candidates", "gtf_build_event_csr", "gtf_candidate_order",
@@ -199,6 +199,9 @@ def lib(lean: bool = False):
     L.gtf_pass_ev.argtypes = [G, N, S, S, E, PR, P, P, ctypes.POINTER(P)]
     L.gtf_tag_prepare.argtypes = [G, P, P, P, P, P]
     L.gtf_tag_sweep.argtypes = [G, P, P, P, P, P, P]
+    L.gtf_tag_workspace_bytes.restype = ctypes.c_size_t
+    L.gtf_tag_workspace_bytes.argtypes = [I32, I32]
+    L.gtf_tag_propagate.argtypes = [G, P, P, F64, I32, P, ctypes.POINTER(ctypes.c_int32), P, ctypes.c_size_t, P]
     L.gtf_extract_workspace_bytes.restype = ctypes.c_size_t
     L.gtf_extract_workspace_bytes.argtypes = [I32, I32]
     L.gtf_extract_candidates.argtypes = [G, E, ctypes.POINTER(GtfExtractIO), ctypes.POINTER(GtfExtractParams), P, P]

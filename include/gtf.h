@@ -22,6 +22,7 @@
  *                       (run_gnn_trackml_mod.sh:101,138,112 stage order)
  *   gtf_tag_sweep    -> tag_propagation/tag_propagation.py:137-164 (one sweep)
  *   gtf_tag_prepare  -> tag_propagation/tag_propagation.py:97-110
+ *   gtf_tag_propagate -> tag_propagation/tag_propagation.py:97-164 (the whole stage)
  *   gtf_tag_sweep_shard -> one sweep (:137-164) on an edge-sharded event
  *   gtf_updated_state_distances -> calculate_distance_between_updated_states/
  *                       calculate_distance_between_updated_track_states.py:27-104,134-195
@@ -337,6 +338,17 @@ int gtf_tag_prepare(const gtf_graph* g, const double* radius, uint8_t* keep, uin
  * on the sender schedule's lane groups, otherwise one thread per node. */
 int gtf_tag_sweep(const gtf_graph* g, const uint8_t* keep, const uint8_t* processed,
                   const int64_t* tags_in, int64_t* tags_out, int32_t* flips, gtf_stream_t stream);
+/* The whole tag-propagation stage in one call (tag_propagation.py:97-164: prepare, then
+ * sweeps while flips / processed > flip_threshold -- the reference's 0.1 -- and fewer than
+ * max_sweeps; the first sweep always runs). tags: device int64 [n_nodes], the initial tags
+ * in, the final tags out; flips_out: host int32 [max_sweeps] (or NULL), the flip count of
+ * every sweep; *sweeps_out: the number of sweeps. workspace: device, at least
+ * gtf_tag_workspace_bytes(n_nodes, n_edges) bytes. Synchronises `stream` once per sweep
+ * (the stop rule reads the flip count). */
+size_t gtf_tag_workspace_bytes(int32_t n_nodes, int32_t n_edges);
+int gtf_tag_propagate(const gtf_graph* g, const double* radius, int64_t* tags, double flip_threshold,
+                      int32_t max_sweeps, int32_t* flips_out, int32_t* sweeps_out, void* workspace,
+                      size_t workspace_bytes, gtf_stream_t stream);
 /* One rank's sweep of tag propagation on an edge-sharded event (the sweep of
  * tag_propagation.py:137-164 over the rank's owned nodes [shard->node_lo, shard->node_hi)
  * of the replicated graph `g`). tags_in / tags_out: device int64 [n_nodes + nranks].

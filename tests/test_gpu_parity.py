@@ -82,3 +82,32 @@ def test_tag_propagation():
     assert list(flips) == list(extra["flips"])
     kept = extra["tags"] >= 0
     assert np.array_equal(tags[kept], extra["tags"][kept])
+
+
+def test_tag_propagate_one_call():
+    """gtf_tag_propagate (the whole stage behind one C-ABI call, caller workspace) against
+    the reference's tags and flip vector, through ctypes with no Python sweep loop"""
+    import ctypes
+    import torch
+    from gtf import _native as nat
+    g, _, extra, _ = load("tags_vol7")
+    d = _dev(g)
+    L = d.lib
+    tags = torch.from_numpy(np.ascontiguousarray(g.node["tag"], dtype=np.int64)).to(d.device)
+    radius = torch.from_numpy(np.ascontiguousarray(g.node["xyzr"][:, 3], dtype=np.float64)).to(d.device)
+    nb = L.gtf_tag_workspace_bytes(g.n_nodes, g.n_edges)
+    ws = torch.zeros(nb, dtype=torch.uint8, device=d.device)
+    flips = (ctypes.c_int32 * 64)()
+    sweeps = ctypes.c_int32(0)
+    nat.check(L.gtf_tag_propagate(ctypes.byref(d.cg), ctypes.c_void_p(radius.data_ptr()),
+                                  ctypes.c_void_p(tags.data_ptr()), 0.1, 64, ctypes.cast(flips, ctypes.c_void_p), ctypes.byref(sweeps),
+                                  ctypes.c_void_p(ws.data_ptr()), nb, d.stream))
+    torch.cuda.synchronize()
+    assert list(flips[:sweeps.value]) == list(extra["flips"])
+    out = tags.cpu().numpy()
+    kept = extra["tags"] >= 0
+    assert np.array_equal(out[kept], extra["tags"][kept])
+    # too small a workspace is refused, not overrun
+    assert L.gtf_tag_propagate(ctypes.byref(d.cg), ctypes.c_void_p(radius.data_ptr()),
+                               ctypes.c_void_p(tags.data_ptr()), 0.1, 64, ctypes.cast(flips, ctypes.c_void_p), ctypes.byref(sweeps),
+                               ctypes.c_void_p(ws.data_ptr()), nb - 1, d.stream) != 0

@@ -35,6 +35,9 @@ def test_library_loads_and_binds():
     assert L.gtf_version().decode().startswith("gtf")
     # workspace size is a pure host function
     assert L.gtf_workspace_bytes(100, 1000) >= 256 + 8 * 1000
+    # tag-propagation workspace: counters, keep [E], processed [N], the second tag array [N]
+    assert L.gtf_tag_workspace_bytes(100, 1000) >= 8 + 1000 + 100 + 8 * 100
+    assert L.gtf_tag_workspace_bytes(0, 0) > 0
 
 
 def test_struct_layout_matches_header():

@@ -313,26 +313,45 @@ def bench_components(g, params, dev, reps=5):
     out["a15_updated_state_distances"] = {"pairs": npairs, "wall_ms": dt * 1e3, "pairs_per_s": npairs / dt}
     tags = np.arange(g.n_nodes, dtype=np.int64)
     radius = np.ascontiguousarray(g.node["xyzr"][:, 3])
+    import ctypes
+    vp = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    rad = torch.from_numpy(np.ascontiguousarray(d._to_dev_nodes(radius))).to(dev)
+    t_init = torch.from_numpy(np.ascontiguousarray(d._to_dev_nodes(tags))).to(dev)
+    ta = torch.empty_like(t_init)
+    # the stage as a device-resident caller runs it: one gtf_tag_propagate call (prepare, the
+    # sweeps with their stop test on the device, one flip-count read per batch), wall time
+    # from the call to its return with the final tags in place
+    ts = []
+    for _ in range(reps + 1):
+        ta.copy_(t_init)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        flips = d.tag_propagation_dev(ta, rad)
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    dt = float(np.median(ts[1:]))
+    # the same with host-order inputs and outputs (upload, download, reordering: the Python API)
     ts = []
     for _ in range(reps + 1):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        _, flips = d.tag_propagation(tags, radius)
+        d.tag_propagation(tags, radius)
         torch.cuda.synchronize()
         ts.append(time.perf_counter() - t0)
-    dt = float(np.median(ts[1:]))
-    # the sweep kernel alone: K sweeps back to back between two events (no read-back)
-    import ctypes
-    vp = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    dt_host = float(np.median(ts[1:]))
+    # the prepare and sweep kernels alone: K calls back to back between two events
     keep = torch.zeros(max(g.n_edges, 1), dtype=torch.uint8, device=dev)
     proc = torch.zeros(max(g.n_nodes, 1), dtype=torch.uint8, device=dev)
     cnt = torch.zeros(2, dtype=torch.int32, device=dev)
-    rad = torch.from_numpy(np.ascontiguousarray(d._to_dev_nodes(radius))).to(dev)
-    ta = torch.from_numpy(np.ascontiguousarray(d._to_dev_nodes(tags))).to(dev)
     tb = torch.empty_like(ta)
-    d.lib.gtf_tag_prepare(ctypes.byref(d.cg), vp(rad), vp(keep), vp(proc), vp(cnt), d.stream)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     K = 50
+    e0.record()
+    for i in range(K):
+        d.lib.gtf_tag_prepare(ctypes.byref(d.cg), vp(rad), vp(keep), vp(proc), vp(cnt), d.stream)
+    e1.record()
+    torch.cuda.synchronize()
+    prep_ms = e0.elapsed_time(e1) / K
     e0.record()
     for i in range(K):
         d.lib.gtf_tag_sweep(ctypes.byref(d.cg), vp(keep), vp(proc), vp(ta if i % 2 == 0 else tb),
@@ -343,12 +362,18 @@ def bench_components(g, params, dev, reps=5):
     sweeps = len(flips)
     nbytes = 4 * g.n_edges + 8 * g.n_nodes   # SURVEY §8d B_tag, per sweep
     out["a16_tag_propagation"] = {"sweeps": sweeps, "flips": [int(x) for x in flips], "stage_wall_ms": dt * 1e3,
-                                  "sweep_call_ms": sweep_ms, "algorithmic_bytes_per_sweep": nbytes,
+                                  "stage_wall_host_order_ms": dt_host * 1e3,
+                                  "prepare_call_ms": prep_ms, "sweep_call_ms": sweep_ms,
+                                  "stage_over_kernels": dt * 1e3 / (prep_ms + sweeps * sweep_ms),
+                                  "algorithmic_bytes_per_sweep": nbytes,
                                   "achieved_GBps": nbytes / (sweep_ms * 1e-3) / 1e9,
                                   "frac_of_peak": nbytes / (sweep_ms * 1e-3) / 1e9 / rf.HBM_PEAK_GBS,
-                                  "note": "sweep_call_ms: K gtf_tag_sweep calls back to back between two events "
-                                          "(flip-counter reset + kernel); stage wall time includes the prepare pass "
-                                          "and the flip-count read-back after every sweep (the script's stop test)"}
+                                  "note": "stage_wall_ms: one gtf_tag_propagate call on device-resident tags / radius "
+                                          "(prepare, sweeps with the stop rule evaluated on the device, one flip-count "
+                                          "read per batch of sweeps), call to return; stage_over_kernels = that wall "
+                                          "time / (prepare + sweeps x sweep) kernel time; *_call_ms: K calls back to "
+                                          "back between two events; stage_wall_host_order_ms adds the host-order "
+                                          "upload, download and reordering of DeviceGraph.tag_propagation"}
     # a2: the initial per-edge states of event conversion (helper.py:238-452 + priors,
     # mixture weights, degree; pipeline.build_event's device half) on the same event
     def tse():
@@ -499,8 +524,10 @@ def bench_sharded(workload, rank, world, dev, steps, warmup, params, backend="nc
     from gtf import synth
     from gtf.device import DeviceGraph
     from gtf.shard import ShardedDeviceGraph
+    from gtf import roofline as rf
     g = synth.workload(workload, seed=0)
     sd = ShardedDeviceGraph(g, rank, world, dev, backend=backend)
+    torch_backend = "gloo" if backend == "gloo" else "nccl"
     snap = sd.d.snapshot(DeviceGraph.PASS_INPUTS)
     sd.d.clear_errors()
     for _ in range(warmup):
@@ -508,7 +535,13 @@ def bench_sharded(workload, rank, world, dev, steps, warmup, params, backend="nc
         sd.step(params)
     sd.d.stage_inputs(steps)   # step i runs on staged copy i of the pass input (as at N = 1)
 
-    def run(exchange):
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(steps)]
+    for row in evs:      # torch creates the HIP event on first record
+        for e in row:
+            e.record()
+    handles = [[e.cuda_event for e in row] for row in evs]
+
+    def run(exchange, instrumented=False):
         sd.d.fill_inputs(snap)
         torch.cuda.synchronize()
         dist.barrier()
@@ -519,21 +552,46 @@ def bench_sharded(workload, rank, world, dev, steps, warmup, params, backend="nc
             if exchange:
                 sd.step(params)
             else:
-                sd.pass_(params)
+                sd.pass_(params, events=handles[i] if instrumented else None)
         t_issue = time.perf_counter() - t0     # host time to enqueue the K steps
         torch.cuda.synchronize()
         dist.barrier()
         torch.cuda.synchronize()
         sd.d.use_inputs(None)
-        issue[exchange] = reduce_scalar(t_issue, dist.ReduceOp.MAX, dev, backend)
-        return reduce_scalar(time.perf_counter() - t0, dist.ReduceOp.MAX, dev, backend)
+        issue[exchange] = reduce_scalar(t_issue, dist.ReduceOp.MAX, dev, torch_backend)
+        return reduce_scalar(time.perf_counter() - t0, dist.ReduceOp.MAX, dev, torch_backend)
 
     issue = {}
     el = run(True)
     el_pass = run(False)
-    flags = int(reduce_scalar(sd.d.errors(), dist.ReduceOp.MAX, dev, backend))
-    hb = int(reduce_scalar(sd.halo_bytes, dist.ReduceOp.MAX, dev, backend))
+    run(False, instrumented=True)   # this rank's kernels between events (the sharded roofline)
+    flags = int(reduce_scalar(sd.d.errors(), dist.ReduceOp.MAX, dev, torch_backend))
+    hb = int(reduce_scalar(sd.halo_bytes, dist.ReduceOp.MAX, dev, torch_backend))
     pl = sd.plan
+
+    def avg(a, b):
+        return float(np.mean([evs[i][a].elapsed_time(evs[i][b]) for i in range(steps)]))
+
+    # this rank's owned receivers / slots / directed edges (the per-GPU sizes of the headline)
+    lo, hi = int(pl.slot_lo[rank]), int(pl.slot_hi[rank])
+    own_nodes = int(pl.node_hi[rank] - pl.node_lo[rank])
+    own_edges = int(sd.d.t["is_edge"][lo:hi].sum().item())
+    k_ms = {"k_sender": avg(0, 1), "k_extrapolate": avg(1, 2), NODE_KERNEL: avg(2, 3)}
+    node_b = rf.node_bytes(own_edges, own_nodes)
+    ext_b = rf.extrap_bytes(own_edges, own_nodes)
+    kr = {NODE_KERNEL: (k_ms[NODE_KERNEL], node_b),
+          "k_sender+k_extrapolate": (k_ms["k_sender"] + k_ms["k_extrapolate"], ext_b)}
+    kname = max(kr, key=lambda k: kr[k][0])
+    own_edges_max = int(reduce_scalar(own_edges, dist.ReduceOp.MAX, dev, torch_backend))
+    own_nodes_max = int(reduce_scalar(own_nodes, dist.ReduceOp.MAX, dev, torch_backend))
+    roof = {"bound": "hbm", "kernel": kname, "rank": rank, "achieved": kr[kname][1] / (kr[kname][0] * 1e-3) / 1e9,
+            "peak": rf.HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": kr[kname][1] / (kr[kname][0] * 1e-3) / 1e9 / rf.HBM_PEAK_GBS, "traffic": None,
+            "algorithmic_bytes_per_launch": kr[kname][1], "kernel_ms": kr[kname][0],
+            "kernel_ms_all": {k: round(v, 5) for k, v in k_ms.items()},
+            "owned_directed_edges": own_edges, "owned_nodes": own_nodes,
+            "byte_model": "SURVEY §8d on this rank's owned receivers and edges",
+            "timing": "HIP events around this rank's kernels (gtf_pass_shard), no exchange"}
     # tag propagation (a16) on the same sharded event: owned-wedge sweeps + one
     # all-reduce(MAX) per sweep; wall time of the whole stage, max over ranks
     try:
@@ -544,9 +602,10 @@ def bench_sharded(workload, rank, world, dev, steps, warmup, params, backend="nc
         t0 = time.perf_counter()
         _, tflips = sd.tag_propagation(tags, g.node["xyzr"][:, 3])
         torch.cuda.synchronize()
-        tag_s = reduce_scalar(time.perf_counter() - t0, dist.ReduceOp.MAX, dev, backend)
+        tag_s = reduce_scalar(time.perf_counter() - t0, dist.ReduceOp.MAX, dev, torch_backend)
         tag = {"ms": tag_s * 1e3, "sweeps": len(tflips), "flips": tflips,
-               "collective": "one all_reduce(MAX) of n_nodes + world int64 words per sweep"}
+               "collective": "one all_reduce(MAX) of n_nodes + world int64 words per sweep" +
+                             (" (libgtf gtf_tag_propagate_shard)" if backend == "native" else "")}
     except Exception as ex:   # reported; the headline stands
         tag = {"error": repr(ex)[:300]}
     return {"scaling": "strong", "n_gpus": world, "edges": g.n_edges, "nodes": g.n_nodes,
@@ -557,7 +616,11 @@ def bench_sharded(workload, rank, world, dev, steps, warmup, params, backend="nc
             "host_issue_note": "host time to enqueue the steps (max over ranks); close to ms_per_step = host-bound",
             "halo_bytes_per_rank_max": hb, "owned_slots_max": pl.cap_slots,
             "owned_slots_min": int((pl.slot_hi - pl.slot_lo).min()),
-            "collective": "all_to_all_single of per-destination halo segments (RCCL over xGMI)",
+            "owned_directed_edges_max": own_edges_max, "owned_nodes_max": own_nodes_max,
+            "collective": ("gtf_halo_exchange: per-destination halo segments, grouped ncclSend / ncclRecv inside "
+                           "libgtf (RCCL over xGMI)" if backend == "native" else
+                           "all_to_all_single of per-destination halo segments (RCCL over xGMI)"),
+            "roofline": roof,
             "node_order": "azimuthal wedges, tiled slot-count buckets inside each", "device_error_flags": flags, "backend": backend,
             "tag_propagation": tag}
 
@@ -660,8 +723,10 @@ def main():
     ap.add_argument("--layout", default="tiled", choices=["tiled", "padded", "schedule", "natural"],
                     help="device node order (DeviceGraph layout)")
     ap.add_argument("--tile", type=int, default=4096, help="nodes per tile of --layout tiled")
-    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
-                    help="torch.distributed backend for N > 1 (gloo: rehearsal with several ranks on one GPU)")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo", "native"],
+                    help="collectives for N > 1: nccl = torch.distributed over RCCL, native = libgtf's own RCCL "
+                         "communicator (gtf_comm_*, the id handed over torch.distributed), gloo = rehearsal with "
+                         "several ranks on one GPU")
     args = ap.parse_args()
     if args.gpus < 1:
         ap.error("--gpus must be >= 1")
@@ -687,7 +752,7 @@ def main():
     if world != args.gpus:
         raise SystemExit("bench.py: WORLD_SIZE=%d but --gpus %d" % (world, args.gpus))
     if world > 1:
-        if args.backend == "nccl":
+        if args.backend in ("nccl", "native"):
             dist.init_process_group("nccl", device_id=torch.device(dev))
         else:   # rehearsal of the N > 1 path with several ranks on one GPU (RCCL needs one GPU per rank)
             dist.init_process_group("gloo")
@@ -750,9 +815,10 @@ def main():
     flags = d.errors()
 
     total_edges = float(g.n_edges)
+    tb = "gloo" if args.backend == "gloo" else "nccl"   # the torch.distributed group's backend
     if world > 1:
-        elapsed = reduce_scalar(elapsed, dist.ReduceOp.MAX, dev, args.backend)
-        total_edges = reduce_scalar(total_edges, dist.ReduceOp.SUM, dev, args.backend)
+        elapsed = reduce_scalar(elapsed, dist.ReduceOp.MAX, dev, tb)
+        total_edges = reduce_scalar(total_edges, dist.ReduceOp.SUM, dev, tb)
 
     def avg(a, b):
         return float(np.mean([evs[i][a].elapsed_time(evs[i][b]) for i in range(K)]))
@@ -807,7 +873,7 @@ def main():
         comps = bench_components(g, p, dev)
     if world > 1 and not args.no_c5:
         try:
-            c5_sharded = bench_c5_sharded(dev, K, W, rank, world, args.backend)
+            c5_sharded = bench_c5_sharded(dev, K, W, rank, world, tb)
         except Exception as ex:   # reported, the headline stands
             c5_sharded = {"error": repr(ex)[:300]}
 
@@ -869,11 +935,23 @@ def main():
                         "parallelism": "event-parallel x%d (each rank its own C4 event, no collective)" % world,
                         "seed_per_rank": "1000 * rank"}
             out["event_replicas"] = replicas
+            out["rccl_world_size"] = dist.get_world_size()
             if sharded and "error" not in sharded:
                 out["value"] = sharded["edges_per_s"]
                 out["ms_per_step"] = sharded["ms_per_step"]
                 out["config"]["parallelism"] = "edge-sharded x%d (one event, azimuthal wedges, halo all-to-all)" % world
                 out["config"]["workload"] = "one pileup-200 TrackML-shaped event (configs[3]) across all GPUs"
+                # per-GPU sizes of the headline: the largest owned range, the event's totals beside them
+                out["config"]["nodes_per_gpu"] = sharded["owned_nodes_max"]
+                out["config"]["directed_edges_per_gpu"] = sharded["owned_directed_edges_max"]
+                out["config"]["event_nodes"] = sharded["nodes"]
+                out["config"]["event_directed_edges"] = sharded["edges"]
+                # the roofline of the headline: rank 0's kernels of the sharded pass (the replica
+                # pass's roofline stays under event_replicas)
+                replicas["roofline"] = out["roofline"]
+                replicas["kernel_ms"] = out["kernel_ms"]
+                out["roofline"] = sharded["roofline"]
+                out["kernel_ms"] = sharded["roofline"]["kernel_ms_all"]
                 out["sharded_single_event"] = sharded
                 if sharded["device_error_flags"]:
                     out["invalid"] = "sharded pass device_error_flags %d" % sharded["device_error_flags"]

@@ -116,7 +116,7 @@ struct WSrc {
     __device__ __forceinline__ bool in(int u) const { return u >= lo && u < hi; }
     // the LDS read at a clamped index always, the global one only outside the window: a
     // select of values (a select of an LDS and a global address miscompiles on gfx950)
-    __device__ __forceinline__ int at(int u) const { return min(max(u - lo, 0), hi - lo - 1); }
+    __device__ __forceinline__ int at(int u) const { return min(max(u - lo, 0), max(hi - lo - 1, 0)); }
     __device__ __forceinline__ double x(int u) const {
         const double a = sx[at(u)];
         return in(u) ? a : gx(*g, u);
@@ -592,7 +592,8 @@ k_parabolic_kl_win(gtf_kl_graph g, gtf_kl_out o) {
     const int node_lo = r[0], n0 = r[1], n1 = r[2], nb1 = r[3], nb2 = r[4], nb3 = r[5];
     const int64_t slot_lo = (int64_t)(uint32_t)r[6];
     const int64_t pair_lo = (int64_t)(uint32_t)r[7] | ((int64_t)r[8] << 32);
-    const int wlo = r[9], whi = r[10];
+    // the window never exceeds the LDS copy: nodes past wlo + WWIN are read from global memory
+    const int wlo = r[9], whi = min(r[10], wlo + WWIN);
     for (int i = (int)threadIdx.x; i < whi - wlo; i += WBLOCK) {
         sx[i] = gx(g, wlo + i);
         sy[i] = gy(g, wlo + i);

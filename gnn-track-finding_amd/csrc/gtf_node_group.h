@@ -121,19 +121,24 @@ struct NodeCtx {
     int v, lo, d, k;
     bool valid;
     uint8_t is_edge, rev_edge, act, act0;
-    double layer;
+    double layer;                   // sender layer (without the static classes)
+    uint64_t cls;                   // gtf_graph.slot_class of the slot (0 without)
+    uint8_t sfl;                    // gtf_graph.slot_sflags of the slot
+    bool use_cls;                   // the static classes cover this group (group-uniform)
+    bool live;                      // UTS entry's xyzr = gnn[slot_src] (gtf_states.fresh bit 1)
+    bool left;                      // side of the UTS entry (x < node x), with same_x
+    int src;                        // slot_src (read for the UTS clustering's coordinates)
     unsigned long long same_layer;  // lanes whose sender has this lane's layer (lazy)
     bool same_layer_ok;
     unsigned long long same_x;      // lanes whose stored UTS x equals this lane's (lazy; NaN: itself)
     bool same_x_ok;
     LaneDict tse, uts;
-    double lik, lr, x0, edge_mw, smw;
+    double lik, lr, edge_mw, smw;
     int8_t side;
     uint8_t fresh;
     bool uts_dirty_lr, edge_mw_dirty;
     int degree;
     bool degree_set;
-    double node_x;             // GNN_Measurement x of the node (reweight side test)
     double xa, za, ra;         // node attribute xyzr x, z, r (clustering tau geometry)
     uint8_t solo;              // node alone in its subgraph (mixture weights)
     bool staged;               // clustering operands already in the group's LDS stage (slot lanes)
@@ -238,6 +243,12 @@ __device__ __forceinline__ bool lane_active(const NodeCtx<G>& c, int rank) {
 // iteration per distinct layer value (leader election with a ballot).
 template <int G>
 __device__ __forceinline__ void g_priors(NodeCtx<G>& c, LaneDict& st, double* sval) {
+    if constexpr (G > 0 && G <= 32) {
+        if (!c.same_layer_ok && c.use_cls) {   // the graph-static classes (gtf_graph.slot_class)
+            c.same_layer = c.valid ? (c.cls & 0xffffffffull) : 0ull;
+            c.same_layer_ok = true;
+        }
+    }
 #if GTF_PAIRWISE_CLASSES
     if constexpr (G > 0 && G <= PAIRWISE_MAX_G) {
         if (!c.same_layer_ok) {
@@ -269,10 +280,18 @@ __device__ __forceinline__ void g_priors(NodeCtx<G>& c, LaneDict& st, double* sv
 }
 
 // calculate_side_norm_factor + reweight (helper.py:99-200), UTS only
+// the x of a UTS entry's stored coordinates: its sender's live GNN x (gtf_states.fresh bit 1,
+// extrapolate_merged_states.py:377) or the stored snapshot
 template <int G>
-__device__ __forceinline__ void g_reweight(NodeCtx<G>& c, double* sval, const double* gnn, double thr,
-                                           uint32_t* err) {
-    (void)gnn;
+__device__ __forceinline__ double uts_x(const NodeCtx<G>& c, const gtf_graph& g, const gtf_states& uts) {
+    if (!c.valid) return 0.0;
+    if (c.live) return g.gnn[4 * (int64_t)g.slot_src[c.k]];
+    return uts.xyzr[4 * (int64_t)c.k];
+}
+
+template <int G>
+__device__ __forceinline__ void g_reweight(NodeCtx<G>& c, double* sval, const gtf_graph& g, const gtf_states& uts,
+                                           double thr, uint32_t* err) {
     LaneDict& st = c.uts;
     const bool act = lane_active(c, st.rank);
     // last dict key = the present key with the largest rank (stale loop variable, :131,138);
@@ -286,38 +305,44 @@ __device__ __forceinline__ void g_reweight(NodeCtx<G>& c, double* sval, const do
     const int last = st.last;
     const int last_is_edge = c.grp.shfl((int)c.is_edge, last);
     const int last_act = c.grp.shfl((int)c.act, last);
-#if GTF_HOIST
-    const double node_x = c.node_x;
-#else
-    const double node_x = gnn[4 * (int64_t)c.v];
-#endif
-    const bool left = c.x0 < node_x;
-    // distinct x values per side (len(set(coords))): the classes of equal stored x are
-    // built once per node (one iteration per distinct value; a NaN is only equal to
-    // itself, as set() keeps every NaN object); a key counts if it is the first active
-    // key of its class -- equal x, same side
-#if GTF_PAIRWISE_CLASSES
-    if constexpr (G > 0 && G <= PAIRWISE_MAX_G) {
-        if (!c.same_x_ok) {
-            c.same_x = equal_lanes(c, sval, c.x0) | (c.valid ? (1ull << c.grp.gl) : 0ull);
+    // distinct x values per side (len(set(coords))): the classes of equal stored x, built
+    // once per node (a NaN is only equal to itself, as set() keeps every NaN object); a key
+    // counts if it is the first active key of its class -- equal x, same side. When every
+    // present key's x is its sender's live GNN x (the entries message passing wrote), the
+    // classes and sides are graph-static (gtf_graph.slot_class / slot_sflags); the present
+    // keys only shrink after this point (pruning), so they stay valid for the pass.
+    if constexpr (G > 0 && G <= 32) {
+        if (!c.same_x_ok && c.use_cls && !c.grp.any(c.valid && st.rank >= 0 && !c.live)) {
+            c.same_x = c.valid ? (c.cls >> 32) : 0ull;
+            c.left = (c.sfl & 1) != 0;
             c.same_x_ok = true;
         }
     }
-#endif
     if (!c.same_x_ok) {
-        bool done = !c.valid || c.x0 != c.x0;
-        c.same_x = c.valid ? (1ull << c.grp.gl) : 0ull;
-        while (true) {
-            const unsigned long long todo = c.grp.bits(!done);
-            if (!todo) break;
-            const int leader = __ffsll((long long)todo) - 1;
-            const double X = c.grp.shfl(c.x0, leader);
-            const bool mine = !done && c.x0 == X;
-            const unsigned long long m = c.grp.bits(mine);
-            if (mine) { c.same_x = m; done = true; }
+        const double x0 = uts_x(c, g, uts);
+        c.left = x0 < g.gnn[4 * (int64_t)c.v];
+#if GTF_PAIRWISE_CLASSES
+        if constexpr (G > 0 && G <= PAIRWISE_MAX_G) {
+            c.same_x = equal_lanes(c, sval, x0) | (c.valid ? (1ull << c.grp.gl) : 0ull);
+            c.same_x_ok = true;
         }
-        c.same_x_ok = true;
+#endif
+        if (!c.same_x_ok) {
+            bool done = !c.valid || x0 != x0;
+            c.same_x = c.valid ? (1ull << c.grp.gl) : 0ull;
+            while (true) {
+                const unsigned long long todo = c.grp.bits(!done);
+                if (!todo) break;
+                const int leader = __ffsll((long long)todo) - 1;
+                const double X = c.grp.shfl(x0, leader);
+                const bool mine = !done && x0 == X;
+                const unsigned long long m = c.grp.bits(mine);
+                if (mine) { c.same_x = m; done = true; }
+            }
+            c.same_x_ok = true;
+        }
     }
+    const bool left = c.left;
     const unsigned long long A = c.grp.bits(act);
     const bool first = act && (c.same_x & A & ((1ull << c.grp.gl) - 1ull)) == 0ull;
     const int dl = c.grp.count(first && left);
@@ -428,16 +453,20 @@ struct StageT {
 
 // the clustering operands of this lane's state, raw, at its slot lane
 template <typename Stage>
-__device__ __forceinline__ void stage_raw(Stage* stg, int li, const gtf_states& S, int64_t k) {
+__device__ __forceinline__ void stage_raw(Stage* stg, int li, const gtf_states& S, int64_t k, const double* gnn,
+                                          bool live, int src) {
     stg->a[li] = S.sv[3 * k];
     stg->b[li] = S.sv[3 * k + 1];
     stg->c[li] = S.sv[3 * k + 2];
     stg->tau[li] = S.tau[k];
     const double* cv = S.cov + 5 * k;
     stg->c00[li] = cv[0]; stg->c01[li] = cv[1]; stg->c10[li] = cv[2]; stg->c11[li] = cv[3]; stg->c22[li] = cv[4];
-    stg->q[li] = S.xyzr[4 * k];
-    stg->w[li] = S.xyzr[4 * k + 2];
-    stg->tg[li] = S.xyzr[4 * k + 3];
+    // the state's stored sender coordinates: the sender's live GNN ones for an entry message
+    // passing wrote (gtf_states.fresh bit 1), else the snapshot
+    const double* xp = live ? gnn + 4 * (int64_t)src : S.xyzr + 4 * k;
+    stg->q[li] = xp[0];
+    stg->w[li] = xp[2];
+    stg->tg[li] = xp[3];
 }
 
 template <typename Stage>
@@ -465,8 +494,8 @@ __device__ __forceinline__ TauGeo stage_geo(const Stage* s, int i, double szb2, 
 // (I1 + I2)^-1 serves both means.
 template <int G, typename Stage>
 __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf_states& S, LaneDict& st,
-                                          Stage* stg, const double* xyzr_node, double chi2_thr,
-                                          double kl_thr, const gtf_params& p, uint32_t* err) {
+                                          Stage* stg, const double* xyzr_node, const double* gnn, bool live,
+                                          double chi2_thr, double kl_thr, const gtf_params& p, uint32_t* err) {
 #if GTF_ABLATE == 1
     return;  // diagnostics build (tools/ablate_build.sh): no clustering work
 #endif
@@ -483,7 +512,7 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
     const double xa = xyzr_node[0], za = xyzr_node[2], ra = xyzr_node[3];
 #endif
     if (pres) {
-        if (!c.staged) stage_raw(stg, me_l, S, c.k);
+        if (!c.staged) stage_raw(stg, me_l, S, c.k, gnn, live, c.src);
         const Cov5 C = stage_cov(stg, me_l);
         const double x = stg->q[me_l], z = stg->w[me_l], r = stg->tg[me_l];
         const Cov5 I = inv_cov5(C);
@@ -641,8 +670,8 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
 // ---------------------------------------------------------------------------
 // the per-slot fields an op sequence reads from memory (the others it only writes)
 struct Need {
-    bool tse_rank, tse_prior, uts_rank, uts_mw, uts_prior, uts_lik, uts_x0, uts_fresh, send_mw;
-    bool node_x, node_xyzr, solo;   // the node's own scalars an op reads
+    bool tse_rank, tse_prior, uts_rank, uts_mw, uts_prior, uts_lik, uts_live, uts_fresh, send_mw;
+    bool src, node_xyzr, solo;   // slot_src (UTS clustering), the node's own scalars an op reads
 };
 
 template <int G>
@@ -693,25 +722,38 @@ __device__ __forceinline__ bool node_fields(NodeCtx<G>& c, const gtf_graph& g, c
     c.rev_edge = c.valid ? g.rev_edge[k] : 0;
     c.act = c.valid ? e.act[k] : 0;
     c.act0 = c.act;
-    if (g.slot_layer) {
+    // the graph-static classes of the slot (gtf_graph.slot_class) where they cover the group,
+    // else the sender layer the priors build them from
+    c.use_cls = G > 0 && G <= 32 && g.slot_class != nullptr;
+    c.cls = 0;
+    c.sfl = 0;
+    c.layer = NAN;
+    if (c.use_cls) {
+        if (c.valid) {
+            c.cls = g.slot_class[k];
+            c.sfl = g.slot_sflags[k];
+        }
+    } else if (g.slot_layer) {
         c.layer = c.valid ? g.slot_layer[k] : NAN;
     } else {
         const int src = c.valid ? g.slot_src[k] : -1;
         c.layer = src >= 0 ? g.layer[src] : NAN;
     }
+    c.src = (nd.src && c.valid) ? g.slot_src[k] : -1;
+    c.live = false;
+    c.left = false;
     c.same_layer = 0;
     c.same_layer_ok = false;
     c.same_x = 0;
     c.same_x_ok = false;
     c.tse = LaneDict{-1, 0.0, 0.0, 0, -1, false, 0, false};
     c.uts = LaneDict{-1, 0.0, 0.0, 0, -1, false, 0, false};
-    c.lik = 0; c.lr = 0; c.x0 = 0; c.edge_mw = 0; c.side = -1; c.fresh = 0;
+    c.lik = 0; c.lr = 0; c.edge_mw = 0; c.side = -1; c.fresh = 0;
     c.uts_dirty_lr = false; c.edge_mw_dirty = false; c.degree = 0; c.degree_set = false;
     c.staged = false;
 #if GTF_HOIST
     // the node's own scalars, in the same round of loads as the slot fields (loaded inside
     // an op, after its LDS fences, each one's latency would add to every wave's life)
-    if (nd.node_x) c.node_x = g.gnn[4 * (int64_t)c.v];
     if (nd.node_xyzr) {
         const double* xn = g.xyzr + 4 * (int64_t)c.v;
         c.xa = xn[0]; c.za = xn[2]; c.ra = xn[3];
@@ -727,8 +769,11 @@ __device__ __forceinline__ bool node_fields(NodeCtx<G>& c, const gtf_graph& g, c
         if (nd.uts_mw) c.uts.mw = uts.mw[k];
         if (nd.uts_prior) c.uts.prior = uts.prior[k];
         if (nd.uts_lik) c.lik = uts.lik[k];
-        if (nd.uts_x0) c.x0 = uts.xyzr[4 * (int64_t)k];
-        if (nd.uts_fresh) c.fresh = uts.fresh[k];
+        if (nd.uts_fresh || nd.uts_live) {
+            const uint8_t f = uts.fresh[k];
+            c.fresh = f & 1;          // written by the last message passing
+            c.live = (f & 2) != 0;    // its xyzr = gnn[slot_src]
+        }
         if (nd.send_mw) c.smw = e.send_mw[k];
     }
     return true;
@@ -765,7 +810,7 @@ __device__ __forceinline__ void node_op(NodeCtx<G>& c, const gtf_graph& g, gtf_n
     if constexpr (OP == OP_RANKS) g_ranks(c);
     if constexpr (OP == OP_PRIORS_TSE) { if (has_tse) g_priors(c, c.tse, sval); }
     if constexpr (OP == OP_PRIORS_UTS) { if (has_uts) g_priors(c, c.uts, sval); }
-    if constexpr (OP == OP_REWEIGHT_UTS) { if (has_uts) g_reweight(c, sval, g.gnn, p.reweight_threshold, w.err); }
+    if constexpr (OP == OP_REWEIGHT_UTS) { if (has_uts) g_reweight(c, sval, g, uts, p.reweight_threshold, w.err); }
     if constexpr (OP == OP_DEGREE) g_degree(c);
     if constexpr (OP == OP_PRUNE) g_prune(c, has_tse, has_uts, w.err);
 #if GTF_HOIST
@@ -776,10 +821,12 @@ __device__ __forceinline__ void node_op(NodeCtx<G>& c, const gtf_graph& g, gtf_n
     if constexpr (OP == OP_MW_UTS) { if (has_uts) g_mixture_weights(c, c.uts, g.solo[c.v], w.err); }
 #endif
     if constexpr (OP == OP_CLUSTER_TSE) {
-        if (has_tse) g_cluster(c, n, tse, c.tse, stg, g.xyzr + 4 * (int64_t)c.v, chi2_thr, kl_thr, p, w.err);
+        if (has_tse)
+            g_cluster(c, n, tse, c.tse, stg, g.xyzr + 4 * (int64_t)c.v, g.gnn, false, chi2_thr, kl_thr, p, w.err);
     }
     if constexpr (OP == OP_CLUSTER_UTS) {
-        if (has_uts) g_cluster(c, n, uts, c.uts, stg, g.xyzr + 4 * (int64_t)c.v, chi2_thr, kl_thr, p, w.err);
+        if (has_uts)
+            g_cluster(c, n, uts, c.uts, stg, g.xyzr + 4 * (int64_t)c.v, g.gnn, c.live, chi2_thr, kl_thr, p, w.err);
     }
 }
 
@@ -794,9 +841,9 @@ struct OpSeq {
     static constexpr bool fresh = ((OPS == OP_FRESH) || ...);
     static constexpr bool cluster_uts = ((OPS == OP_CLUSTER_UTS) || ...);
     static constexpr Need need{uses_tse, ((OPS == OP_CLUSTER_TSE) || ...), uses_uts, reweight,
-                               reweight || cluster_uts, reweight, reweight,
+                               reweight || cluster_uts, reweight, reweight || cluster_uts,
                                ((OPS == OP_RANKS) || ...) || fresh, fresh,
-                               reweight, cluster, ((OPS == OP_MW_TSE || OPS == OP_MW_UTS) || ...)};
+                               cluster_uts, cluster, ((OPS == OP_MW_TSE || OPS == OP_MW_UTS) || ...)};
 };
 
 // has_uts of the node; where the sequence finishes message passing (OP_FRESH) a node that
@@ -878,7 +925,8 @@ __device__ __forceinline__ void node_seq_body(const gtf_graph& g, gtf_nodes& n, 
 #else
         const bool maybe = c.valid;
 #endif
-        if (c.staged && maybe) stage_raw(stg, c.grp.gl, Q::cluster_uts ? uts : tse, c.k);
+        if (c.staged && maybe)
+            stage_raw(stg, c.grp.gl, Q::cluster_uts ? uts : tse, c.k, g.gnn, Q::cluster_uts && c.live, c.src);
     }
 #endif
     const bool has_tse = n.has_tse[c.v];
@@ -1047,7 +1095,7 @@ __global__ void __launch_bounds__(NBLOCK) k_node_group(gtf_graph g, gtf_nodes n,
     const int gi = (blockIdx.x * NBLOCK + (int)threadIdx.x) / G;
     const Need nd{(bool)ops.uses_tse, (bool)ops.uses_tse, (bool)ops.uses_uts, (bool)ops.uses_uts,
                   (bool)ops.uses_uts, (bool)ops.uses_uts, (bool)ops.uses_uts, (bool)ops.uses_uts,
-                  (bool)ops.uses_uts, true, true, true};
+                  (bool)ops.uses_uts, (bool)ops.uses_uts, true, true};
     if (!node_load(c, g, n, tse, uts, e, list, seg, count, gi, nd)) return;
     double* sval = s_val + (threadIdx.x & ~63);
     Stage* stg = s_stage + (int)threadIdx.x / G;

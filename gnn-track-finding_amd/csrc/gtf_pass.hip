@@ -282,6 +282,7 @@ __global__ void __launch_bounds__(BLOCK) k_extrapolate(gtf_graph g, gtf_nodes n,
     // everything indexed by its sender / receiver, issued before any early exit (the
     // exits would otherwise serialise each load behind the previous one's branch).
     const uint8_t is_edge = g.is_edge[k], act = e.act[k];
+    const uint8_t f_old = uts.fresh[k];   // bit 1 (live coordinates) survives a rejected extrapolation
     const int src = g.slot_src[k], v = g.slot_dst[k];
     // written by k_sender for active edges of merged senders: in out-edge order through
     // slot_outidx (one gather beside the sender's), or by slot
@@ -298,7 +299,7 @@ __global__ void __launch_bounds__(BLOCK) k_extrapolate(gtf_graph g, gtf_nodes n,
     const double* mcp = n.merged_cov + 5 * (int64_t)u;
     const double mc00 = mcp[0], mc01 = mcp[1], mc10 = mcp[2], mc22 = mcp[4];
     if (!is_edge || src < 0 || !hm || act != 1) {
-        uts.fresh[k] = 0;
+        if (f_old & 1) uts.fresh[k] = f_old & 2;
         return;
     }
 
@@ -361,7 +362,7 @@ __global__ void __launch_bounds__(BLOCK) k_extrapolate(gtf_graph g, gtf_nodes n,
     if (w.diag->edge_chi2) w.diag->edge_chi2[k] = chi2;   // diagnostics (gtf_set_diagnostics), off by default
     if (!(chi2 <= p.chi2_cut)) {                                                   // :298
         e.act[k] = 0;                                                              // :393
-        uts.fresh[k] = 0;
+        if (f_old & 1) uts.fresh[k] = f_old & 2;
         return;
     }
     const double lik = (1.0 / sqrt((2.0 * M_PI) * fabs(S))) * exp(-0.5 * chi2);  // :302-304
@@ -418,12 +419,29 @@ __global__ void __launch_bounds__(BLOCK) k_extrapolate(gtf_graph g, gtf_nodes n,
     uts.sv[3 * (int64_t)k + 2] = xu2;
     uts.tau[k] = tau;
     store_cov5(uts.cov, k, Cov5{P00, P01, P10, P11, vt + var_ms});
-    double* sx = uts.xyzr + 4 * (int64_t)k;
-    sx[0] = node_x; sx[1] = node_y; sx[2] = node_z; sx[3] = node_r;
     uts.lik[k] = lik;
     // mixture_weight = smw (:384) and the empty prior / lr / side of a fresh entry are set
-    // by the node kernel's OP_FRESH, merged with its own stores of those fields
-    uts.fresh[k] = 1;   // the receiver's has_uts flag follows in the node kernel (OP_FRESH)
+    // by the node kernel's OP_FRESH, merged with its own stores of those fields. The entry's
+    // 'xyzr' (:377) is the sender's GNN coordinates, which stay resident in g.gnn: bit 1
+    // marks it live instead of writing a 32-byte copy per accepted edge (gtf_uts_materialize
+    // writes it when it is read back or before g.gnn changes)
+    uts.fresh[k] = 3;   // the receiver's has_uts flag follows in the node kernel (OP_FRESH)
+}
+
+// gtf_uts_materialize: the stored 'xyzr' snapshot (extrapolate_merged_states.py:377) of every
+// entry whose coordinates are live (fresh bit 1)
+__global__ void __launch_bounds__(BLOCK) k_uts_materialize(gtf_graph g, gtf_states uts) {
+    const int k = blockIdx.x * BLOCK + threadIdx.x;
+    if (k >= g.n_slots) return;
+    const uint8_t f = uts.fresh[k];
+    if (!(f & 2)) return;
+    const int u = g.slot_src[k];
+    if (u >= 0) {
+        const double* x = g.gnn + 4 * (int64_t)u;
+        double* y = uts.xyzr + 4 * (int64_t)k;
+        y[0] = x[0]; y[1] = x[1]; y[2] = x[2]; y[3] = x[3];
+    }
+    uts.fresh[k] = f & 1;
 }
 
 // ---------------------------------------------------------------------------
@@ -478,6 +496,13 @@ __device__ __forceinline__ bool edge_active(const gtf_graph& g, const gtf_edges&
     return g.is_edge[k] && e.act[k] == 1;
 }
 
+// the stored sender coordinates of state k: the sender's live GNN ones (gtf_states.fresh
+// bit 1, UTS only) or the snapshot
+__device__ __forceinline__ const double* state_xyzr(const gtf_graph& g, const gtf_states& st, int k) {
+    if (st.fresh && (st.fresh[k] & 2)) return g.gnn + 4 * (int64_t)g.slot_src[k];
+    return st.xyzr + 4 * (int64_t)k;
+}
+
 // compute_prior_probabilities for one node (helper.py:30-63)
 __device__ void node_priors(const gtf_graph& g, const gtf_edges& e, const gtf_states& st, Seg s) {
     for (int k = s.lo; k < s.hi; k++) {
@@ -502,12 +527,12 @@ __device__ void node_reweight(const gtf_graph& g, gtf_edges& e, gtf_states& st, 
     int nl = 0, nr = 0, dl = 0, dr = 0;
     for (int k = s.lo; k < s.hi; k++) {
         if (st.rank[k] < 0 || !edge_active(g, e, k)) continue;
-        const double xk = st.xyzr[4 * (int64_t)k];
+        const double xk = state_xyzr(g, st, k)[0];
         const bool left = xk < node_x;
         bool dup = false;  // distinct x values per side: len(set(coords))
         for (int j = s.lo; j < k; j++) {
             if (st.rank[j] < 0 || !edge_active(g, e, j)) continue;
-            const double xj = st.xyzr[4 * (int64_t)j];
+            const double xj = state_xyzr(g, st, j)[0];
             if ((xj < node_x) == left && xj == xk) { dup = true; break; }
         }
         if (left) { nl++; if (!dup) dl++; } else { nr++; if (!dup) dr++; }
@@ -517,7 +542,7 @@ __device__ void node_reweight(const gtf_graph& g, gtf_edges& e, gtf_states& st, 
         const bool last_act = g.is_edge[last] && e.act[last] == 1;
         for (int k = s.lo; k < s.hi; k++) {
             if (st.rank[k] < 0 || !edge_active(g, e, k)) continue;
-            const bool left = st.xyzr[4 * (int64_t)k] < node_x;
+            const bool left = state_xyzr(g, st, k)[0] < node_x;
             st.side[k] = left ? 0 : 1;
             st.lr[k] = last_act ? (double)(left ? dl : dr) : 1.0;
         }
@@ -558,7 +583,7 @@ __device__ void node_mixture_weights(const gtf_graph& g, gtf_states& st, Seg s, 
 // the fields of the entries message passing (re)wrote (g_fresh, thread-per-node form)
 __device__ void node_fresh(gtf_nodes& n, gtf_states& uts, const gtf_edges& e, Seg s, int v) {
     for (int k = s.lo; k < s.hi; k++)
-        if (uts.fresh[k]) {
+        if (uts.fresh[k] & 1) {
             n.has_uts[v] = 1;
             uts.mw[k] = e.send_mw[k];
             uts.prior[k] = NAN;
@@ -574,7 +599,7 @@ __device__ void node_assign_ranks(gtf_states& uts, Seg s) {
     for (int k = s.lo; k < s.hi; k++) next = max(next, uts.rank[k]);
     next += 1;
     for (int k = s.lo; k < s.hi; k++)
-        if (uts.fresh[k] && uts.rank[k] < 0) uts.rank[k] = next++;
+        if ((uts.fresh[k] & 1) && uts.rank[k] < 0) uts.rank[k] = next++;
 }
 
 // remove_state_metadata pruning (remove_state_metadata.py:31-48)
@@ -614,7 +639,7 @@ __device__ void node_cluster(const gtf_graph& g, gtf_nodes& n, const gtf_states&
             const int kj = ord[j];
             const Cov5 cj = load_cov5(st.cov, kj);
             const double D = mahalanobis(ai, bi, ci, st.sv[3 * (int64_t)kj], st.sv[3 * (int64_t)kj + 1], cj, na,
-                                         st.xyzr + 4 * (int64_t)ki, st.xyzr + 4 * (int64_t)kj, p.sigma0rz2,
+                                         state_xyzr(g, st, ki), state_xyzr(g, st, kj), p.sigma0rz2,
                                          p.sigma0rz, p.sigma0rz, p.sigma0rz2, p.endcap_boundary);
             if (D == 0.0) continue;  // zeros are excluded (np.nonzero)
             any_nonzero = true;
@@ -736,7 +761,11 @@ __global__ void __launch_bounds__(BLOCK) k_node(gtf_graph g, gtf_nodes n, gtf_st
             case OP_MW_TSE: if (n.has_tse[v]) node_mixture_weights(g, tse, s, v, w.err); break;
             case OP_MW_UTS: if (n.has_uts[v]) node_mixture_weights(g, uts, s, v, w.err); break;
             case OP_CLUSTER_TSE:
-                if (n.has_tse[v]) node_cluster(g, n, tse, e, s, v, chi2_thr, kl_thr, p, w.err);
+                if (n.has_tse[v]) {
+                    gtf_states t = tse;
+                    t.fresh = nullptr;   // TSE coordinates are always the stored ones
+                    node_cluster(g, n, t, e, s, v, chi2_thr, kl_thr, p, w.err);
+                }
                 break;
             case OP_CLUSTER_UTS:
                 if (n.has_uts[v]) node_cluster(g, n, uts, e, s, v, chi2_thr, kl_thr, p, w.err);
@@ -1018,6 +1047,25 @@ extern "C" {
 size_t gtf_workspace_bytes(int32_t n_nodes, int32_t n_slots) {
     (void)n_nodes;
     return 256 + align256(sizeof(double) * (size_t)(n_slots > 0 ? n_slots : 1));
+}
+
+int gtf_workspace_init(void* ws, gtf_stream_t stream) {
+    hipError_t e = hipMemsetAsync(ws, 0, 256, (hipStream_t)stream);   // error word + gtf_diag (no diagnostics)
+    return e == hipSuccess ? 0 : fail("workspace init", e);
+}
+
+int gtf_uts_materialize(const gtf_graph* g, gtf_states* uts, gtf_stream_t stream) {
+    int rc = check_graph(g);
+    if (rc) return rc;
+    if (!uts) { snprintf(g_err, sizeof(g_err), "gtf_uts_materialize: null states"); return -2; }
+    if (g->n_slots > 0 && (!uts->fresh || !uts->xyzr || !g->slot_src || !g->gnn)) {
+        snprintf(g_err, sizeof(g_err), "gtf_uts_materialize: needs uts->fresh, uts->xyzr, g->slot_src and g->gnn");
+        return -2;
+    }
+    if (g->n_slots > 0)
+        hipLaunchKernelGGL(k_uts_materialize, dim3(grid(g->n_slots)), dim3(BLOCK), 0, (hipStream_t)stream, *g, *uts);
+    hipError_t err = hipGetLastError();
+    return err == hipSuccess ? 0 : fail("materialize launch", err);
 }
 
 int gtf_clear_errors(void* ws, gtf_stream_t stream) {

@@ -6,6 +6,7 @@
 // single atomic per wave.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
 
 #include "../../include/gtf.h"
 #include "gtf_math.h"
@@ -34,9 +35,104 @@ __global__ void __launch_bounds__(BLOCK) k_tag_prepare(gtf_graph g, const double
     if ((threadIdx.x & 63) == 0 && b) atomicAdd(n_processed, (int)__popcll(b));
 }
 
+// The same on the sender schedule's lane groups (gtf_graph.out_sched + out_lanes): every lane
+// reads its out-edge's neighbour radius in one round beside the node's own, a group ballot
+// gives processed[u]; nodes without an out-edge are not processed (the launch's last blocks)
+template <int G>
+__device__ __forceinline__ int prep_group(const gtf_graph& g, const double* radius, uint8_t* keep, uint8_t* processed,
+                                          const int4* list, const int2* lanes, int count, int b) {
+    const int t = b * BLOCK + (int)threadIdx.x;
+    const int gi = t / G, gl = t & (G - 1);
+    if (gi >= count) return 0;   // group-uniform
+    const int4 en = list[gi];
+    const int u = en.x;
+    const double ru = radius[u];
+    bool any = false;
+    if (lanes) {   // one out-edge per lane (<= G of them)
+        const int2 kv = lanes[t];
+        const bool edge = kv.x >= 0;
+        const double rw = radius[edge ? kv.y : u];
+        const bool k = edge && !(rw > ru);
+        if (edge) keep[en.y + gl] = (uint8_t)k;
+        any = k;
+    } else {       // chunks of G out-edges
+        for (int i = en.y + gl; i < en.z; i += G) {
+            const int w = g.out_dst ? g.out_dst[i] : g.slot_dst[g.out_slot[i]];
+            const bool k = !(radius[w] > ru);
+            keep[i] = (uint8_t)k;
+            any = any || k;
+        }
+    }
+    const unsigned long long m = __ballot(any);
+    const bool grp_any = G == 64 ? m != 0ull : ((m >> (t & 63 & ~(G - 1))) & ((1ull << G) - 1ull)) != 0ull;
+    if (gl == 0) processed[u] = (uint8_t)grp_any;
+    return gl == 0 && grp_any;
+}
+
+struct PrepBuckets {
+    const int4* list[3];
+    const int2* lanes[2];
+    int32_t count[3];
+    int32_t blocks[3];
+};
+
+__global__ void __launch_bounds__(BLOCK) k_tag_prepare_sched(gtf_graph g, const double* radius, uint8_t* keep,
+                                                             uint8_t* processed, int32_t* n_processed, PrepBuckets pb) {
+    int b = blockIdx.x, mine = 0;
+    if (b < pb.blocks[0]) {
+        mine = prep_group<4>(g, radius, keep, processed, pb.list[0], pb.lanes[0], pb.count[0], b);
+    } else if ((b -= pb.blocks[0]) < pb.blocks[1]) {
+        mine = prep_group<8>(g, radius, keep, processed, pb.list[1], pb.lanes[1], pb.count[1], b);
+    } else if ((b -= pb.blocks[1]) < pb.blocks[2]) {
+        mine = prep_group<16>(g, radius, keep, processed, pb.list[2], nullptr, pb.count[2], b);
+    } else {
+        const int u = (b - pb.blocks[2]) * BLOCK + (int)threadIdx.x;
+        if (u < g.n_nodes && g.out_ptr[u + 1] == g.out_ptr[u]) processed[u] = 0;
+        return;
+    }
+    const unsigned long long m = __ballot(mine);
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(n_processed, (int)__popcll(m));
+}
+
+// The stop rule of the sweep loop on the device (tag_propagation.py:130-164): sweep s runs
+// only while the previous sweep flipped more than flip_threshold of the processed nodes
+// (frac = 0 when none are processed, where the reference divides by zero), so a batch of
+// sweeps is enqueued without a host read between them and the sweeps past the stop return
+// at once. Every block takes the same decision from the finished previous sweep's count.
+struct TagCtl {
+    const int32_t* total;   // processed count (gtf_tag_prepare)
+    const int32_t* prev;    // flips of the previous sweep, NULL for the first
+    int32_t* stop;          // set once the rule stops the loop
+    int32_t* nexec;         // sweeps executed
+    double thr;
+};
+
+__device__ __forceinline__ bool tag_skip(const TagCtl& c) {
+    if (!c.stop) return false;
+    if (*c.stop) return true;
+    if (c.prev) {
+        const int32_t tot = *c.total, f = *c.prev;
+        const double frac = tot ? (double)f / (double)tot : 0.0;
+        if (!(frac > c.thr)) {
+            if (blockIdx.x == 0 && threadIdx.x == 0) atomicExch(c.stop, 1);
+            return true;
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(c.nexec, 1);
+    return false;
+}
+
+// the final tags into the caller's array: after an odd number of executed sweeps they sit
+// in the workspace copy (sweep s reads buffer s % 2 and writes the other)
+__global__ void __launch_bounds__(BLOCK) k_tag_final(int64_t* tags, const int64_t* other, const int32_t* nexec, int n) {
+    const int u = blockIdx.x * BLOCK + threadIdx.x;
+    if (u < n && (*nexec & 1)) tags[u] = other[u];
+}
+
 // tags_out[u] = max(tags_in[u], tags_in[kept successors]) (:141-150 -- max, not min)
 __global__ void __launch_bounds__(BLOCK) k_tag_sweep(gtf_graph g, const uint8_t* keep, const uint8_t* processed,
-                                                     const int64_t* tin, int64_t* tout, int32_t* flips) {
+                                                     const int64_t* tin, int64_t* tout, int32_t* flips, TagCtl ctl) {
+    if (tag_skip(ctl)) return;
     const int u = gtf::xcd_local(blockIdx.x, gridDim.x) * BLOCK + threadIdx.x;
     int flipped = 0;
     if (u < g.n_nodes) {
@@ -120,7 +216,8 @@ struct TagBuckets {
 
 __global__ void __launch_bounds__(BLOCK) k_tag_sweep_sched(gtf_graph g, const uint8_t* keep, const uint8_t* processed,
                                                            const int64_t* tin, int64_t* tout, int32_t* flips,
-                                                           TagBuckets tb) {
+                                                           TagBuckets tb, TagCtl ctl) {
+    if (tag_skip(ctl)) return;
     int b = blockIdx.x, flipped = 0;
     if (b < tb.blocks[0]) {
         flipped = tb.lanes[0] ? tag_group_lanes<4>(g, keep, processed, tin, tout, tb.list[0], tb.lanes[0], tb.count[0], b)
@@ -172,22 +269,46 @@ __global__ void __launch_bounds__(BLOCK) k_tag_sweep_owned(gtf_graph g, const ui
 
 extern "C" {
 
+static int hip_fail(const char* what) {
+    char m[256];
+    snprintf(m, sizeof(m), "%s: %s", what, hipGetErrorString(hipGetLastError()));
+    gtf::set_error(m);
+    return -1;
+}
+
 int gtf_tag_prepare(const gtf_graph* g, const double* radius, uint8_t* keep, uint8_t* processed,
                     int32_t* n_processed, gtf_stream_t stream) {
     if (int rc = gtf::check_abi(g, "gtf_tag_prepare")) return rc;
     hipStream_t st = (hipStream_t)stream;
-    if (hipMemsetAsync(n_processed, 0, sizeof(int32_t), st) != hipSuccess) return -1;
-    if (g->n_nodes > 0)
+    if (hipMemsetAsync(n_processed, 0, sizeof(int32_t), st) != hipSuccess) return hip_fail("gtf_tag_prepare");
+    if (g->n_nodes > 0 && g->out_sched) {   // lane groups over the sender schedule
+        PrepBuckets pb;
+        const int cnt[3] = {g->n_o4, g->n_o8, g->n_o16}, gs[3] = {4, 8, 16};
+        const int4* l = reinterpret_cast<const int4*>(g->out_sched);
+        const int2* ln = reinterpret_cast<const int2*>(g->out_lanes);
+        pb.lanes[0] = ln;
+        pb.lanes[1] = ln ? ln + 4 * g->n_o4 : nullptr;
+        int total = 0;
+        for (int q = 0; q < 3; q++) {
+            pb.list[q] = l;
+            l += cnt[q];
+            pb.count[q] = cnt[q];
+            pb.blocks[q] = (cnt[q] + BLOCK / gs[q] - 1) / (BLOCK / gs[q]);
+            total += pb.blocks[q];
+        }
+        total += (g->n_nodes + BLOCK - 1) / BLOCK;   // nodes without an out-edge
+        hipLaunchKernelGGL(k_tag_prepare_sched, dim3(total), dim3(BLOCK), 0, st, *g, radius, keep, processed,
+                           n_processed, pb);
+    } else if (g->n_nodes > 0) {
         hipLaunchKernelGGL(k_tag_prepare, dim3((g->n_nodes + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, st, *g, radius,
                            keep, processed, n_processed);
-    return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : hip_fail("gtf_tag_prepare launch");
 }
 
-int gtf_tag_sweep(const gtf_graph* g, const uint8_t* keep, const uint8_t* processed, const int64_t* tags_in,
-                  int64_t* tags_out, int32_t* flips, gtf_stream_t stream) {
-    if (int rc = gtf::check_abi(g, "gtf_tag_sweep")) return rc;
-    hipStream_t st = (hipStream_t)stream;
-    if (hipMemsetAsync(flips, 0, sizeof(int32_t), st) != hipSuccess) return -1;
+static int tag_sweep(const gtf_graph* g, const uint8_t* keep, const uint8_t* processed, const int64_t* tags_in,
+                     int64_t* tags_out, int32_t* flips, const TagCtl& ctl, hipStream_t st) {
+    if (hipMemsetAsync(flips, 0, sizeof(int32_t), st) != hipSuccess) return hip_fail("gtf_tag_sweep");
     if (g->n_nodes > 0 && g->out_sched) {   // lane groups over the sender schedule
         TagBuckets tb;
         const int cnt[3] = {g->n_o4, g->n_o8, g->n_o16}, gs[3] = {4, 8, 16};
@@ -207,25 +328,39 @@ int gtf_tag_sweep(const gtf_graph* g, const uint8_t* keep, const uint8_t* proces
         total += tb.copy_blocks;
         if (total > 0)
             hipLaunchKernelGGL(k_tag_sweep_sched, dim3(total), dim3(BLOCK), 0, st, *g, keep, processed, tags_in,
-                               tags_out, flips, tb);
+                               tags_out, flips, tb, ctl);
     } else if (g->n_nodes > 0) {
         hipLaunchKernelGGL(k_tag_sweep, dim3((g->n_nodes + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, st, *g, keep,
-                           processed, tags_in, tags_out, flips);
+                           processed, tags_in, tags_out, flips, ctl);
     }
-    return hipGetLastError() == hipSuccess ? 0 : -1;
+    return hipGetLastError() == hipSuccess ? 0 : hip_fail("gtf_tag_sweep launch");
+}
+
+int gtf_tag_sweep(const gtf_graph* g, const uint8_t* keep, const uint8_t* processed, const int64_t* tags_in,
+                  int64_t* tags_out, int32_t* flips, gtf_stream_t stream) {
+    if (int rc = gtf::check_abi(g, "gtf_tag_sweep")) return rc;
+    const TagCtl none{nullptr, nullptr, nullptr, nullptr, 0.0};
+    return tag_sweep(g, keep, processed, tags_in, tags_out, flips, none, (hipStream_t)stream);
 }
 
 static size_t tag_align(size_t x) { return (x + 255) & ~size_t(255); }
 
+// the stop-rule words of gtf_tag_propagate: processed count, stop flag, executed sweeps, then
+// a ring of per-sweep flip counts
+constexpr int TAG_RING = 1024;
+constexpr size_t TAG_HDR = 4 * sizeof(int32_t) + TAG_RING * sizeof(int32_t);
+
 size_t gtf_tag_workspace_bytes(int32_t n_nodes, int32_t n_edges) {
     const size_t n = n_nodes > 0 ? (size_t)n_nodes : 1, e = n_edges > 0 ? (size_t)n_edges : 1;
-    return tag_align(2 * sizeof(int32_t)) + tag_align(e) + tag_align(n) + tag_align(sizeof(int64_t) * n);
+    return tag_align(TAG_HDR) + tag_align(e) + tag_align(n) + tag_align(sizeof(int64_t) * n);
 }
 
-// The whole stage behind one call: prepare, then sweeps until flips / processed <= the
-// threshold (the loop of tag_propagation.py:130-164, first sweep unconditional), the tag
-// arrays ping-ponging between `tags` and the workspace; one stream synchronisation per
-// sweep, where the stop rule reads the flip count.
+// The whole stage behind one call: prepare, then the sweeps (the loop of
+// tag_propagation.py:130-164, first sweep unconditional) in batches of 2, 4, 8, ... launches
+// whose stop test runs on the device (TagCtl), the tag arrays ping-ponging between `tags` and
+// the workspace; the host reads the batch's flip counts once per batch (one stream
+// synchronisation) and stops as soon as the rule has. The final tags land in `tags` by a
+// device copy when the executed count is odd.
 int gtf_tag_propagate(const gtf_graph* g, const double* radius, int64_t* tags, double flip_threshold,
                       int32_t max_sweeps, int32_t* flips_out, int32_t* sweeps_out, void* workspace,
                       size_t workspace_bytes, gtf_stream_t stream) {
@@ -242,44 +377,53 @@ int gtf_tag_propagate(const gtf_graph* g, const double* radius, int64_t* tags, d
     hipStream_t st = (hipStream_t)stream;
     const size_t n = g->n_nodes > 0 ? (size_t)g->n_nodes : 1, e = n_edges > 0 ? (size_t)n_edges : 1;
     char* w = static_cast<char*>(workspace);
-    int32_t* cnt = reinterpret_cast<int32_t*>(w);   // [0] processed, [1] flips
-    w += tag_align(2 * sizeof(int32_t));
+    int32_t* hdr = reinterpret_cast<int32_t*>(w);   // [0] processed [1] stop [2] executed [3] - [4..] flip ring
+    int32_t* ring = hdr + 4;
+    w += tag_align(TAG_HDR);
     uint8_t* keep = reinterpret_cast<uint8_t*>(w);
     w += tag_align(e);
     uint8_t* proc = reinterpret_cast<uint8_t*>(w);
     w += tag_align(n);
     int64_t* other = reinterpret_cast<int64_t*>(w);
     *sweeps_out = 0;
-    if (int rc = gtf_tag_prepare(g, radius, keep, proc, cnt, stream)) return rc;
-    int32_t total = 0;
-    if (hipMemcpyAsync(&total, cnt, sizeof(int32_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess) {
-        gtf::set_error("gtf_tag_propagate: reading the processed count failed");
-        return -1;
-    }
-    int64_t* cur = tags;
-    int64_t* nxt = other;
-    double frac = 1.0;
-    int32_t s = 0;
-    while (frac > flip_threshold && s < max_sweeps) {
-        if (int rc = gtf_tag_sweep(g, keep, proc, cur, nxt, cnt + 1, stream)) return rc;
-        int32_t f = 0;
-        if (hipMemcpyAsync(&f, cnt + 1, sizeof(int32_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
-            hipStreamSynchronize(st) != hipSuccess) {
-            gtf::set_error("gtf_tag_propagate: reading the flip count failed");
-            return -1;
+    if (hipMemsetAsync(hdr, 0, 4 * sizeof(int32_t), st) != hipSuccess) return hip_fail("gtf_tag_propagate");
+    if (int rc = gtf_tag_prepare(g, radius, keep, proc, hdr, stream)) return rc;
+    int32_t s = 0, batch = 2, executed = 0;
+    int32_t host[4 + TAG_RING];
+    bool stopped = false;
+    while (!stopped && s < max_sweeps) {
+        const int32_t at = s % TAG_RING;
+        int32_t nb = batch < max_sweeps - s ? batch : max_sweeps - s;
+        if (nb > TAG_RING - at) nb = TAG_RING - at;   // the batch's counts stay contiguous in the ring
+        for (int32_t i = 0; i < nb; i++) {
+            const int32_t q = s + i;
+            const TagCtl ctl{hdr, q > 0 ? ring + (q - 1) % TAG_RING : nullptr, hdr + 1, hdr + 2, flip_threshold};
+            int64_t* tin = (q & 1) ? other : tags;
+            int64_t* tout = (q & 1) ? tags : other;
+            if (int rc = tag_sweep(g, keep, proc, tin, tout, ring + q % TAG_RING, ctl, st)) return rc;
         }
-        if (flips_out) flips_out[s] = f;
-        s++;
-        frac = total ? (double)f / (double)total : 0.0;
-        int64_t* t = cur;
-        cur = nxt;
-        nxt = t;
+        if (hipMemcpyAsync(host, hdr, 4 * sizeof(int32_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipMemcpyAsync(host + 4 + at, ring + at, nb * sizeof(int32_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            return hip_fail("gtf_tag_propagate: reading the flip counts");
+        executed = host[2];
+        for (int32_t q = s; q < executed; q++) {
+            const int32_t f = host[4 + q % TAG_RING];
+            if (flips_out) flips_out[q] = f;
+            // the rule on the host too: the batch's last executed sweep may already stop it
+            const double frac = host[0] ? (double)f / (double)host[0] : 0.0;
+            if (q == executed - 1 && !(frac > flip_threshold)) stopped = true;
+        }
+        stopped = stopped || host[1] != 0 || executed < s + nb;
+        s = executed;
+        if (batch < TAG_RING / 2) batch *= 2;
     }
-    *sweeps_out = s;
-    if (cur != tags && g->n_nodes > 0 &&
-        hipMemcpyAsync(tags, cur, sizeof(int64_t) * (size_t)g->n_nodes, hipMemcpyDeviceToDevice, st) != hipSuccess)
-        return -1;
+    *sweeps_out = executed;
+    if (g->n_nodes > 0) {
+        hipLaunchKernelGGL(k_tag_final, dim3((g->n_nodes + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, st, tags, other,
+                           hdr + 2, g->n_nodes);
+        if (hipGetLastError() != hipSuccess) return hip_fail("gtf_tag_propagate: final copy");
+    }
     return 0;
 }
 
@@ -294,12 +438,13 @@ int gtf_tag_sweep_shard(const gtf_graph* g, const uint8_t* keep, const uint8_t* 
     }
     hipStream_t st = (hipStream_t)stream;
     int64_t* words = tags_out + g->n_nodes;   // the nranks flip-count words
-    if (hipMemsetAsync(words, 0, sizeof(int64_t) * (size_t)nranks, st) != hipSuccess) return -1;
+    if (hipMemsetAsync(words, 0, sizeof(int64_t) * (size_t)nranks, st) != hipSuccess)
+        return hip_fail("gtf_tag_sweep_shard");
     if (g->n_nodes > 0)
         hipLaunchKernelGGL(k_tag_sweep_owned, dim3((g->n_nodes + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, st, *g, keep,
                            processed, tags_in, tags_out, shard->node_lo, shard->node_hi,
                            reinterpret_cast<unsigned long long*>(words + rank));
-    return hipGetLastError() == hipSuccess ? 0 : -1;
+    return hipGetLastError() == hipSuccess ? 0 : hip_fail("gtf_tag_sweep_shard launch");
 }
 
 }  // extern "C"

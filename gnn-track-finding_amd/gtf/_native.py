@@ -16,7 +16,7 @@ F64 = ctypes.c_double
 
 
 U32 = ctypes.c_uint32
-ABI_VERSION = 4   # GTF_ABI_VERSION of include/gtf.h
+ABI_VERSION = 5   # GTF_ABI_VERSION of include/gtf.h
 
 
 class GtfGraph(ctypes.Structure):
@@ -31,7 +31,7 @@ class GtfGraph(ctypes.Structure):
                 ("out_sched", P), ("n_o4", I32), ("n_o8", I32), ("n_o16", I32), ("n_g2", I32),
                 ("pack_ent", P), ("pack_wave", P), ("n_pack_waves", I32), ("out_lanes", P),
                 ("pad_tiles", I32), ("pad_tile_nodes", I32), ("pad_tile_slots", I32), ("pad_count", I32 * 6),
-                ("pad_reserved_", I32), ("slot_outidx", P)]
+                ("pad_reserved_", I32), ("slot_outidx", P), ("slot_class", P), ("slot_sflags", P)]
 
     def __init__(self, **fields):
         super().__init__(**fields)
@@ -111,6 +111,7 @@ class GtfDiag(ctypes.Structure):
 
 
 DIAG_OFFSET = 64
+COMM_ID_BYTES = 128   # GTF_COMM_ID_BYTES
 
 
 class GtfPairOut(ctypes.Structure):
@@ -138,7 +139,7 @@ ERR_FLAGS = {
 }
 
 # exported symbols (must match include/gtf.h; tests check the .so exports all of them)
-SYMBOLS = ["gtf_workspace_bytes", "gtf_clear_errors", "gtf_read_errors", "gtf_extrapolate", "gtf_update",
+SYMBOLS = ["gtf_workspace_bytes", "gtf_workspace_init", "gtf_uts_materialize", "gtf_clear_errors", "gtf_read_errors", "gtf_extrapolate", "gtf_update",
            "gtf_message_passing", "gtf_node_ops",
            "gtf_cluster", "gtf_pass", "gtf_pass_ev", "gtf_tag_prepare", "gtf_tag_sweep", "gtf_tag_sweep_shard", "gtf_tag_workspace_bytes", "gtf_tag_propagate", "gtf_parabolic_kl", "gtf_track_state_estimates", "gtf_pass_shard",
            "gtf_shard_chunk_bytes", "gtf_shard_pack", "gtf_shard_unpack", "gtf_halo_pack", "gtf_halo_unpack",
@@ -148,6 +149,9 @@ SYMBOLS = ["gtf_workspace_bytes", "gtf_clear_errors", "gtf_read_errors", "gtf_ex
            "gtf_updated_state_pair_counts", "gtf_updated_state_distances", "gtf_set_diagnostics",
            "gtf_device_init", "gtf_malloc", "gtf_free", "gtf_memcpy_htod", "gtf_memcpy_dtoh", "gtf_memcpy_dtod",
            "gtf_memset", "gtf_stream_synchronize",
+           "gtf_comm_unique_id", "gtf_comm_init", "gtf_comm_destroy", "gtf_comm_rank", "gtf_comm_size",
+           "gtf_halo_exchange", "gtf_allreduce_max_i64", "gtf_allgather_bytes", "gtf_tag_shard_workspace_bytes",
+           "gtf_tag_propagate_shard",
            "gtf_last_error",
            "gtf_version"]
 
@@ -186,11 +190,13 @@ def lib(lean: bool = False):
     L.gtf_workspace_bytes.restype = ctypes.c_size_t
     L.gtf_workspace_bytes.argtypes = [I32, I32]
     L.gtf_clear_errors.argtypes = [P, P]
+    L.gtf_workspace_init.argtypes = [P, P]
     L.gtf_read_errors.argtypes = [P, ctypes.POINTER(ctypes.c_uint32), P]
     L.gtf_set_diagnostics.argtypes = [P, ctypes.POINTER(GtfDiag), P]
     G, N, S, E, PR = (ctypes.POINTER(GtfGraph), ctypes.POINTER(GtfNodes), ctypes.POINTER(GtfStates),
                       ctypes.POINTER(GtfEdges), ctypes.POINTER(GtfParams))
     L.gtf_extrapolate.argtypes = [G, N, S, E, PR, P, P]
+    L.gtf_uts_materialize.argtypes = [G, S, P]
     L.gtf_update.argtypes = [G, N, S, S, E, PR, P, P]
     L.gtf_message_passing.argtypes = [G, N, S, E, PR, P, P]
     L.gtf_node_ops.argtypes = [G, N, S, S, E, PR, ctypes.POINTER(ctypes.c_int8), I32, F64, F64, P, P]
@@ -231,15 +237,30 @@ def lib(lean: bool = False):
         getattr(L, fn).argtypes = [P, P, ctypes.c_size_t, P]
     L.gtf_memset.argtypes = [P, I32, ctypes.c_size_t, P]
     L.gtf_stream_synchronize.argtypes = [P]
+    I64 = ctypes.c_int64
+    L.gtf_comm_unique_id.argtypes = [P]
+    L.gtf_comm_init.argtypes = [ctypes.POINTER(P), I32, I32, P]
+    L.gtf_comm_destroy.argtypes = [P]
+    L.gtf_comm_rank.argtypes = [P]
+    L.gtf_comm_size.argtypes = [P]
+    L.gtf_halo_exchange.argtypes = [P, N, E, HA, HA, P, P, P, P, P]
+    L.gtf_allreduce_max_i64.argtypes = [P, P, I64, P]
+    L.gtf_allgather_bytes.argtypes = [P, P, P, I64, P]
+    L.gtf_tag_shard_workspace_bytes.restype = ctypes.c_size_t
+    L.gtf_tag_shard_workspace_bytes.argtypes = [I32, I32, I32]
+    L.gtf_tag_propagate_shard.argtypes = [P, G, SH, P, P, F64, I32, P, ctypes.POINTER(ctypes.c_int32), P,
+                                          ctypes.c_size_t, P]
     L.gtf_last_error.restype = ctypes.c_char_p
     L.gtf_version.restype = ctypes.c_char_p
-    for fn in ("gtf_clear_errors", "gtf_read_errors", "gtf_extrapolate", "gtf_update", "gtf_cluster", "gtf_pass",
+    for fn in ("gtf_workspace_init", "gtf_uts_materialize", "gtf_clear_errors", "gtf_read_errors", "gtf_extrapolate", "gtf_update", "gtf_cluster", "gtf_pass",
                "gtf_pass_ev", "gtf_message_passing", "gtf_node_ops",
                "gtf_tag_prepare", "gtf_tag_sweep", "gtf_tag_sweep_shard", "gtf_parabolic_kl", "gtf_track_state_estimates", "gtf_pass_shard", "gtf_shard_pack",
                "gtf_shard_unpack", "gtf_halo_pack", "gtf_halo_unpack", "gtf_extract_candidates", "gtf_build_event_csr",
                "gtf_candidate_order", "gtf_updated_state_pair_counts", "gtf_updated_state_distances",
                "gtf_set_diagnostics", "gtf_build_event_csr_device", "gtf_device_init", "gtf_malloc", "gtf_free",
-               "gtf_memcpy_htod", "gtf_memcpy_dtoh", "gtf_memcpy_dtod", "gtf_memset", "gtf_stream_synchronize"):
+               "gtf_memcpy_htod", "gtf_memcpy_dtoh", "gtf_memcpy_dtod", "gtf_memset", "gtf_stream_synchronize",
+               "gtf_comm_unique_id", "gtf_comm_init", "gtf_comm_destroy", "gtf_comm_rank", "gtf_comm_size",
+               "gtf_halo_exchange", "gtf_allreduce_max_i64", "gtf_allgather_bytes", "gtf_tag_propagate_shard"):
         getattr(L, fn).restype = ctypes.c_int
     _lib = L
     return L

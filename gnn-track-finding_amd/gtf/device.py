@@ -91,6 +91,63 @@ def pack_schedule(slot_ptr):
     return ent, wave
 
 
+CLASS_MAX = 32   # segments of up to this many slots get graph-static classes (gtf_graph.slot_class)
+
+
+def slot_classes(g: TrackGraph):
+    """gtf_graph.slot_class / slot_sflags (ABI v5): for every slot of a receiver segment of
+    d <= 32 slots, bits 0..31 = the segment positions whose sender has this slot's sender
+    layer (compute_prior_probabilities' groups, helper.py:30-63), bits 32..63 = the positions
+    whose sender's GNN x equals this slot's sender's (the side norm's distinct-x classes,
+    helper.py:111-139, for entries holding their sender's live coordinates); a NaN (orphan
+    key) equals only itself. sflags bit 0 = sender GNN x < receiver GNN x (the side,
+    helper.py:116-121). Larger segments get 0 (the kernel builds their classes)."""
+    S = g.n_slots
+    cls = np.zeros(S, np.uint64)
+    src = g.slot["slot_src"].astype(np.int64)
+    ok = src >= 0
+    layer = np.full(S, np.nan)
+    sx = np.full(S, np.nan)
+    if g.n_nodes:
+        layer[ok] = g.node["layer"][src[ok]]
+        sx[ok] = g.node["gnn"][src[ok], 0]
+    rx = g.node["gnn"][g.slot_dst(), 0] if S else np.zeros(0)
+    with np.errstate(invalid="ignore"):
+        sfl = (sx < rx).astype(np.uint8)
+    sp = g.slot_ptr.astype(np.int64)
+    deg = np.diff(sp)
+    for d in range(1, CLASS_MAX + 1):
+        v = np.nonzero(deg == d)[0]
+        if v.size == 0:
+            continue
+        idx = sp[v][:, None] + np.arange(d)[None, :]                 # [n, d] slots
+        own = np.eye(d, dtype=bool)[None, :, :]
+        bits = (np.uint64(1) << np.arange(d, dtype=np.uint64))[None, None, :]
+        word = np.zeros((v.size, d), np.uint64)
+        for shift, val in ((0, layer), (32, sx)):
+            a = val[idx]
+            eq = (a[:, :, None] == a[:, None, :]) | own              # [n, i, j]
+            m = np.bitwise_or.reduce(np.where(eq, bits, np.uint64(0)), axis=2)
+            word |= m << np.uint64(shift)
+        cls[idx.reshape(-1)] = word.reshape(-1)
+    return cls, sfl
+
+
+def live_coordinates(g: TrackGraph) -> np.ndarray:
+    """gtf_states.fresh bit 1 for an uploaded graph: the updated_track_states entries whose
+    stored 'xyzr' is bit for bit their sender's current GNN_Measurement coordinates (what
+    extrapolate_merged_states.py:377 stores; a close-proximity merge of the sender since,
+    extract_track_candidates.py:111-118, breaks it). Those entries' xyzr is read from gnn."""
+    src = g.slot["slot_src"].astype(np.int64)
+    ok = (src >= 0) & (g.slot["uts_rank"] >= 0)
+    live = np.zeros(g.n_slots, bool)
+    if ok.any():
+        a = np.ascontiguousarray(g.slot["uts_xyzr"][ok]).view(np.int64)
+        b = np.ascontiguousarray(g.node["gnn"][src[ok]]).view(np.int64)
+        live[ok] = (a == b).all(axis=1)
+    return live
+
+
 def _torch():
     import torch
     if not torch.cuda.is_available():
@@ -174,10 +231,15 @@ class DeviceGraph:
         # stores its running values in out-edge order (GTF_NO_OUTIDX=1: by slot, for A/B)
         import os
         self.use_outidx = os.environ.get("GTF_NO_OUTIDX", "0") != "1"
+        # graph-static slot classes for the node kernel (GTF_NO_CLASSES=1: built in the kernel, A/B)
+        self.use_classes = os.environ.get("GTF_NO_CLASSES", "0") != "1"
         oidx = np.full(g.n_slots, -1, np.int32)
         if g.n_edges:
             oidx[g.out_slot] = np.arange(g.n_edges, dtype=np.int32)
         up("slot_outidx", oidx)
+        cls, sfl = slot_classes(g)
+        up("slot_class", cls.view(np.int64))
+        up("slot_sflags", sfl)
         sub = g.node["sub_id"].astype(np.int64)
         if g.n_nodes:
             sizes = np.bincount(sub - sub.min())
@@ -213,6 +275,9 @@ class DeviceGraph:
             up(f, g.node[f])
         for f in SLOT_FIELDS:
             if f in ("slot_key",):
+                continue
+            if f == "uts_fresh":   # bit 0: fresh; bit 1: the entry's xyzr is its sender's live gnn
+                up(f, ((g.slot[f] != 0).astype(np.uint8) | (live_coordinates(g).astype(np.uint8) << 1)))
                 continue
             up(f, g.slot[f])
         self._staged, self._resident = [], None   # stage_inputs() copies
@@ -278,7 +343,9 @@ class DeviceGraph:
                     out_slot=p("out_slot"), slot_outpos=p("slot_outpos"), is_edge=p("is_edge"),
                     rev_edge=p("rev_edge"), solo=p("solo"), gnn=p("gnn"), xyzr=p("xyzr"), layer=p("layer"),
                     out_dst=p("out_dst"), slot_layer=p("slot_layer"),
-                    slot_outidx=p("slot_outidx") if self.use_outidx else ctypes.c_void_p(0))
+                    slot_outidx=p("slot_outidx") if self.use_outidx else ctypes.c_void_p(0),
+                    slot_class=p("slot_class") if self.use_classes else ctypes.c_void_p(0),
+                    slot_sflags=p("slot_sflags") if self.use_classes else ctypes.c_void_p(0))
         # with the node schedule (lane groups) and the sender schedule
         sched = dict(n_big=self.n_big, sched=p("sched"), n_g4=self.n_g_all[0], n_g8=self.n_g_all[1],
                      n_g16=self.n_g_all[2], n_g32=self.n_g_all[3], n_g64=self.n_g_all[4], sched_seg=p("sched_seg"),
@@ -483,34 +550,36 @@ class DeviceGraph:
 
     # ------------------------------------------------------- tag propagation
     def tag_propagation(self, tags, radius, threshold=0.1, max_sweeps=100000):
-        """Jacobi sweeps until flips / processed <= threshold (tag_propagation.py:137)."""
+        """Jacobi sweeps until flips / processed <= threshold (tag_propagation.py:97-164), the
+        whole stage in one gtf_tag_propagate call (stop rule on the device, one host read per
+        batch of sweeps). tags / radius in host node order; returns (tags, flips per sweep)."""
         self._natural_only("tag_propagation")
-        E = self.n_edges
-        keep = self._dev_zeros(max(E, 1), np.uint8)
-        proc = self._dev_zeros(max(self.n_nodes, 1), np.uint8)
-        cnt = self._dev_zeros(2, np.int32)
         r = self._dev_from(np.ascontiguousarray(self._to_dev_nodes(radius), dtype=np.float64))
         ta = self._dev_from(np.ascontiguousarray(self._to_dev_nodes(tags), dtype=np.int64))
-        tb = self._dev_zeros(max(self.n_nodes, 1), np.int64)
-        vp = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
-        nat.check(self.lib.gtf_tag_prepare(ctypes.byref(self.cg), vp(r), vp(keep), vp(proc), vp(cnt), self.stream))
-        total = int(self._np(cnt)[0])
-        flips_hist = []
-        frac = 1.0
-        flips = cnt[1:2] if self.torch is not None else cnt.view(4, 1, np.int32)
-        while frac > threshold and len(flips_hist) < max_sweeps:
-            nat.check(self.lib.gtf_tag_sweep(ctypes.byref(self.cg), vp(keep), vp(proc), vp(ta), vp(tb), vp(flips),
-                                             self.stream))
-            f = int(self._np(flips)[0])
-            flips_hist.append(f)
-            frac = f / total if total else 0.0
-            ta, tb = tb, ta
+        flips = self.tag_propagation_dev(ta, r, threshold, max_sweeps)
         out = self._np(ta)[:self.n_nodes]
         if self.order is not None:
             h = np.empty_like(out)
             h[self.order] = out
             out = h
-        return out, flips_hist
+        return out, flips
+
+    def tag_propagation_dev(self, tags, radius, threshold=0.1, max_sweeps=100000):
+        """gtf_tag_propagate on device arrays in this graph's node order: `tags` (int64 [N]) is
+        replaced by the final tags; returns the flip count of every sweep"""
+        nb = int(self.lib.gtf_tag_workspace_bytes(self.n_nodes, self.n_edges))
+        ws = getattr(self, "_tag_ws", None)
+        if ws is None or ws.numel() < nb:
+            ws = self._tag_ws = self._dev_zeros(nb, np.uint8)
+        hf = getattr(self, "_tag_flips", None)
+        if hf is None or hf.size < max(max_sweeps, 1):
+            hf = self._tag_flips = np.zeros(max(max_sweeps, 1), np.int32)
+        n = ctypes.c_int32(0)
+        vp = lambda t: ctypes.c_void_p(t.data_ptr() if t.numel() else 0)  # noqa: E731
+        nat.check(self.lib.gtf_tag_propagate(ctypes.byref(self.cg), vp(radius), vp(tags), float(threshold),
+                                             int(max_sweeps), ctypes.c_void_p(hf.ctypes.data), ctypes.byref(n),
+                                             vp(ws), ctypes.c_size_t(nb), self.stream))
+        return [int(x) for x in hf[:n.value]]
 
     def _dev_zeros(self, n, dtype):
         """a zeroed device array of this graph's allocator"""
@@ -580,8 +649,14 @@ class DeviceGraph:
         return h
 
     # ---------------------------------------------------------------- results
+    def materialize(self):
+        """write the live updated_track_states coordinates (gtf_states.fresh bit 1) into
+        uts_xyzr on the device (gtf_uts_materialize): before reading them back"""
+        nat.check(self.lib.gtf_uts_materialize(ctypes.byref(self.cg_sched), ctypes.byref(self.cuts), self.stream))
+
     def download(self, g: TrackGraph) -> TrackGraph:
         """copy the mutable arrays back into the host TrackGraph (in place, host order)"""
+        self.materialize()
         nm = None if self.order is None else self.order >= 0          # (padded: not a dummy node)
         sm = None if self.slot_perm is None else self.slot_perm >= 0  # (padded: not a padding slot)
         for f in MUTABLE_NODE:
@@ -594,6 +669,8 @@ class DeviceGraph:
             if f in STATIC_SLOT or f == "slot_key":
                 continue
             a = self._np(self.t[f]).reshape((-1,) + g.slot[f].shape[1:])
+            if f == "uts_fresh":
+                a = a & 1   # (bit 1 is cleared by materialize())
             if self.slot_perm is None:
                 g.slot[f][...] = a
             else:

@@ -62,10 +62,15 @@ def device_memory() -> str:
     return default_mem()
 
 
+_DEVICE_TOUCHED = False   # this process has (begun to) initialise the GPU
+
+
 def _warm_device():
     """load libgtf lean and create the device context (one small allocation)"""
     import ctypes
     from . import _native as nat
+    global _DEVICE_TOUCHED
+    _DEVICE_TOUCHED = True
     try:
         L = nat.lib(lean=True)
         if L.gtf_device_init(0) == 0:
@@ -178,6 +183,12 @@ def _get_pool(n, warm_file):
         _drop_pool()
     if _POOL is None:
         import atexit
+        if _DEVICE_TOUCHED:
+            # a fork of a process that holds a GPU context works, but the children share its
+            # pages copy-on-write and its later host-to-device copies slow down (_Pool)
+            import warnings
+            warnings.warn("gtf.dropin: re-forking the worker pool after this process initialised the GPU",
+                          RuntimeWarning, stacklevel=3)
         _POOL = _Pool(n, warm_file)
         atexit.register(_drop_pool)
     return _POOL
@@ -232,6 +243,8 @@ def run_dir(input_dir: str, output_dir: str, body: Callable, *, states=("tse", "
             out_node, out_slot = g.node, g.slot
         elif nonempty:
             from .device import DeviceGraph
+            global _DEVICE_TOUCHED
+            _DEVICE_TOUCHED = True
             if warm is not None:
                 warm.join()
             tp = [time.perf_counter()]
@@ -273,6 +286,8 @@ def run_dir(input_dir: str, output_dir: str, body: Callable, *, states=("tse", "
             wt.append(m[2])
         t3 = time.perf_counter()
     except BaseException:
+        if warm is not None:
+            warm.join()  # never fork (a later pool) while that thread may hold runtime or malloc locks
         _drop_pool()     # workers may be mid-job: start clean next time
         raise
     # the slowest worker's phases (seconds) and the latest worker start after t0

@@ -255,7 +255,11 @@ class ShardedDeviceGraph:
     pass for its receivers and exchanges the halo with the other ranks after each pass."""
 
     def __init__(self, g: TrackGraph, rank: int, world: int, device="cuda", backend="nccl", group=None,
-                 tile: int = None, widen: int = None):
+                 tile: int = None, widen: int = None, comm=None):
+        """backend: "nccl" (torch.distributed over RCCL), "gloo" (torch.distributed staged through
+        host memory), "native" (libgtf's own RCCL communicator, gtf.comm.NativeComm: `comm`,
+        else one made from `group` when torch.distributed runs, else a world of one), or
+        "local" (no collective: SplitDeviceGraph)."""
         import torch
         from .device import DeviceGraph, TILE, sched_segments, sender_lanes
         self.torch = torch
@@ -291,7 +295,9 @@ class ShardedDeviceGraph:
                                slot_layer=p("slot_layer"), sched_seg=vp(self.sched_seg),
                                out_sched=vp(self.out_sched), n_o4=n_o[0], n_o8=n_o[1], n_o16=n_o[2], n_g2=n_g2,
                                out_lanes=vp(self.out_lanes),
-                               slot_outidx=p("slot_outidx") if d.use_outidx else ctypes.c_void_p(0))
+                               slot_outidx=p("slot_outidx") if d.use_outidx else ctypes.c_void_p(0),
+                               slot_class=p("slot_class") if d.use_classes else ctypes.c_void_p(0),
+                               slot_sflags=p("slot_sflags") if d.use_classes else ctypes.c_void_p(0))
         self.shard = nat.GtfShard(vp(self.senders), int(self.senders.numel()), int(pl.node_lo[rank]),
                                   int(pl.node_hi[rank]), int(pl.slot_lo[rank]), int(pl.slot_hi[rank]))
         # halo exchange buffers and lists (fixed per plan)
@@ -303,6 +309,21 @@ class ShardedDeviceGraph:
         self.chunk_bytes = int(d.lib.gtf_shard_chunk_bytes(pl.cap_nodes, pl.cap_slots))
         self.chunk = torch.zeros(self.chunk_bytes, dtype=torch.uint8, device=dev)
         self.gathered = torch.zeros(self.chunk_bytes * world, dtype=torch.uint8, device=dev)
+        self.comm = None
+        if backend == "native":
+            from .comm import NativeComm
+            if comm is None:
+                import torch.distributed as dist
+                if dist.is_available() and dist.is_initialized():
+                    comm = NativeComm.from_torch(group, lib=d.lib)
+                elif world == 1:
+                    comm = NativeComm.single(lib=d.lib)
+                else:
+                    raise ValueError("backend 'native' with world > 1 needs a NativeComm (gtf.comm) or torch.distributed")
+            if comm.world != world or comm.rank != rank:
+                raise ValueError("NativeComm is rank %d of %d, the shard rank %d of %d" % (comm.rank, comm.world, rank, world))
+            self.comm = comm
+            self._sizes_c = ((ctypes.c_int64 * world)(*self.send_sizes), (ctypes.c_int64 * world)(*self.recv_sizes))
 
     def _halo(self, send):
         torch = self.torch
@@ -353,6 +374,14 @@ class ShardedDeviceGraph:
 
     def exchange(self):
         """the halo: what the other ranks' next pass reads, one all-to-all"""
+        if self.comm is not None:   # pack, all-to-all and unpack inside libgtf (gtf_halo_exchange)
+            d = self.d
+            _, st, sbuf, rbuf = self._io()[:4]
+            nat.check(d.lib.gtf_halo_exchange(self.comm.ptr, ctypes.byref(d.cn), ctypes.byref(d.ce),
+                                              ctypes.byref(self.halo_send), ctypes.byref(self.halo_recv), sbuf, rbuf,
+                                              ctypes.cast(self._sizes_c[0], ctypes.c_void_p),
+                                              ctypes.cast(self._sizes_c[1], ctypes.c_void_p), st))
+            return
         if self.world == 1:
             return
         _, st, sbuf, rbuf, sview, rview = self._io()
@@ -381,8 +410,11 @@ class ShardedDeviceGraph:
         pl = self.plan
         nat.check(d.lib.gtf_shard_pack(ctypes.byref(d.cn), ctypes.byref(d.ce), ctypes.byref(self.shard),
                                        pl.cap_nodes, pl.cap_slots, ctypes.c_void_p(self.chunk.data_ptr()), d.stream))
+        if self.comm is not None:
+            self.comm.allgather_bytes(self.chunk, self.gathered, d.stream)
         if self.world > 1:
-            allgather_bytes(self.chunk, self.gathered, self.backend, self.group)
+            if self.comm is None:
+                allgather_bytes(self.chunk, self.gathered, self.backend, self.group)
             nat.check(d.lib.gtf_shard_unpack(ctypes.byref(d.cn), ctypes.byref(d.ce),
                                              ctypes.c_void_p(self.gathered.data_ptr()), self.world, self.rank,
                                              ctypes.c_void_p(self.ranges.data_ptr()), pl.cap_nodes, pl.cap_slots,
@@ -406,6 +438,21 @@ class ShardedDeviceGraph:
         N, W = d.n_nodes, self.world
         dev = d.device
         vp = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+        if self.comm is not None:   # the whole stage inside libgtf (gtf_tag_propagate_shard)
+            r = torch.from_numpy(np.ascontiguousarray(d._to_dev_nodes(radius), dtype=np.float64)).to(dev)
+            ta = torch.from_numpy(np.ascontiguousarray(d._to_dev_nodes(tags), dtype=np.int64)).to(dev)
+            nb = int(d.lib.gtf_tag_shard_workspace_bytes(N, d.n_edges, W))
+            ws = torch.zeros(nb, dtype=torch.uint8, device=dev)
+            hf = np.zeros(max(int(max_sweeps), 1), np.int32)
+            n = ctypes.c_int32(0)
+            nat.check(d.lib.gtf_tag_propagate_shard(self.comm.ptr, ctypes.byref(self.cg), ctypes.byref(self.shard),
+                                                    vp(r), vp(ta), float(threshold), int(max_sweeps),
+                                                    ctypes.c_void_p(hf.ctypes.data), ctypes.byref(n), vp(ws),
+                                                    ctypes.c_size_t(nb), d.stream))
+            out = ta.cpu().numpy()
+            h = np.empty_like(out)
+            h[d.order] = out
+            return h, [int(x) for x in hf[:n.value]]
         keep = torch.zeros(max(d.n_edges, 1), dtype=torch.uint8, device=dev)
         proc = torch.zeros(max(N, 1), dtype=torch.uint8, device=dev)
         cnt = torch.zeros(2, dtype=torch.int32, device=dev)

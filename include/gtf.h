@@ -24,6 +24,10 @@
  *   gtf_tag_prepare  -> tag_propagation/tag_propagation.py:97-110
  *   gtf_tag_propagate -> tag_propagation/tag_propagation.py:97-164 (the whole stage)
  *   gtf_tag_sweep_shard -> one sweep (:137-164) on an edge-sharded event
+ *   gtf_comm_*, gtf_halo_exchange, gtf_allreduce_max_i64, gtf_allgather_bytes,
+ *   gtf_tag_propagate_shard -> no reference counterpart: the collectives of one event
+ *                       sharded over the GPUs of a node, in place of the
+ *                       serial subgraph loop src/extrapolate/extrapolate_merged_states.py:406-451
  *   gtf_updated_state_distances -> calculate_distance_between_updated_states/
  *                       calculate_distance_between_updated_track_states.py:27-104,134-195
  */
@@ -42,7 +46,7 @@ typedef void* gtf_stream_t; /* a hipStream_t */
 /* Version of the struct layouts below. gtf_graph carries it with its own size, and every
  * entry point taking a gtf_graph refuses a caller built against another layout
  * (status -3, gtf_last_error() names both). Bumped on every layout change. */
-#define GTF_ABI_VERSION 4u
+#define GTF_ABI_VERSION 5u
 
 /* ---- graph structure (read-only on the path) ------------------------------ */
 typedef struct gtf_graph {
@@ -126,6 +130,19 @@ typedef struct gtf_graph {
      * each extrapolation sees in out-edge order (contiguous per sender, coalesced stores)
      * and the extrapolation reads it through this index; NULL: stored by slot. [S] */
     const int32_t* slot_outidx;
+    /* optional (v5): graph-static partitions of every receiver's slot segment, built once per
+     * graph (gtf/device.py) so the node kernel does not rebuild them in every pass. For slot
+     * k at position i of a segment of d <= 32 slots: bits 0..31 = the positions j of the
+     * segment whose sender has slot k's sender layer (layer[slot_src], compute_prior_
+     * probabilities' groups, helper.py:30-63; an orphan or NaN layer: {i}); bits 32..63 = the
+     * positions whose sender's GNN_Measurement x equals slot k's sender's (the side norm's
+     * distinct-x classes, helper.py:111-139, for entries whose stored x is the sender's live
+     * GNN x -- see gtf_states.fresh); 0 for segments of more than 32 slots. [S], or NULL
+     * (the kernel then builds the classes itself). */
+    const uint64_t* slot_class;
+    /* optional (v5, with slot_class): bit 0 = the sender's GNN x < the receiver's GNN x (the
+     * side of a live entry, helper.py:116-121). [S], or NULL. */
+    const uint8_t* slot_sflags;
 } gtf_graph;
 
 /* ---- per-node mutable state ------------------------------------------------ */
@@ -151,7 +168,11 @@ typedef struct gtf_states {
     double*  prior;           /* [S]   prior */
     double*  lr;              /* [S]   lr_layer_norm (UTS only) */
     int8_t*  side;            /* [S]   0 left, 1 right (UTS only) */
-    uint8_t* fresh;           /* [S]   entry written by the last message passing (UTS only) */
+    uint8_t* fresh;           /* [S]   UTS only: bit 0 = entry written by the last message passing;
+                                 bit 1 = the entry's xyzr is its sender's live GNN coordinates
+                                 gnn[slot_src] (extrapolate_merged_states.py:377 stores exactly
+                                 those), so xyzr[k] itself is not written -- gtf_uts_materialize
+                                 writes it (before a caller mutates g->gnn or reads uts->xyzr) */
 } gtf_states;
 
 /* ---- per-edge attributes (stored per slot) --------------------------------- */
@@ -187,12 +208,17 @@ enum {
     GTF_ERR_TOO_MANY_STATES = 1024 /* a15: a node with more than 2048 updated states (not processed) */
 };
 
-/* Workspace: caller allocates gtf_workspace_bytes() bytes of device memory, zeroed once
- * (its first 256 bytes are a header: the error word at offset 0, gtf_diag at
- * GTF_DIAG_OFFSET). */
+/* Workspace: caller allocates gtf_workspace_bytes() bytes of device memory and initialises
+ * it once with gtf_workspace_init (or allocates it zeroed). Its first 256 bytes are a
+ * header: the error word at offset 0, the gtf_diag record at GTF_DIAG_OFFSET. */
 size_t gtf_workspace_bytes(int32_t n_nodes, int32_t n_slots);
 
-/* Zero the error word (stream-ordered; the registered diagnostics stay). */
+/* Zero the whole header (stream-ordered): no error flags, no diagnostics registered.
+ * Required once on a workspace that was not allocated zeroed (hipMalloc): the kernels write
+ * through every non-NULL gtf_diag pointer they find there. */
+int gtf_workspace_init(void* workspace, gtf_stream_t stream);
+
+/* Zero the error word only (stream-ordered); the registered diagnostics stay. */
 int gtf_clear_errors(void* workspace, gtf_stream_t stream);
 
 /* ---- Optional diagnostics outputs (SURVEY §5 "Metrics / logging"), off by default ----
@@ -261,6 +287,12 @@ int gtf_update(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* ut
 int gtf_cluster(const gtf_graph* g, gtf_nodes* n, gtf_states* states, gtf_edges* e, int32_t key,
                 double chi2_threshold, double kl_threshold, const gtf_params* p, void* workspace,
                 gtf_stream_t stream);
+/* Write gnn[slot_src] into uts->xyzr of every entry whose xyzr is live (uts->fresh bit 1) and
+ * clear that bit: the stored snapshot extrapolate_merged_states.py:377 makes. Call it before
+ * mutating g->gnn (extraction's close-proximity merge, extract_track_candidates.py:111-118)
+ * and before reading uts->xyzr back. */
+int gtf_uts_materialize(const gtf_graph* g, gtf_states* uts, gtf_stream_t stream);
+
 /* extrapolate -> update -> cluster(updated_track_states, p->cluster_chi2, p->cluster_kl) */
 int gtf_pass(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts, gtf_edges* e,
              const gtf_params* p, void* workspace, gtf_stream_t stream);
@@ -360,6 +392,42 @@ int gtf_tag_propagate(const gtf_graph* g, const double* radius, int64_t* tags, d
 int gtf_tag_sweep_shard(const gtf_graph* g, const uint8_t* keep, const uint8_t* processed,
                         const int64_t* tags_in, int64_t* tags_out, const gtf_shard* shard,
                         int32_t rank, int32_t nranks, gtf_stream_t stream);
+
+/* ---- Native collectives for the sharded event (SURVEY §8b gtf_comm_init, §8e) ----------
+ * RCCL over xGMI inside libgtf, one communicator per rank (one process per GPU; create it
+ * with the rank's device current), every call stream-ordered on the caller's stream. RCCL is
+ * loaded on first use (GTF_RCCL = its path, else an RCCL already loaded in the process, else
+ * librccl.so.1). Rank 0 calls gtf_comm_unique_id and hands the GTF_COMM_ID_BYTES to the other
+ * ranks (file, socket, MPI, ...); each rank then calls gtf_comm_init. Status -4: an RCCL
+ * error (gtf_last_error names it). These replace the role of the reference's serial subgraph
+ * loop (src/extrapolate/extrapolate_merged_states.py:406-451) for one event spread over the
+ * GPUs of a node. */
+#define GTF_COMM_ID_BYTES 128
+typedef struct gtf_comm gtf_comm;
+int gtf_comm_unique_id(void* id);
+int gtf_comm_init(gtf_comm** comm, int32_t rank, int32_t nranks, const void* rccl_uid);
+int gtf_comm_destroy(gtf_comm* comm);
+int gtf_comm_rank(const gtf_comm* comm);
+int gtf_comm_size(const gtf_comm* comm);
+/* The per-pass halo exchange: gtf_halo_pack into send_buf, one all-to-all of the
+ * per-destination segments (send_bytes[p] / recv_bytes[p]: host int64 [nranks], segments back
+ * to back in rank order, a rank's own segment empty), gtf_halo_unpack from recv_buf. */
+int gtf_halo_exchange(gtf_comm* comm, gtf_nodes* n, gtf_edges* e, const gtf_halo* send, const gtf_halo* recv,
+                      void* send_buf, void* recv_buf, const int64_t* send_bytes, const int64_t* recv_bytes,
+                      gtf_stream_t stream);
+/* in-place all-reduce(MAX) of int64 words (the sharded tag sweep's exchange) */
+int gtf_allreduce_max_i64(gtf_comm* comm, int64_t* words, int64_t count, gtf_stream_t stream);
+/* all-gather of one equal-size chunk per rank into gathered (nranks chunks, rank order):
+ * gtf_shard_pack -> this -> gtf_shard_unpack completes every replica */
+int gtf_allgather_bytes(gtf_comm* comm, const void* chunk, void* gathered, int64_t bytes, gtf_stream_t stream);
+/* The whole tag-propagation stage on an edge-sharded event (tag_propagation.py:97-164): prepare
+ * on the replica, per sweep gtf_tag_sweep_shard over the owned nodes + one all-reduce(MAX),
+ * stop when flips / processed <= flip_threshold (one synchronisation per sweep). tags: device
+ * int64 [n_nodes] in / out (every rank ends with the whole array). */
+size_t gtf_tag_shard_workspace_bytes(int32_t n_nodes, int32_t n_edges, int32_t nranks);
+int gtf_tag_propagate_shard(gtf_comm* comm, const gtf_graph* g, const gtf_shard* shard, const double* radius,
+                            int64_t* tags, double flip_threshold, int32_t max_sweeps, int32_t* flips_out,
+                            int32_t* sweeps_out, void* workspace, size_t workspace_bytes, gtf_stream_t stream);
 
 /* ---- Distances between updated track states --------------------
  * calculate_distance_between_updated_states/calculate_distance_between_updated_track_states.py:
@@ -493,7 +561,7 @@ typedef struct gtf_kl_graph {
      * slot, its first pair low / high 32 bits, window [lo, hi) of at most 768 nodes holding the
      * tile's neighbours, 0); the block copies the window's x, y and truth ids into LDS and reads
      * the neighbours there. blk != NULL overrides list / first / count. */
-    const int32_t* blk;       /* [8 * n_blk] or NULL */
+    const int32_t* blk;       /* [12 * n_blk] or NULL */
     int32_t n_blk;
     int32_t pad_blk_;
 } gtf_kl_graph;

@@ -111,3 +111,90 @@ def test_tag_propagate_one_call():
     assert L.gtf_tag_propagate(ctypes.byref(d.cg), ctypes.c_void_p(radius.data_ptr()),
                                ctypes.c_void_p(tags.data_ptr()), 0.1, 64, ctypes.cast(flips, ctypes.c_void_p), ctypes.byref(sweeps),
                                ctypes.c_void_p(ws.data_ptr()), nb - 1, d.stream) != 0
+
+
+@pytest.mark.parametrize("schedule", [True, False])
+@pytest.mark.parametrize("max_sweeps", [64, 3, 0])
+def test_tag_propagate_stop_rule_and_cap(schedule, max_sweeps):
+    """the stop rule evaluated on the device (gtf_tag_propagate's batched sweeps): the
+    reference's flip vector, cut at max_sweeps, on the sender-schedule and the thread-per-node
+    kernels; the tags equal the host loop of single sweeps run that many times"""
+    import ctypes
+    import torch
+    from gtf import _native as nat
+    from gtf.device import DeviceGraph
+    g, _, extra, _ = load("tags_vol7")
+    d = DeviceGraph(g, schedule=schedule)
+    L = d.lib
+    t0 = np.ascontiguousarray(g.node["tag"], dtype=np.int64)
+    tags = torch.from_numpy(t0).to(d.device)
+    radius = torch.from_numpy(np.ascontiguousarray(g.node["xyzr"][:, 3], dtype=np.float64)).to(d.device)
+    nb = L.gtf_tag_workspace_bytes(g.n_nodes, g.n_edges)
+    ws = torch.full((nb,), 0xFF, dtype=torch.uint8, device=d.device)   # no zeroing needed
+    flips = (ctypes.c_int32 * 64)()
+    sweeps = ctypes.c_int32(-1)
+    nat.check(L.gtf_tag_propagate(ctypes.byref(d.cg), ctypes.c_void_p(radius.data_ptr()),
+                                  ctypes.c_void_p(tags.data_ptr()), 0.1, max_sweeps,
+                                  ctypes.cast(flips, ctypes.c_void_p), ctypes.byref(sweeps),
+                                  ctypes.c_void_p(ws.data_ptr()), nb, d.stream))
+    torch.cuda.synchronize()
+    want = list(extra["flips"])[:max_sweeps]
+    assert sweeps.value == len(want) and list(flips[:sweeps.value]) == want
+    # the same number of single sweeps (gtf_tag_sweep), host loop
+    keep = torch.zeros(max(g.n_edges, 1), dtype=torch.uint8, device=d.device)
+    proc = torch.zeros(max(g.n_nodes, 1), dtype=torch.uint8, device=d.device)
+    cnt = torch.zeros(2, dtype=torch.int32, device=d.device)
+    vp = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    ta, tb = torch.from_numpy(t0).to(d.device), torch.empty(g.n_nodes, dtype=torch.int64, device=d.device)
+    nat.check(L.gtf_tag_prepare(ctypes.byref(d.cg), vp(radius), vp(keep), vp(proc), vp(cnt), d.stream))
+    for _ in range(len(want)):
+        nat.check(L.gtf_tag_sweep(ctypes.byref(d.cg), vp(keep), vp(proc), vp(ta), vp(tb), vp(cnt[1:2]), d.stream))
+        ta, tb = tb, ta
+    torch.cuda.synchronize()
+    assert torch.equal(tags, ta)
+
+
+def test_workspace_init_contract():
+    """a workspace that was not allocated zeroed (filled with 0xFF here: every gtf_diag
+    pointer garbage) is usable after gtf_workspace_init, as include/gtf.h documents"""
+    import ctypes
+    import torch
+    from gtf import _native as nat
+    g, out, extra, meta = load("pass_full")
+    exp = expected_graph(g, out)
+    p = _params(meta)
+    d = _dev(g)
+    d.t["ws"].fill_(0xFF)
+    nat.check(d.lib.gtf_workspace_init(d.ptr("ws"), d.stream))
+    d.full_pass(p)
+    d.raise_errors()
+    got = d.download(g.copy())
+    errs = compare(got, exp, rtol=RTOL, atol=1e-12)
+    assert errs == [], "\n".join(errs)
+    ws = d.t["ws"][:256].cpu().numpy()
+    assert not ws[nat.DIAG_OFFSET:nat.DIAG_OFFSET + ctypes.sizeof(nat.GtfDiag)].any()
+
+
+def test_live_coordinates_equal_stored():
+    """the updated states' 'xyzr' kept live in gnn (gtf_states.fresh bit 1: k_extrapolate
+    does not write the snapshot) against the same passes with the snapshot materialised
+    between them (download -> gtf_uts_materialize, the stored path of every reader): two
+    fused passes, bit for bit, and the downloaded xyzr equal to the senders' coordinates"""
+    g, out, extra, meta = load("pass_full")
+    p = _params(meta)
+    a, b = _dev(g), _dev(g)
+    for d in (a, b):
+        d.clear_errors()
+    a.full_pass(p)
+    a.full_pass(p)                        # pass 2 reads pass 1's entries live
+    b.full_pass(p)
+    b.download(g.copy())                  # materialises: pass 2 reads them stored
+    b.full_pass(p)
+    ga, gb = a.download(g.copy()), b.download(g.copy())
+    assert a.errors() == 0 and b.errors() == 0
+    errs = compare(ga, gb, rtol=0.0, atol=0.0)
+    assert errs == [], "\n".join(errs)
+    pres = (ga.slot["uts_rank"] >= 0) & (ga.slot["slot_src"] >= 0)
+    src = ga.slot["slot_src"][pres]
+    assert pres.sum() > 100
+    assert np.array_equal(ga.slot["uts_xyzr"][pres], ga.node["gnn"][src])

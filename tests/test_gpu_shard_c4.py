@@ -1,5 +1,5 @@
 """The edge-sharded pass at full C4 size (BASELINE configs[3]): the benchmark
-event (179,788 hits / 1,027,548 directed edges) cut into 2 and 4 azimuthal wedges, one
+event (179,788 hits / 1,027,548 directed edges) cut into 2, 4 and 8 azimuthal wedges, one
 rank per wedge, the ranks sharing the box's one GPU and exchanging the halo over gloo
 (the N > 1 path of bench.py with RCCL replaced by gloo; the kernels and the exchange
 lists are the same).
@@ -7,7 +7,8 @@ lists are the same).
 Two passes with the halo exchange between them, then sync(). Every rank's owned
 receivers and slots must equal the one-GPU pass bit for bit after pass 1 and after
 pass 2, and pass 1 (assembled from the ranks) must match the oracle digest
-tests/golden/c4_digest.npz. That keeps the reference's per-sender cumulative
+tests/golden/c4_digest.npz. World 8 is configs[3] itself ("edge-sharded across 8 x MI355X"):
+the narrowest wedges, where the most senders straddle a cut. That keeps the reference's per-sender cumulative
 ``merged_cov[1,1] += var_ms`` (src/extrapolate/extrapolate_merged_states.py:127-128)
 across wedge boundaries: a sender whose successors sit in several wedges is scanned
 by every rank that owns one of them, each from the same halo copy of its state."""
@@ -85,7 +86,7 @@ def single_gpu():
     return g, outs
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_sharded_c4_equals_single_gpu_and_digest(world, single_gpu, tmp_path):
     import torch.multiprocessing as mp
     from test_gpu_c4_digest import _digest, digest_errors
@@ -96,7 +97,7 @@ def test_sharded_c4_equals_single_gpu_and_digest(world, single_gpu, tmp_path):
     for p in ps:
         p.start()
     for p in ps:
-        p.join(110)
+        p.join(110 + 25 * world)   # (8 ranks build and upload the event side by side)
     for p in ps:
         if p.exitcode is None:
             p.kill()

@@ -64,7 +64,7 @@ def _run(which, world, tmp_path, backend="gloo"):
     for p in ps:
         p.start()
     for p in ps:
-        p.join(110)
+        p.join(110 + 25 * world)
     for p in ps:
         if p.exitcode is None:
             p.kill()
@@ -72,7 +72,7 @@ def _run(which, world, tmp_path, backend="gloo"):
     return [np.load(os.path.join(tmp_path, "%s_w%d_r%d.npz" % (which, world, r))) for r in range(world)]
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_sharded_tags_vol7_equal_reference(world, tmp_path):
     from fixtures import load
     from gtf.device import DeviceGraph
@@ -85,7 +85,7 @@ def test_sharded_tags_vol7_equal_reference(world, tmp_path):
         assert np.array_equal(z["tags"][kept], extra["tags"][kept])
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_sharded_tags_c4_equal_single_gpu(world, tmp_path):
     from gtf.device import DeviceGraph
     g, tags, radius = _graph("c4")

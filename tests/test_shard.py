@@ -67,7 +67,7 @@ def test_wedge_layout_is_a_permutation_with_small_halo(world):
     assert halo < 0.5 * sum(x.size for x in h0.need_nodes)
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_halo_plan_is_what_the_next_pass_reads(world):
     """rank r needs exactly: the merged state of every sender it scans that another rank
     owns, and the activation of every out-edge of those senders (and of its own) whose

@@ -151,6 +151,22 @@ __device__ __forceinline__ void merge_with_inv(const double m1[3], const Cov5& i
     mv_cov5(co, t, mo);
 }
 
+// merge_with_inv of the parabolic (a, b, c) and the joint (a, b, tau) means at once, as one
+// 4-vector (a, b, c, tau): components 0 and 1 of the two merges are the same operations on
+// the same operands, so they are formed once
+__device__ __forceinline__ void merge4_with_inv(const double m1[4], const Cov5& i1, const double m2[4], const Cov5& i2,
+                                                const Cov5& co, double mo[4]) {
+    const double a0 = fma(i1.c00, m1[0], i1.c01 * m1[1]), a1 = fma(i1.c10, m1[0], i1.c11 * m1[1]);
+    const double b0 = fma(i2.c00, m2[0], i2.c01 * m2[1]), b1 = fma(i2.c10, m2[0], i2.c11 * m2[1]);
+    const double t0 = a0 + b0, t1 = a1 + b1;
+    const double tc = i1.c22 * m1[2] + i2.c22 * m2[2];
+    const double tt = i1.c22 * m1[3] + i2.c22 * m2[3];
+    mo[0] = fma(co.c00, t0, co.c01 * t1);
+    mo[1] = fma(co.c10, t0, co.c11 * t1);
+    mo[2] = co.c22 * tc;
+    mo[3] = co.c22 * tt;
+}
+
 __device__ __forceinline__ void merge_states(const double m1[3], const Cov5& c1, const double m2[3], const Cov5& c2,
                                              double mo[3], Cov5& co) {
     const Cov5 i1 = inv_cov5(c1);
@@ -207,16 +223,18 @@ __device__ __forceinline__ TauGeo tau_geo(double x, double z, double r, double z
 
 // mahalanobis_distance (clustering.py:11-78) from [a, b], the 2x2 covariance blocks,
 // the node's sigma pair and the two neighbours' TauGeo.
-__device__ __forceinline__ double mahalanobis_geo(double a1, double b1, const Cov5& c1, double a2, double b2,
-                                                  const Cov5& c2, double sza2, double sra2, const TauGeo& gb,
-                                                  const TauGeo& gc) {
+// its [a, b] term (d1) and its tau term (d2), separately
+__device__ __forceinline__ double maha_d1(double a1, double b1, const Cov5& c1, double a2, double b2, const Cov5& c2) {
     const double r0 = a1 - a2, r1 = b1 - b2;
     double i00, i01, i10, i11;
     inv2(c1.c00 + c2.c00, c1.c01 + c2.c01, c1.c10 + c2.c10, c1.c11 + c2.c11, i00, i01, i10, i11);
     // residual @ inv (gemv_t), then @ residual (ddot)
     const double t0 = fma(r1, i10, r0 * i00);
     const double t1 = fma(r1, i11, r0 * i01);
-    const double d1 = fma(t1, r1, t0 * r0);
+    return fma(t1, r1, t0 * r0);
+}
+
+__device__ __forceinline__ double maha_d2(double sza2, double sra2, const TauGeo& gb, const TauGeo& gc) {
     const double j2 = gb.q, j3 = -gc.q;
     const double j1 = -j3 - j2;
     const double j5 = -gb.w, j6 = gc.w;
@@ -229,7 +247,14 @@ __device__ __forceinline__ double mahalanobis_geo(double a1, double b1, const Co
     cdt = fma(j5 * gb.sr2, j5, cdt);
     cdt = fma(j6 * gc.sr2, j6, cdt);
     const double res = gb.tau - gc.tau;
-    const double d2 = (res * res) * (1.0 / cdt);
+    return (res * res) * (1.0 / cdt);
+}
+
+__device__ __forceinline__ double mahalanobis_geo(double a1, double b1, const Cov5& c1, double a2, double b2,
+                                                  const Cov5& c2, double sza2, double sra2, const TauGeo& gb,
+                                                  const TauGeo& gc) {
+    const double d1 = maha_d1(a1, b1, c1, a2, b2, c2);
+    const double d2 = maha_d2(sza2, sra2, gb, gc);
     return d1 + d2;
 }
 

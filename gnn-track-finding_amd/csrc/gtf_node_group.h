@@ -442,10 +442,15 @@ __device__ __forceinline__ void g_ranks(NodeCtx<G>& c) {
 // dict position to it: the operands can then be staged before the ops have settled
 // which keys are present and in what order (GTF_EARLY_STAGE).
 template <int CAP>
+#ifndef GTF_STAGE_NOINV
+#define GTF_STAGE_NOINV 0   // (with GTF_KL_LEAN) inverses in the owning lane's registers, not in LDS
+#endif
 struct StageT {
     double a[CAP], b[CAP], c[CAP], tau[CAP];
     double c00[CAP], c01[CAP], c10[CAP], c11[CAP], c22[CAP];
+#if !GTF_STAGE_NOINV
     double i00[CAP], i01[CAP], i10[CAP], i11[CAP], i22[CAP];
+#endif
     double q[CAP], w[CAP], tg[CAP], prior[CAP];   // (early staging parks x, z, r in q, w, tg)
     uint8_t ec[CAP];  // neighbour in the endcap (|x| >= boundary): picks its sigma_z / sigma_r pair
     uint8_t ord[CAP]; // slot lane of the state at each dict position
@@ -473,10 +478,14 @@ template <typename Stage>
 __device__ __forceinline__ Cov5 stage_cov(const Stage* s, int i) {
     return Cov5{s->c00[i], s->c01[i], s->c10[i], s->c11[i], s->c22[i]};
 }
+#if !GTF_STAGE_NOINV
 template <typename Stage>
 __device__ __forceinline__ Cov5 stage_inv(const Stage* s, int i) {
     return Cov5{s->i00[i], s->i01[i], s->i10[i], s->i11[i], s->i22[i]};
 }
+#elif !GTF_KL_LEAN
+#error "GTF_STAGE_NOINV needs GTF_KL_LEAN"
+#endif
 template <typename Stage>
 __device__ __forceinline__ TauGeo stage_geo(const Stage* s, int i, double szb2, double srb2) {
     TauGeo t;
@@ -513,11 +522,12 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
 #endif
     if (pres) {
         if (!c.staged) stage_raw(stg, me_l, S, c.k, gnn, live, c.src);
-        const Cov5 C = stage_cov(stg, me_l);
         const double x = stg->q[me_l], z = stg->w[me_l], r = stg->tg[me_l];
-        const Cov5 I = inv_cov5(C);
+#if !GTF_STAGE_NOINV
+        const Cov5 I = inv_cov5(stage_cov(stg, me_l));
         stg->i00[me_l] = I.c00; stg->i01[me_l] = I.c01; stg->i10[me_l] = I.c10; stg->i11[me_l] = I.c11;
         stg->i22[me_l] = I.c22;
+#endif
         const TauGeo t = tau_geo(x, z, r, za, ra, p.sigma0rz2, p.sigma0rz, p.sigma0rz, p.sigma0rz2, p.endcap_boundary);
         stg->q[me_l] = t.q; stg->w[me_l] = t.w; stg->tg[me_l] = t.tau;
         stg->ec[me_l] = fabs(x) >= p.endcap_boundary;
@@ -546,11 +556,21 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
             lmask |= (1u << i) | (1u << j);
         }
     };
+#ifndef GTF_PAIR_SPLIT
+#define GTF_PAIR_SPLIT 0   // the [a, b] term's operands, then the tau term's (fewer LDS values live at once)
+#endif
     auto pair_d = [&](int i, int j) {
         const int li = sb + stg->ord[sb + i], lj = sb + stg->ord[sb + j];
+#if GTF_PAIR_SPLIT
+        const double d1 = maha_d1(stg->a[li], stg->b[li], stage_cov(stg, li), stg->a[lj], stg->b[lj], stage_cov(stg, lj));
+        __builtin_amdgcn_sched_barrier(0);
+        const double d2 = maha_d2(sza2, sra2, stage_geo(stg, li, szb2, srb2), stage_geo(stg, lj, szb2, srb2));
+        return d1 + d2;
+#else
         return mahalanobis_geo(stg->a[li], stg->b[li], stage_cov(stg, li), stg->a[lj], stg->b[lj],
                                stage_cov(stg, lj), sza2, sra2, stage_geo(stg, li, szb2, srb2),
                                stage_geo(stg, lj, szb2, srb2));
+#endif
     };
 #ifndef GTF_PAIR_UNROLL
 #define GTF_PAIR_UNROLL 1
@@ -600,6 +620,88 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
     if (t1 < (1 << 20)) pair_ij(t1, ti1, tj1);
     // merged pair = (idx[0], idx[1]) of concatenate((rows, cols)) (:231-233)
     const int p0 = ti0, p1 = (t1 < (1 << 20)) ? ti1 : tj0;
+#ifndef GTF_KL_LEAN
+#define GTF_KL_LEAN 0
+#endif
+#if GTF_KL_LEAN
+    // the parabolic and the joint merged means share components 0 and 1 bit for bit (the same
+    // a, b through the same block-diagonal products: merge_with_inv), so one 4-vector
+    // (a, b, c, tau) carries both; the per-lane KL operands are re-read from LDS every
+    // iteration instead of held in registers across the loop (fewer live registers)
+    double mm[4];
+    Cov5 mc;
+    const int l0 = sb + stg->ord[sb + p0], l1 = sb + stg->ord[sb + p1];
+#if GTF_STAGE_NOINV == 2
+    // inverses recomputed from the staged covariances where they are used (np.linalg.inv of a
+    // state's covariance is the same value wherever the reference recomputes it): no register
+    // holds one across the loop
+    auto inv_of = [&](int l) { return inv_cov5(stage_cov(stg, l)); };
+#elif GTF_STAGE_NOINV
+    // every present state's inverse in its own lane (np.linalg.inv of its covariance, the same
+    // value wherever the reference recomputes it); a merge takes it from the owner by shuffles
+    Cov5 myI{0.0, 0.0, 0.0, 0.0, 0.0};
+    if (pres) myI = inv_cov5(stage_cov(stg, me_l));
+    auto inv_of = [&](int l) {
+        const int src = l - sb;
+        return Cov5{c.grp.shfl(myI.c00, src), c.grp.shfl(myI.c01, src), c.grp.shfl(myI.c10, src),
+                    c.grp.shfl(myI.c11, src), c.grp.shfl(myI.c22, src)};
+    };
+#else
+    auto inv_of = [&](int l) { return stage_inv(stg, l); };
+#endif
+    {
+        const Cov5 i0 = inv_of(l0), i1 = inv_of(l1);
+        mc = inv_cov5(add_cov5(i0, i1));
+        const double x0[4] = {stg->a[l0], stg->b[l0], stg->c[l0], stg->tau[l0]};
+        const double x1[4] = {stg->a[l1], stg->b[l1], stg->c[l1], stg->tau[l1]};
+        merge4_with_inv(x0, i0, x1, i1, mc, mm);
+    }
+    double mprior = stg->prior[l0] + stg->prior[l1];
+    unsigned alive = ((1u << d) - 1u) & ~tiemask;
+    if (alive == 0) {
+        if (c.grp.gl == 0) raise_node(err, c.v, GTF_ERR_TIE_EMPTIED);
+    } else {
+        while (GTF_ABLATE != 3) {                                                  // :251-287
+            asm volatile("" ::: "memory");
+            const Cov5 im = inv_cov5(mc);   // the merged state's inverse, shared by KL and the next merge
+            const bool me = pres && (alive >> pos & 1u);
+            double D = INFINITY;
+            bool dn = false;
+            if (me) {
+                const double js_me[3] = {stg->a[me_l], stg->b[me_l], stg->tau[me_l]};
+                const double jm[3] = {mm[0], mm[1], mm[3]};
+#if GTF_STAGE_NOINV == 2
+                const Cov5 cme = stage_cov(stg, me_l);
+                D = kl_with_inv(js_me, cme, inv_cov5(cme), jm, mc, im);
+#elif GTF_STAGE_NOINV
+                D = kl_with_inv(js_me, stage_cov(stg, me_l), myI, jm, mc, im);
+#else
+                D = kl_with_inv(js_me, stage_cov(stg, me_l), stage_inv(stg, me_l), jm, mc, im);
+#endif
+                if (D != D) { dn = true; D = INFINITY; }
+            }
+            if (c.grp.any(dn)) {
+                if (c.grp.gl == 0) raise_node(err, c.v, GTF_ERR_NAN_KL);
+                break;
+            }
+            const double mind = c.grp.min_d(D);
+            if (!(mind < kl_thr)) break;
+            const int m = c.grp.min_i((me && D == mind) ? pos : 99);  // first minimum (list.index)
+            const int lm = sb + stg->ord[sb + m];
+            const Cov5 ii = inv_of(lm);
+            const Cov5 nmc = inv_cov5(add_cov5(ii, im));
+            const double x[4] = {stg->a[lm], stg->b[lm], stg->c[lm], stg->tau[lm]};
+            double nm[4];
+            merge4_with_inv(x, ii, mm, im, nmc, nm);
+            mm[0] = nm[0]; mm[1] = nm[1]; mm[2] = nm[2]; mm[3] = nm[3];
+            mc = nmc;
+            mprior = stg->prior[lm] + mprior;
+            alive &= ~(1u << m);
+            if (alive == 0) break;
+        }
+    }
+    const double pm[3] = {mm[0], mm[1], mm[2]};
+#else
     double pm[3], jm[3];
     Cov5 mc;
     const int l0 = sb + stg->ord[sb + p0], l1 = sb + stg->ord[sb + p1];
@@ -651,6 +753,7 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
             if (alive == 0) break;
         }
     }
+#endif
     wave_lds_sync();
     if (c.grp.gl == 0) {                                                           // :291-293
         n.has_merged[c.v] = 1;
@@ -801,11 +904,32 @@ __device__ __forceinline__ void node_store(NodeCtx<G>& c, gtf_nodes& n, gtf_stat
     if (c.degree_set && c.grp.gl == 0) n.degree[c.v] = c.degree;
 }
 
+// OP_FLUSH: the fields no later op of a compile-time sequence changes (the TSE dict, the UTS
+// ranks, lr / side and the edge weight once the last reweight ran), stored before the
+// clustering so their registers are free there; node_store then skips them
+template <int G>
+__device__ __forceinline__ void node_flush(NodeCtx<G>& c, gtf_states& tse, gtf_states& uts, gtf_edges& e) {
+    const int k = c.k;
+    if (c.valid) {
+        if (c.edge_mw_dirty) e.edge_mw[k] = c.edge_mw;
+        if (c.tse.dirty & D_RANK) tse.rank[k] = c.tse.rank;
+        if (c.tse.dirty & D_MW) tse.mw[k] = c.tse.mw;
+        if (c.tse.dirty & D_PRIOR) tse.prior[k] = c.tse.prior;
+        if (c.uts.dirty & D_RANK) uts.rank[k] = c.uts.rank;
+        if (c.uts_dirty_lr) { uts.lr[k] = c.lr; uts.side[k] = c.side; }
+    }
+    c.edge_mw_dirty = false;
+    c.tse.dirty = 0;
+    c.uts.dirty &= (uint8_t)~D_RANK;
+    c.uts_dirty_lr = false;
+}
+
 template <int G, int OP, typename Stage>
 __device__ __forceinline__ void node_op(NodeCtx<G>& c, const gtf_graph& g, gtf_nodes& n, gtf_states& tse,
-                                        gtf_states& uts, const gtf_params& p, const Ws& w, double* sval,
-                                        Stage* stg, double chi2_thr, double kl_thr, bool has_tse,
+                                        gtf_states& uts, gtf_edges& e, const gtf_params& p, const Ws& w,
+                                        double* sval, Stage* stg, double chi2_thr, double kl_thr, bool has_tse,
                                         bool has_uts) {
+    if constexpr (OP == OP_FLUSH) node_flush(c, tse, uts, e);
     if constexpr (OP == OP_FRESH) g_fresh(c);
     if constexpr (OP == OP_RANKS) g_ranks(c);
     if constexpr (OP == OP_PRIORS_TSE) { if (has_tse) g_priors(c, c.tse, sval); }
@@ -878,10 +1002,10 @@ __device__ __forceinline__ bool ops_have_fresh(const NodeOps& ops) {
 __device__ uint64_t g_op_time[GTF_OP_TIMING_WAVES * 24];
 template <int G, int OP, typename Stage>
 __device__ __forceinline__ void node_op_timed(NodeCtx<G>& c, const gtf_graph& g, gtf_nodes& n, gtf_states& tse,
-                                              gtf_states& uts, const gtf_params& p, const Ws& w, double* sval,
+                                              gtf_states& uts, gtf_edges& e, const gtf_params& p, const Ws& w, double* sval,
                                               Stage* stg, double chi2_thr, double kl_thr, bool has_tse, bool has_uts,
                                               uint64_t* tb, int& ti) {
-    node_op<G, OP, Stage>(c, g, n, tse, uts, p, w, sval, stg, chi2_thr, kl_thr, has_tse, has_uts);
+    node_op<G, OP, Stage>(c, g, n, tse, uts, e, p, w, sval, stg, chi2_thr, kl_thr, has_tse, has_uts);
     const uint64_t t = __builtin_readcyclecounter();
     if (tb && ti < 20) tb[ti] = t;
     ti++;
@@ -935,10 +1059,10 @@ __device__ __forceinline__ void node_seq_body(const gtf_graph& g, gtf_nodes& n, 
     // diagnostics build: the node's loads and stores only (every field marked dirty)
     if (has_tse || has_uts) { c.uts.dirty = c.tse.dirty = D_RANK | D_MW | D_PRIOR; c.uts_dirty_lr = true; c.edge_mw_dirty = true; }
 #elif GTF_OP_TIMING
-    (node_op_timed<G, OPS, Stage>(c, g, n, tse, uts, p, w, sval, stg, chi2_thr, kl_thr, has_tse, has_uts, tb, ti),
+    (node_op_timed<G, OPS, Stage>(c, g, n, tse, uts, e, p, w, sval, stg, chi2_thr, kl_thr, has_tse, has_uts, tb, ti),
      ...);
 #else
-    (node_op<G, OPS, Stage>(c, g, n, tse, uts, p, w, sval, stg, chi2_thr, kl_thr, has_tse, has_uts), ...);
+    (node_op<G, OPS, Stage>(c, g, n, tse, uts, e, p, w, sval, stg, chi2_thr, kl_thr, has_tse, has_uts), ...);
 #endif
     node_store(c, n, tse, uts, e);
 #if GTF_OP_TIMING
@@ -1011,8 +1135,16 @@ __device__ __forceinline__ void node_bucket(int q, int b, char* smem) {
 
 // one launch over every bucket: blocks of the long-running buckets (many slots per node)
 // are dealt first so they overlap the bulk of small nodes instead of trailing it
+#ifndef GTF_NODE_WAVES
+#define GTF_NODE_WAVES 0   // > 0: amdgpu_waves_per_eu lower bound for the fused node kernel (register budget)
+#endif
+#if GTF_NODE_WAVES > 0
+#define GTF_NODE_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(GTF_NODE_WAVES)))
+#else
+#define GTF_NODE_WAVES_ATTR
+#endif
 template <int... OPS>
-__global__ void __launch_bounds__(NBLOCK) k_node_multi(NodeKArgs args) {
+__global__ void __launch_bounds__(NBLOCK) GTF_NODE_WAVES_ATTR k_node_multi(NodeKArgs args) {
     (void)args;   // read through node_kargs()
     using Q = OpSeq<OPS...>;
     __shared__ __attribute__((aligned(16))) char smem[Q::cluster ? node_smem_bytes() : NBLOCK * sizeof(double)];
@@ -1078,7 +1210,7 @@ __global__ void __launch_bounds__(NBLOCK) k_node_pack(gtf_graph g, gtf_nodes n, 
     Stage* stg = (Stage*)(smem + NBLOCK * sizeof(double)) + (Q::cluster ? (int)threadIdx.x / 64 : 0);
     const bool has_tse = n.has_tse[c.v];
     const bool has_uts = fresh_has_uts(c, n, Q::fresh);
-    (node_op<0, OPS, Stage>(c, g, n, tse, uts, p, w, sval, stg, chi2_thr, kl_thr, has_tse, has_uts), ...);
+    (node_op<0, OPS, Stage>(c, g, n, tse, uts, e, p, w, sval, stg, chi2_thr, kl_thr, has_tse, has_uts), ...);
     node_store(c, n, tse, uts, e);
 }
 
@@ -1104,7 +1236,7 @@ __global__ void __launch_bounds__(NBLOCK) k_node_group(gtf_graph g, gtf_nodes n,
     for (int i = 0; i < ops.n; i++) {
         switch (ops.op[i]) {
 #define GTF_CASE(OPC) \
-    case OPC: node_op<G, OPC, Stage>(c, g, n, tse, uts, p, w, sval, stg, chi2_thr, kl_thr, has_tse, has_uts); break;
+    case OPC: node_op<G, OPC, Stage>(c, g, n, tse, uts, e, p, w, sval, stg, chi2_thr, kl_thr, has_tse, has_uts); break;
             GTF_CASE(OP_FRESH)
             GTF_CASE(OP_RANKS)
             GTF_CASE(OP_PRIORS_TSE)

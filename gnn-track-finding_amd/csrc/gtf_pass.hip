@@ -732,6 +732,7 @@ enum : int8_t {
     OP_CLUSTER_TSE = 9,  // clustering.py:197-321 on track_state_estimates
     OP_CLUSTER_UTS = 10, // ... on updated_track_states
     OP_FRESH = 11,       // finish the entries k_extrapolate wrote (weight = sender's, no prior/lr/side)
+    OP_FLUSH = 12,       // (internal, compile-time sequences) store the slot fields no later op changes
 };
 
 struct NodeOps {
@@ -1026,6 +1027,14 @@ int run_pass(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts,
 #elif GTF_SEQ_VARIANT == 4
     rc = launch_seq<EXTRAP_OPS, UPDATE_OPS>(g, n, tse, uts, e, p, w, 0.0, 0.0, st);
 #else
+#ifndef GTF_EARLY_STORE
+#define GTF_EARLY_STORE 0   // store the update's final slot fields before the clustering (shorter live ranges)
+#endif
+#if GTF_EARLY_STORE
+    rc = launch_seq<EXTRAP_OPS, UPDATE_OPS, OP_FLUSH, CLUSTER_UTS_OPS>(g, n, tse, uts, e, p, w, p->cluster_chi2,
+                                                                       p->cluster_kl, st);
+    if (false)
+#endif
     rc = launch_seq<EXTRAP_OPS, UPDATE_OPS, CLUSTER_UTS_OPS>(g, n, tse, uts, e, p, w, p->cluster_chi2,
                                                              p->cluster_kl, st);
 #endif

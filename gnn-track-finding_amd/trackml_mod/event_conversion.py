@@ -12,10 +12,12 @@ subgraphs; the track state estimates run on the GPU (gtf_track_state_estimates t
 utilities.helper), then edge activation, priors, mixture weights and node degree; every
 subgraph is saved as <i>_subgraph.gpickle in CCA order.
 
-One deviation, for repositories that ship without the raw TrackML files (the reference's
-own copy lacks event000001000-truth.csv and -hits.csv, .MISSING_LARGE_BLOBS): when they
-are absent and the mapping file is present, the mapping is read as it is (a note on
-stderr) instead of failing on the missing files. The reference's timing prints are not
+One opt-in deviation, for repositories that ship without the raw TrackML files (the
+reference's own copy lacks event000001000-truth.csv and -hits.csv, .MISSING_LARGE_BLOBS):
+with GTF_REUSE_TRUTH_MAPPING=1, when they are absent and the mapping file is present, the
+mapping is read as it is (a note on stderr; its node set is checked against
+nodes_to_hits.csv when that file exists) instead of failing on the missing files. By
+default the CLI fails there like the reference. The reference's timing prints are not
 produced.
 """
 import argparse
@@ -55,12 +57,20 @@ def main():
     import pandas as pd
     raw = [event_truth + f for f in ("truth.csv", "particles.csv", "hits.csv")] + [event_network + "nodes_to_hits.csv"]
     missing = [f for f in raw if not os.path.isfile(f)]
-    if missing and os.path.isfile(event_truth_file):
-        print("event_conversion: %s absent; reading the existing truth mapping %s"
+    reuse = os.environ.get("GTF_REUSE_TRUTH_MAPPING", "0") == "1"
+    if missing and reuse and os.path.isfile(event_truth_file):
+        # opt-in only: the reference fails here (its load_save_truth reads the raw files)
+        print("event_conversion: %s absent; reading the existing truth mapping %s (GTF_REUSE_TRUTH_MAPPING=1)"
               % (", ".join(os.path.basename(f) for f in missing), event_truth_file), file=sys.stderr)
+        truth = pd.read_csv(event_truth_file)
+        n2h = event_network + "nodes_to_hits.csv"
+        if os.path.isfile(n2h):   # a mapping left from another event would give wrong truth silently
+            want = set(pd.read_csv(n2h, usecols=["node_idx"])["node_idx"].tolist())
+            if set(truth["node_idx"].tolist()) != want:
+                raise SystemExit("event_conversion: %s does not map the nodes of %s" % (event_truth_file, n2h))
     else:
         _io.aggregate_truth(event_network, event_truth, event_truth_file)                # :51-53
-    truth = pd.read_csv(event_truth_file)
+        truth = pd.read_csv(event_truth_file)
 
     subGraphs = _io.build_networkx(event_network, min_volume, max_volume, truth=truth)    # :63-86
     subGraphs = h.compute_track_state_estimates(subGraphs, sigma0xy, sigma0rz, sigma0rz2, endcap_boundary)  # :94

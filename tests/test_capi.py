@@ -115,3 +115,18 @@ def test_kl_gnn_stride_is_checked_without_a_gpu():
     g = nat.GtfKlGraph(n_nodes=0, n_slots=0, gnn_stride=3)
     rc = L.gtf_parabolic_kl(ctypes.byref(g), 0, ctypes.byref(nat.GtfKlOut()), ctypes.c_void_p(0))
     assert rc == -2 and b"gnn_stride" in L.gtf_last_error()
+
+
+def test_rccl_is_loaded_lazily():
+    """libgtf links no RCCL (gtf_comm_* dlopen it on first use): the drop-in CLIs that never
+    touch a collective do not map its ~0.5 GB of device code at start-up"""
+    from gtf import _native
+    if not os.path.exists(_native.LIB_PATH):
+        pytest.skip("libgtf.so not built")
+    out = subprocess.run(["readelf", "-d", _native.LIB_PATH], capture_output=True, text=True).stdout
+    needed = re.findall(r"\(NEEDED\)\s+Shared library: \[([^\]]+)\]", out)
+    assert needed and not any("rccl" in n for n in needed), needed
+    L = _native.lib()
+    comm = ctypes.c_void_p()
+    assert L.gtf_comm_init(ctypes.byref(comm), 0, 0, None) != 0      # bad arguments, no RCCL needed
+    assert b"bad arguments" in L.gtf_last_error()

@@ -139,9 +139,16 @@ def test_event_conversion_cli(tmp_path):
     _truth_frame().to_csv(str(tru / "event000001000-full-mapping-minCurv-0.3-800.csv"), index=False)
     r = subprocess.run([sys.executable, os.path.join(PKG, "trackml_mod", "event_conversion.py"), "-o", str(out) + "/",
                         "-n", str(net), "-t", str(tru), "-a", "7", "-z", "7", "-e", "0.3", "-r", "0.4", "-m", "0.6",
-                        "-b", "550"], capture_output=True, text=True, timeout=600)
+                        "-b", "550"], capture_output=True, text=True, timeout=600,
+                       env=dict(os.environ, GTF_REUSE_TRUTH_MAPPING="1"))
     assert r.returncode == 0, r.stderr[-3000:]
     assert "reading the existing truth mapping" in r.stderr
+    # without the opt-in the CLI fails on the missing raw files, as the reference does
+    r0 = subprocess.run([sys.executable, os.path.join(PKG, "trackml_mod", "event_conversion.py"), "-o",
+                         str(tmp_path) + "/out0/", "-n", str(net), "-t", str(tru), "-a", "7", "-z", "7", "-e", "0.3",
+                         "-r", "0.4", "-m", "0.6", "-b", "550"], capture_output=True, text=True, timeout=600,
+                        env={k: v for k, v in os.environ.items() if k != "GTF_REUSE_TRUTH_MAPPING"})
+    assert r0.returncode != 0
     ptr, nodes = gold["node_ptr"], gold["nodes"]
     for i in range(gold["n_subgraphs"]):
         with open(str(out / ("%d_subgraph.gpickle" % i)), "rb") as f:

@@ -29,8 +29,12 @@ def c4():
 
 
 def _state(d):
-    """every array a pass may write (DeviceGraph.snapshot's default set)"""
-    return {k: v.cpu().numpy().reshape(-1) for k, v in d.snapshot().items()}
+    """every array a pass may write (DeviceGraph.snapshot's default set), with the live state
+    coordinates materialised as download() does (gtf_uts_materialize; fresh bit 0)"""
+    d.materialize()
+    out = {k: v.cpu().numpy().reshape(-1) for k, v in d.snapshot().items()}
+    out["uts_fresh"] = out["uts_fresh"] & 1
+    return out
 
 
 def _state_keys(g):

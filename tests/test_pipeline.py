@@ -193,6 +193,7 @@ def test_gpu_run_script_with_dropin_clis(tmp_path):
 
     def cli(module, *args):
         r = subprocess.run([sys.executable, os.path.join(pkg, module)] + list(args), capture_output=True, text=True,
+                           env=dict(os.environ, GTF_REUSE_TRUTH_MAPPING="1"),
                            timeout=600)
         assert r.returncode == 0, (module, r.stderr[-3000:])
 

@@ -8,17 +8,18 @@
 # tools/ab.sh.
 set -e
 cd "$(dirname "$0")/../gnn-track-finding_amd/csrc"
-SRC="gtf_pass.hip gtf_tags.hip gtf_kl.hip gtf_tse.hip gtf_shard.hip gtf_extract.hip gtf_a15.hip gtf_build.cpp gtf_build_dev.hip gtf_mem.hip"
-CXX="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -shared"
-if [ -n "$1" ]; then
+# one variant: the library's Makefile with its own object directory and output name
+build() {
   name=$1; shift
-  $CXX "$@" -o ../gtf/libgtf_$name.so $SRC
+  make -s -j8 OUT=../gtf/libgtf_$name.so OBJDIR=../../build/obj_$name EXTRA="$*"
+}
+if [ -n "$1" ]; then
+  build "$@"
   exit 0
 fi
 for a in 1 2 3 6; do   # (4: loads + stores of every field -- faulted on a drop-in graph, not built)
-  $CXX -DGTF_ABLATE=$a -o ../gtf/libgtf_ablate$a.so $SRC &
+  build ablate$a -DGTF_ABLATE=$a
 done
 for v in 1 2 3 4; do
-  $CXX -DGTF_SEQ_VARIANT=$v -o ../gtf/libgtf_seq$v.so $SRC &
+  build seq$v -DGTF_SEQ_VARIANT=$v
 done
-wait

@@ -24,6 +24,7 @@ NAMES = {
     "k_node_multi<10, 5, 8, 3>": "k_node_multi<cluster> (KL-distance kernel)",
     "k_node_multi<1, 3, 4, 3, 4, 5, 6, 2, 3, 4, 10, 5, 8, 3>": "k_node_multi<update+cluster> (KL-distance kernel)",
     "k_node_multi<11, 1, 3, 4, 3, 4, 5, 6, 2, 3, 4, 10, 5, 8, 3>": "k_node_multi<update+cluster> (KL-distance kernel)",
+    "k_node_multi<11, 1, 3, 4, 3, 4, 5, 6, 2, 3, 4, 12, 10, 5, 8, 3>": "k_node_multi<update+cluster> (KL-distance kernel)",
     "k_parabolic_kl<double, false>": "k_parabolic_kl (fp64)",
     "k_parabolic_kl<float, false>": "k_parabolic_kl (fp32)",
     "k_parabolic_kl_win<double, false>": "k_parabolic_kl_win (fp64, tiled layout)",

@@ -36,6 +36,7 @@ def main(path):
         t = time.perf_counter()
         pre = ["-m", "cProfile", "-s", "cumulative"] if name == prof else []
         r = subprocess.run([sys.executable] + pre + [os.path.join(PKG, module)] + list(args), check=True,
+                           env=dict(os.environ, GTF_REUSE_TRUTH_MAPPING="1"),
                            capture_output=True, text=True)
         if pre:
             print("\n".join(r.stdout.splitlines()[:60]))

@@ -196,7 +196,12 @@ int gtf_tag_propagate_shard(gtf_comm* comm, const gtf_graph* g, const gtf_shard*
     p += al(n);
     int64_t* buf[2] = {reinterpret_cast<int64_t*>(p), reinterpret_cast<int64_t*>(p + al(sizeof(int64_t) * w))};
     *sweeps_out = 0;
-    if (int rc = gtf_tag_prepare(g, radius, keep, proc, cnt, stream)) return rc;
+    // prepare covers the whole replica: a rank's graph view carries only its own senders'
+    // schedule, so the thread-per-node form (no out_sched) runs here
+    gtf_graph whole = *g;
+    whole.out_sched = nullptr;
+    whole.out_lanes = nullptr;
+    if (int rc = gtf_tag_prepare(&whole, radius, keep, proc, cnt, stream)) return rc;
     int32_t total = 0;
     if (N > 0 && hipMemcpyAsync(buf[0], tags, sizeof(int64_t) * (size_t)N, hipMemcpyDeviceToDevice, st) != hipSuccess)
         return fail("gtf_tag_propagate_shard: copying the tags");

@@ -26,14 +26,38 @@
 #define GTF_EARLY_STAGE 0   // clustering operands loaded into LDS with the slot fields
 #endif
 
+// Lane exchanges inside one wavefront through ds_bpermute with byte addresses computed
+// once per lane: a power-of-two group's lanes are [gbase, gbase + G), so a shuffle from
+// group lane src reads wave lane gbase + src and an xor-butterfly step with o < G stays in
+// the group by itself -- none of the lane-id and bounds arithmetic of the generic __shfl /
+// __shfl_xor (which recomputes the lane id on every call)
+#ifndef GTF_FAST_SHFL
+#define GTF_FAST_SHFL 1
+#endif
+__device__ __forceinline__ int bperm32(int addr, int v) { return __builtin_amdgcn_ds_bpermute(addr, v); }
+template <typename T>
+__device__ __forceinline__ T bperm(int addr, T x) {
+    static_assert(sizeof(T) == 4 || sizeof(T) == 8, "32- or 64-bit lane values");
+    if constexpr (sizeof(T) == 4) {
+        return __builtin_bit_cast(T, bperm32(addr, __builtin_bit_cast(int, x)));
+    } else {
+        const unsigned long long u = __builtin_bit_cast(unsigned long long, x);
+        const unsigned lo = (unsigned)bperm32(addr, (int)(unsigned)u);
+        const unsigned hi = (unsigned)bperm32(addr, (int)(unsigned)(u >> 32));
+        return __builtin_bit_cast(T, ((unsigned long long)hi << 32) | lo);
+    }
+}
+
 template <int G>
 struct Grp {
     int gl;     // lane within the group
     int gbase;  // first wave lane of the group
+    int lane4;  // 4 x the wave lane (ds_bpermute byte address of this lane)
     __device__ __forceinline__ Grp() {
         const int lane = threadIdx.x & 63;
         gl = lane & (G - 1);
         gbase = lane & ~(G - 1);
+        lane4 = lane << 2;
     }
     __device__ __forceinline__ unsigned long long bits(bool pred) const {
         const unsigned long long b = __ballot(pred);
@@ -41,26 +65,35 @@ struct Grp {
     }
     __device__ __forceinline__ int count(bool pred) const { return __popcll(bits(pred)); }
     __device__ __forceinline__ bool any(bool pred) const { return bits(pred) != 0ull; }
+#if GTF_FAST_SHFL
+    template <typename T>
+    __device__ __forceinline__ T shfl(T x, int src) const { return bperm<T>((gbase + src) << 2, x); }
+    template <typename T>
+    __device__ __forceinline__ T xshfl(T x, int o) const { return bperm<T>(lane4 ^ (o << 2), x); }
+#else
     template <typename T>
     __device__ __forceinline__ T shfl(T x, int src) const { return __shfl(x, src, G); }
+    template <typename T>
+    __device__ __forceinline__ T xshfl(T x, int o) const { return __shfl_xor(x, o, G); }
+#endif
     __device__ __forceinline__ int max_i(int x) const {
 #pragma unroll
-        for (int o = G / 2; o > 0; o >>= 1) x = max(x, __shfl_xor(x, o, G));
+        for (int o = G / 2; o > 0; o >>= 1) x = max(x, xshfl(x, o));
         return x;
     }
     __device__ __forceinline__ int min_i(int x) const {
 #pragma unroll
-        for (int o = G / 2; o > 0; o >>= 1) x = min(x, __shfl_xor(x, o, G));
+        for (int o = G / 2; o > 0; o >>= 1) x = min(x, xshfl(x, o));
         return x;
     }
     __device__ __forceinline__ double min_d(double x) const {  // NaN-free inputs
 #pragma unroll
-        for (int o = G / 2; o > 0; o >>= 1) x = fmin(x, __shfl_xor(x, o, G));
+        for (int o = G / 2; o > 0; o >>= 1) x = fmin(x, xshfl(x, o));
         return x;
     }
     __device__ __forceinline__ unsigned or_u(unsigned x) const {
 #pragma unroll
-        for (int o = G / 2; o > 0; o >>= 1) x |= __shfl_xor(x, o, G);
+        for (int o = G / 2; o > 0; o >>= 1) x |= xshfl(x, o);
         return x;
     }
     __device__ __forceinline__ int size() const { return G; }

@@ -461,7 +461,9 @@ class ShardedDeviceGraph:
         ta[:N] = torch.from_numpy(np.ascontiguousarray(d._to_dev_nodes(tags), dtype=np.int64)).to(dev)
         tb = torch.zeros(N + W, dtype=torch.int64, device=dev)
         st = d.stream
-        nat.check(d.lib.gtf_tag_prepare(ctypes.byref(self.cg), vp(r), vp(keep), vp(proc), vp(cnt), st))
+        # the replica's whole-event graph (d.cg: its sender schedule lists every sender); self.cg's
+        # schedule holds only this rank's senders
+        nat.check(d.lib.gtf_tag_prepare(ctypes.byref(d.cg), vp(r), vp(keep), vp(proc), vp(cnt), st))
         total = int(cnt[0].item())
         hist = []
         frac = 1.0

@@ -362,7 +362,9 @@ int gtf_halo_unpack(gtf_nodes* n, gtf_edges* e, const gtf_halo* h, const void* b
 
 /* Tag propagation. radius: [N] node radius (attr 'zr'[1]); keep: [E] output mask of
  * kept inward neighbours per out-edge (u8, indexed by out-edge position);
- * processed: [N] u8 output; n_processed: device int32 output. */
+ * processed: [N] u8 output; n_processed: device int32 output. With g->out_sched set the
+ * prepare runs on its lane groups, so that schedule must list every node with an out-edge
+ * (not a shard's restricted one: pass the graph without out_sched then). */
 int gtf_tag_prepare(const gtf_graph* g, const double* radius, uint8_t* keep, uint8_t* processed,
                     int32_t* n_processed, gtf_stream_t stream);
 /* one Jacobi sweep: tags_out[u] = max(tags_in[u], tags_in[kept neighbours]); *flips = the

@@ -23,6 +23,9 @@ from gtf.params import Params  # noqa: E402
 
 OPS = ["fresh", "ranks", "priors_uts", "reweight", "priors_uts", "reweight", "degree", "prune", "priors_tse",
        "priors_uts", "reweight", "cluster_uts", "degree", "mw_uts", "priors_uts"]
+if os.environ.get("GTF_OPT_FLUSH", "0") == "1":   # a GTF_EARLY_STORE build: OP_FLUSH before the clustering
+    OPS.insert(OPS.index("cluster_uts"), "flush")
+NP = len(OPS) + 3   # start, after the loads, after each op, after the stores
 W = 65536
 
 L = nat.lib()
@@ -49,11 +52,11 @@ RT = 100.0               # ticks per microsecond
 out = {"waves": int(rows.shape[0]), "kernel_span_us": float((rows[:, 21].max() - t0) / RT), "by_G": {}}
 for G in sorted(set(rows[:, 23].tolist()), reverse=True):
     r = rows[rows[:, 23] == G]
-    ph = np.diff(r[:, :18], axis=1)   # load, 15 ops, store
+    ph = np.diff(r[:, :NP], axis=1)   # load, the ops, store
     names = ["%02d_%s" % (i, n) for i, n in enumerate(["load"] + OPS + ["store"])]
     out["by_G"][int(G)] = {"waves": int(r.shape[0]),
-                           "lifetime_mean": float((r[:, 17] - r[:, 0]).mean()),
-                           "lifetime_p90": float(np.percentile(r[:, 17] - r[:, 0], 90)),
+                           "lifetime_mean": float((r[:, NP - 1] - r[:, 0]).mean()),
+                           "lifetime_p90": float(np.percentile(r[:, NP - 1] - r[:, 0], 90)),
                            "lifetime_us_mean": float((r[:, 21] - r[:, 20]).mean() / RT),
                            "start_first_us": float((r[:, 20].min() - t0) / RT),
                            "start_last_us": float((r[:, 20].max() - t0) / RT),

@@ -99,7 +99,12 @@ if os.environ.get("GTF_SPLIT_GRAPH", "0") == "1":
                 fork[i].record(cap)
                 for s_ in sp.streams:
                     s_.wait_event(fork[i])
-                sp.step(p)
+                # without the step's closing mutual stream waits (the eager path's guard against the
+                # next step's pack overwriting a buffer the other stream still unpacks): the
+                # capture's join below orders both streams, and the two mutual waits -- each stream
+                # made to depend on the other's last node -- crashed hipStreamEndCapture (rc 139,
+                # tools/capture_probe.py modes "exchange" vs "step", profiles/r04/capture/)
+                sp.step(p, join=False)
                 for r_, s_ in enumerate(sp.streams):
                     joins[i][r_].record(s_)
                     cap.wait_event(joins[i][r_])

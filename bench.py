@@ -632,7 +632,8 @@ PMC_SUMMARY = os.path.join(ROOT, "profiles", "r03", "final", "c4", "pmc_c4.json"
 # per-launch SQ instruction counters of the pass kernels (tools/gpu_sqmix.sh, same event)
 SQ_SUMMARY = os.path.join(ROOT, "profiles", "r03", "final", "sqmix", "sqmix.json")
 SQ_NAMES = {"k_sender+k_extrapolate": ("k_sender_sched", "k_extrapolate"),
-            NODE_KERNEL: ("k_node_multi<11, 1, 3, 4, 3, 4, 5, 6, 2, 3, 4, 10, 5, 8, 3>",)}
+            NODE_KERNEL: ("k_node_multi<11, 1, 3, 4, 3, 4, 5, 6, 2, 3, 4, 12, 10, 5, 8, 3>",
+                          "k_node_multi<11, 1, 3, 4, 3, 4, 5, 6, 2, 3, 4, 10, 5, 8, 3>")}
 
 
 def committed_valu(kernel, ms, workload, layout, tile):
@@ -645,8 +646,11 @@ def committed_valu(kernel, ms, workload, layout, tile):
     try:
         with open(SQ_SUMMARY) as f:
             allc = json.load(f)
-        cs = [allc[n] for n in SQ_NAMES[kernel]]
-    except (OSError, KeyError, ValueError):
+        if kernel == NODE_KERNEL:   # the fused kernel under its current or its earlier op list
+            cs = [next(allc[n] for n in SQ_NAMES[kernel] if n in allc)]
+        else:
+            cs = [allc[n] for n in SQ_NAMES[kernel]]
+    except (OSError, KeyError, ValueError, StopIteration):
         return None
     floor = sum(rf.valu_issue_floor_s(c) for c in cs)
     return {"bound": "valu_issue", "valu_insts_per_launch": sum(c["SQ_INSTS_VALU"] for c in cs),

@@ -22,6 +22,9 @@
 #ifndef GTF_HOIST
 #define GTF_HOIST 1   // the node's own scalars (x, xyzr, solo) loaded with the slot fields
 #endif
+#ifndef GTF_KL_LEAN
+#define GTF_KL_LEAN 1   // the clustering's merged means as one 4-vector, KL operands re-read per iteration
+#endif
 #ifndef GTF_EARLY_STAGE
 #define GTF_EARLY_STAGE 0   // clustering operands loaded into LDS with the slot fields
 #endif
@@ -32,7 +35,7 @@
 // the group by itself -- none of the lane-id and bounds arithmetic of the generic __shfl /
 // __shfl_xor (which recomputes the lane id on every call)
 #ifndef GTF_FAST_SHFL
-#define GTF_FAST_SHFL 1
+#define GTF_FAST_SHFL 0   // measured neutral in instruction count; its lane register costs a spill at 5 waves
 #endif
 __device__ __forceinline__ int bperm32(int addr, int v) { return __builtin_amdgcn_ds_bpermute(addr, v); }
 template <typename T>
@@ -61,7 +64,8 @@ struct Grp {
     }
     __device__ __forceinline__ unsigned long long bits(bool pred) const {
         const unsigned long long b = __ballot(pred);
-        return G == 64 ? b : ((b >> gbase) & ((1ull << G) - 1ull));
+        if constexpr (G == 64) return b;
+        else return (b >> gbase) & ((1ull << G) - 1ull);
     }
     __device__ __forceinline__ int count(bool pred) const { return __popcll(bits(pred)); }
     __device__ __forceinline__ bool any(bool pred) const { return bits(pred) != 0ull; }
@@ -476,7 +480,8 @@ __device__ __forceinline__ void g_ranks(NodeCtx<G>& c) {
 // which keys are present and in what order (GTF_EARLY_STAGE).
 template <int CAP>
 #ifndef GTF_STAGE_NOINV
-#define GTF_STAGE_NOINV 0   // (with GTF_KL_LEAN) inverses in the owning lane's registers, not in LDS
+#define GTF_STAGE_NOINV 2   // (with GTF_KL_LEAN) no inverses in LDS: 1 = in the owning lane's registers,
+                            // 2 = recomputed from the staged covariances where used
 #endif
 struct StageT {
     double a[CAP], b[CAP], c[CAP], tau[CAP];
@@ -653,9 +658,6 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
     if (t1 < (1 << 20)) pair_ij(t1, ti1, tj1);
     // merged pair = (idx[0], idx[1]) of concatenate((rows, cols)) (:231-233)
     const int p0 = ti0, p1 = (t1 < (1 << 20)) ? ti1 : tj0;
-#ifndef GTF_KL_LEAN
-#define GTF_KL_LEAN 0
-#endif
 #if GTF_KL_LEAN
     // the parabolic and the joint merged means share components 0 and 1 bit for bit (the same
     // a, b through the same block-diagonal products: merge_with_inv), so one 4-vector
@@ -1169,7 +1171,7 @@ __device__ __forceinline__ void node_bucket(int q, int b, char* smem) {
 // one launch over every bucket: blocks of the long-running buckets (many slots per node)
 // are dealt first so they overlap the bulk of small nodes instead of trailing it
 #ifndef GTF_NODE_WAVES
-#define GTF_NODE_WAVES 0   // > 0: amdgpu_waves_per_eu lower bound for the fused node kernel (register budget)
+#define GTF_NODE_WAVES 5   // > 0: amdgpu_waves_per_eu lower bound for the fused node kernel (register budget)
 #endif
 #if GTF_NODE_WAVES > 0
 #define GTF_NODE_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(GTF_NODE_WAVES)))

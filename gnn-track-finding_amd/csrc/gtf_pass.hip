@@ -1028,7 +1028,7 @@ int run_pass(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts,
     rc = launch_seq<EXTRAP_OPS, UPDATE_OPS>(g, n, tse, uts, e, p, w, 0.0, 0.0, st);
 #else
 #ifndef GTF_EARLY_STORE
-#define GTF_EARLY_STORE 0   // store the update's final slot fields before the clustering (shorter live ranges)
+#define GTF_EARLY_STORE 1   // store the update's final slot fields before the clustering (shorter live ranges)
 #endif
 #if GTF_EARLY_STORE
     rc = launch_seq<EXTRAP_OPS, UPDATE_OPS, OP_FLUSH, CLUSTER_UTS_OPS>(g, n, tse, uts, e, p, w, p->cluster_chi2,

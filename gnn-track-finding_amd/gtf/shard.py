@@ -395,11 +395,11 @@ class ShardedDeviceGraph:
         _, st, sbuf = self._io()[:3]
         nat.check(d.lib.gtf_halo_pack(ctypes.byref(d.cn), ctypes.byref(d.ce), ctypes.byref(self.halo_send), sbuf, st))
 
-    def halo_unpack(self, buf):
+    def halo_unpack(self, buf, stream=None):
         """the received halo segments (device buffer address `buf`, receive layout) into this
-        rank's replica (on its stream)"""
+        rank's replica (on its stream, or on `stream`: a torch stream)"""
         d = self.d
-        st = self._io()[1]
+        st = self._io()[1] if stream is None else ctypes.c_void_p(stream.cuda_stream)
         nat.check(d.lib.gtf_halo_unpack(ctypes.byref(d.cn), ctypes.byref(d.ce), ctypes.byref(self.halo_recv), buf,
                                         st))
 

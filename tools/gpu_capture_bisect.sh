@@ -3,7 +3,7 @@
 # stopping at the first that fails (a crash ends the call's GPU work)
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-OUT=$R/gpurun_out/r04/capture
+OUT=$R/gpurun_out/r04/capture${CAPTURE_TAG:-}
 mkdir -p $OUT
 for m in ${MODES:-one shard halo fork exchange step}; do
   timeout -k 10 120 python3 -X faulthandler -u tools/capture_probe.py $m > $OUT/$m.log 2>&1

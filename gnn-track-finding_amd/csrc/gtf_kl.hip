@@ -294,12 +294,12 @@ __device__ __forceinline__ void pkl_node_body(const gtf_kl_graph& g, const gtf_k
 
 template <typename T, int G, bool STATES>
 __device__ __forceinline__ void pkl_node(const gtf_kl_graph& g, const gtf_kl_out& o, const int32_t* list, int count,
-                                         int bid, char* smem, int first = 0) {
-    const int gi = (bid * BLOCK + (int)threadIdx.x) / G;
+                                         int bid, char* smem, int first = 0, int tid = -1) {
+    if (tid < 0) tid = (int)threadIdx.x;   // (tid: the thread in a BLOCK-thread (sub)block)
+    const int gi = (bid * BLOCK + tid) / G;
     if (gi >= count) return;  // group-uniform
     const int v = list ? list[gi] : first + gi;   // (ordered layout: the bucket is a node range)
-    pkl_node_body<T, G, STATES>(g, o, GSrc(g), v, threadIdx.x & (G - 1),
-                                (KlStage<T, G>*)smem + (int)threadIdx.x / G);
+    pkl_node_body<T, G, STATES>(g, o, GSrc(g), v, tid & (G - 1), (KlStage<T, G>*)smem + tid / G);
 }
 
 // d <= 2: one thread per node, both states in registers (the bulk of a TrackML
@@ -346,15 +346,13 @@ __device__ __forceinline__ void pkl_node1_ordered(const gtf_kl_graph& g, const g
     }
 }
 
-// one- or two-edge node v (two: its slots l, l + 1 and pair pp; else slot l): both states
-// in registers
+// one- or two-edge node v (two: its slots l, l + 1 with senders u0, u1 and pair pp; else
+// slot l, sender u0): both states in registers
 template <typename T, bool STATES, typename S>
 __device__ __forceinline__ void pkl_b0_body(const gtf_kl_graph& g, const gtf_kl_out& o, const S& src, int v, bool two,
-                                            int64_t l, int64_t pp) {
+                                            int64_t l, int64_t pp, int u0, int u1) {
     const double xv = src.x(v), yv = src.y(v);
     const long long tv = (o.truth && g.truth) ? src.t(v) : 0;
-    const int u0 = g.slot_src[l];
-    const int u1 = two ? g.slot_src[l + 1] : u0;
     const double x0 = src.x(u0), y0 = src.y(u0);
     const double x1 = src.x(u1), y1 = src.y(u1);
     long long t0 = 0, t1 = 0;
@@ -514,8 +512,9 @@ __device__ __forceinline__ void pkl_node4_body(const gtf_kl_graph& g, const gtf_
 
 template <typename T, bool STATES>
 __device__ __forceinline__ void pkl_node4(const gtf_kl_graph& g, const gtf_kl_out& o, const int32_t* list, int count,
-                                          int bid, int first) {
-    const int gi = bid * BLOCK + (int)threadIdx.x;
+                                          int bid, int first, int tid = -1) {
+    if (tid < 0) tid = (int)threadIdx.x;
+    const int gi = bid * BLOCK + tid;
     if (gi >= count) return;
     pkl_node4_body<T, STATES>(g, o, GSrc(g), list ? list[gi] : first + gi);
 }
@@ -562,74 +561,127 @@ __global__ void __launch_bounds__(BLOCK) KL_ATTR k_parabolic_kl(gtf_kl_graph g, 
     else pkl_node1<T, STATES>(g, o, g.list[0], g.count[0], gtf::xcd_local(b, bk.blocks[0]));
 }
 
-// Tiled layout (gtf_kl_graph.blk, gtf.parabolic.ParabolicKL(tile=T)): one block of WBLOCK
-// threads per tile of <= WTILE nodes, the nodes of a tile ordered by bucket (one- and
-// two-edge, 3..4, 5..8, > 8 in-edges), the tiles cut from an azimuth-sorted node order.
-// The block first copies the x, y and truth ids of its window -- the tile and its two
-// neighbours, where the neighbours of its nodes lie -- into LDS in one round of coalesced
-// loads; every node then reads its neighbours from LDS (global memory beyond the window),
-// so a node costs one round of memory latency instead of two dependent ones (the slot
-// list, then the gathers). Record per tile (12 int32): first node, bucket-0 count, its
-// one-edge count, bucket 1 / 2 / 3 counts, bucket 0's first slot, its first pair (lo, hi),
-// window [lo, hi), 0.
+// Tiled layout (gtf_kl_graph.blk, gtf.parabolic.ParabolicKL(tile=T)): the nodes
+// azimuth-sorted per event and cut into tiles of <= 256 one- / two-edge (bucket-0) nodes
+// and the other nodes between them, bucket 0 first inside a tile. One block of WBLOCK
+// threads per tile, one bucket-0 node per thread: in ONE round of independent loads it
+// reads its thread's sender list and the x, y and truth ids of the tile's window -- the
+// tile and up to 128 nodes either side, where a hit's neighbours lie -- into LDS, then
+// every node reads its own coordinates and its neighbours' there (global memory outside
+// the window). The ordered layout needs two dependent rounds (the sender list, then the
+// gathers). Record per tile (12 int32): first node, bucket-0 count, its one-edge count,
+// 0, 0, 0, bucket 0's first slot, its first pair (lo, hi), window [lo, hi), 0. The 3..4,
+// 5..8 and > 8 buckets run from gtf_kl_graph.list in the same launch, ahead of the tiles,
+// each 256-thread block as WBLOCK / BLOCK sub-blocks of the list kernel's.
 constexpr int WBLOCK = 256;
-constexpr int WTILE = 256;
-constexpr int WWIN = 3 * WTILE;
-constexpr size_t wstage_bytes(size_t t) {
-    return stage_bytes(8, t) * (WBLOCK / BLOCK) > stage_bytes(64, t) * (WBLOCK / BLOCK)
-               ? stage_bytes(8, t) * (WBLOCK / BLOCK) : stage_bytes(64, t) * (WBLOCK / BLOCK);
+#ifndef GTF_KL_WWIN
+#define GTF_KL_WWIN 1024
+#endif
+constexpr int WWIN = GTF_KL_WWIN;          // window nodes (gtf.parabolic.WIN_NODES)
+constexpr int WPT = (WWIN + WBLOCK - 1) / WBLOCK;
+constexpr int SUBS = WBLOCK / BLOCK;
+constexpr size_t sub_stage_bytes(size_t t) {
+    return stage_bytes(4, t) > stage_bytes(64, t) ? stage_bytes(4, t) : stage_bytes(64, t);
+}
+constexpr size_t win_lds_bytes(size_t t) {
+    return WWIN * 24 > SUBS * sub_stage_bytes(t) ? WWIN * 24 : SUBS * sub_stage_bytes(t);
 }
 #ifndef GTF_KL_WIN_WAVES
-#define GTF_KL_WIN_WAVES 4
+#define GTF_KL_WIN_WAVES 5
 #endif
+struct WinBuckets {
+    int32_t blocks[4];   // [0] tile blocks (n_blk padded to 8), [1..3] list blocks
+};
+
 template <typename T, bool STATES>
-__global__ void __launch_bounds__(WBLOCK) __attribute__((amdgpu_waves_per_eu(GTF_KL_WIN_WAVES)))
-k_parabolic_kl_win(gtf_kl_graph g, gtf_kl_out o) {
-    __shared__ double sx[WWIN], sy[WWIN];
-    __shared__ long long st[WWIN];
-    __shared__ __attribute__((aligned(16))) char stage[wstage_bytes(sizeof(T))];
-    const int32_t* r = g.blk + 12 * (int64_t)gtf::xcd_local(blockIdx.x, gridDim.x);
-    const int node_lo = r[0], n0 = r[1], n1 = r[2], nb1 = r[3], nb2 = r[4], nb3 = r[5];
+__device__ __forceinline__ void pkl_tile(const gtf_kl_graph& g, const gtf_kl_out& o, int tile, char* lds) {
+    double* sx = (double*)lds;
+    double* sy = sx + WWIN;
+    long long* st = (long long*)(sy + WWIN);
+    const int32_t* r = g.blk + 12 * (int64_t)tile;
+    const int node_lo = r[0], n0 = r[1], n1 = r[2];
     const int64_t slot_lo = (int64_t)(uint32_t)r[6];
     const int64_t pair_lo = (int64_t)(uint32_t)r[7] | ((int64_t)r[8] << 32);
-    // the window never exceeds the LDS copy: nodes past wlo + WWIN are read from global memory
-    const int wlo = r[9], whi = min(r[10], wlo + WWIN);
-    for (int i = (int)threadIdx.x; i < whi - wlo; i += WBLOCK) {
-        sx[i] = gx(g, wlo + i);
-        sy[i] = gy(g, wlo + i);
-        if (g.truth) st[i] = g.truth[wlo + i];
+    const int wlo = r[9], wn = min(r[10], r[9] + WWIN) - r[9];
+    const int t = (int)threadIdx.x;
+    // one round: the thread's senders, then the window (all independent of each other)
+    const bool mine = t < n0, two = t >= n1;
+    const int64_t l = slot_lo + (two ? n1 + 2 * (int64_t)(t - n1) : t);
+    int u0 = 0, u1 = 0;
+    if (mine) {
+        u0 = ld_list(g.slot_src + l);
+        u1 = two ? ld_list(g.slot_src + l + 1) : u0;
+    }
+    double wx[WPT], wy[WPT];
+    long long wt[WPT];
+#pragma unroll
+    for (int j = 0; j < WPT; j++) {
+        const int i = t + j * WBLOCK;
+        if (i < wn) {
+            wx[j] = gx(g, wlo + i);
+            wy[j] = gy(g, wlo + i);
+            wt[j] = g.truth ? g.truth[wlo + i] : 0;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < WPT; j++) {
+        const int i = t + j * WBLOCK;
+        if (i < wn) {
+            sx[i] = wx[j];
+            sy[i] = wy[j];
+            st[i] = wt[j];
+        }
     }
     __syncthreads();
-    const WSrc src{&g, sx, sy, st, wlo, whi};
-    const int t = (int)threadIdx.x;
-    // > 8 in-edges: one wavefront per node (each wave's stage region is its own 4 KB)
-    for (int i = t / 64, v = node_lo + n0 + nb1 + nb2; i < nb3; i += WBLOCK / 64) {
-        pkl_node_body<T, 64, STATES>(g, o, src, v + i, t & 63, (KlStage<T, 64>*)stage + t / 64);
-        gtf::wave_lds_sync();
+    if (!mine) return;
+    const WSrc src{&g, sx, sy, st, wlo, wlo + wn};
+    pkl_b0_body<T, STATES>(g, o, src, node_lo + t, two, l, pair_lo + (t - n1), u0, u1);
+}
+
+template <typename T, bool STATES>
+__global__ void __launch_bounds__(WBLOCK) __attribute__((amdgpu_waves_per_eu(GTF_KL_WIN_WAVES)))
+k_parabolic_kl_win(gtf_kl_graph g, gtf_kl_out o, WinBuckets bk) {
+    __shared__ __attribute__((aligned(16))) char lds[win_lds_bytes(sizeof(T))];
+    int b = blockIdx.x;
+    const int sub = (int)threadIdx.x / BLOCK, tid = (int)threadIdx.x % BLOCK;
+    char* stage = lds + sub * sub_stage_bytes(sizeof(T));
+    if (b < bk.blocks[3]) {   // > 8 in-edges: a wavefront per node (longest-running first)
+        pkl_node<T, 64, STATES>(g, o, g.list[3], g.count[3], gtf::xcd_local(b, bk.blocks[3]) * SUBS + sub, stage, 0, tid);
+        return;
     }
-    // 5..8: 8 lanes per node (the groups of a wave use that wave's 4 KB as well)
-    for (int i = t / 8, v = node_lo + n0 + nb1; i < nb2; i += WBLOCK / 8) {
-        pkl_node_body<T, 8, STATES>(g, o, src, v + i, t & 7, (KlStage<T, 8>*)stage + t / 8);
-        gtf::wave_lds_sync();
+    b -= bk.blocks[3];
+    if (b < bk.blocks[2]) {
+        pkl_node<T, 8, STATES>(g, o, g.list[2], g.count[2], gtf::xcd_local(b, bk.blocks[2]) * SUBS + sub, stage, 0, tid);
+        return;
     }
-    // 3..4: one thread per node
-    for (int i = t, v = node_lo + n0; i < nb1; i += WBLOCK) pkl_node4_body<T, STATES>(g, o, src, v + i);
-    // one and two in-edges: one thread per node, slots and pair by arithmetic
-    for (int i = t; i < n0; i += WBLOCK) {
-        const bool two = i >= n1;
-        pkl_b0_body<T, STATES>(g, o, src, node_lo + i, two, slot_lo + (two ? n1 + 2 * (int64_t)(i - n1) : i),
-                               pair_lo + (i - n1));
+    b -= bk.blocks[2];
+    if (b < bk.blocks[1]) {
+        pkl_node4<T, STATES>(g, o, g.list[1], g.count[1], gtf::xcd_local(b, bk.blocks[1]) * SUBS + sub, 0, tid);
+        return;
     }
+    b -= bk.blocks[1];
+    const int tile = gtf::xcd_local(b, bk.blocks[0]);
+    if (tile >= g.n_blk) return;   // (block-uniform: the padding to 8)
+    pkl_tile<T, STATES>(g, o, tile, lds);
 }
 
 template <typename T>
 int launch(const gtf_kl_graph* g, const gtf_kl_out* o, hipStream_t st) {
-    if (g->blk) {   // tiled layout: one block per tile record
-        if (g->n_blk > 0) {
+    if (g->blk) {   // tiled layout: one block per tile record, buckets 1..3 by list
+        WinBuckets wb;
+        wb.blocks[0] = gtf::pad8(g->n_blk);
+        int total = wb.blocks[0];
+        for (int i = 1; i < 4; i++) {
+            const int per_block = i == 1 ? WBLOCK : WBLOCK / BG[i];   // nodes per 256-thread block
+            wb.blocks[i] = gtf::pad8((g->count[i] + per_block - 1) / per_block);
+            total += wb.blocks[i];
+        }
+        if (g->n_blk == 0) total -= wb.blocks[0], wb.blocks[0] = 0;
+        if (total > 0) {
             if (o->sv || o->cov)
-                hipLaunchKernelGGL((k_parabolic_kl_win<T, true>), dim3(g->n_blk), dim3(WBLOCK), 0, st, *g, *o);
+                hipLaunchKernelGGL((k_parabolic_kl_win<T, true>), dim3(total), dim3(WBLOCK), 0, st, *g, *o, wb);
             else
-                hipLaunchKernelGGL((k_parabolic_kl_win<T, false>), dim3(g->n_blk), dim3(WBLOCK), 0, st, *g, *o);
+                hipLaunchKernelGGL((k_parabolic_kl_win<T, false>), dim3(total), dim3(WBLOCK), 0, st, *g, *o, wb);
         }
         const hipError_t e = hipGetLastError();
         if (e != hipSuccess) {
@@ -668,8 +720,8 @@ extern "C" int gtf_parabolic_kl(const gtf_kl_graph* g, int32_t dtype, const gtf_
     if (g->n_nodes < 0 || g->n_slots < 0) { gtf::set_error("gtf_parabolic_kl: negative sizes"); return -2; }
     if (g->blk && g->n_blk < 0) { gtf::set_error("gtf_parabolic_kl: bad block table"); return -2; }
     int listed = 0;
-    const bool ordered = !g->list[0] && !g->list[1] && !g->list[2] && !g->list[3];
-    for (int i = 0; i < 4; i++) {
+    const bool ordered = !g->blk && !g->list[0] && !g->list[1] && !g->list[2] && !g->list[3];
+    for (int i = g->blk ? 1 : 0; i < 4; i++) {
         if (g->count[i] < 0 || (g->count[i] > 0 && !g->list[i] && !ordered)) {
             gtf::set_error("gtf_parabolic_kl: bad node list");
             return -2;

@@ -27,7 +27,9 @@ from . import _native as nat
 from .graph import TrackGraph
 
 BUCKETS = ((1, 2), (3, 4), (5, 8), (9, 1 << 30))   # in-degree ranges of the 1/4/8/64-lane groups
-TILE_MAX = 256   # nodes per tile of the tiled layout (gtf_kl.hip WTILE)
+TILE_MAX = 256   # bucket-0 nodes per tile of the tiled layout (one per thread of a gtf_kl.hip WBLOCK)
+WIN_NODES = 1024   # LDS window of a tile (gtf_kl.hip WWIN)
+WIN_MARGIN = 128   # window nodes either side of a tile (99 % of the vol-7 neighbours lie within 73)
 
 
 def _ptr(t):
@@ -57,11 +59,12 @@ class ParabolicKL:
     caller's node ids, and ``host_nodes`` / ``host_slots`` reorder per-node / per-slot
     outputs; pairs keep the caller's (node, i, j) rows through pair_index().
 
-    tile = T > 0: the same bucket order inside every tile of T consecutive nodes (an event
-    of a batch, or part of one) instead of over the whole batch, with one block record per
-    wavefront (gtf_kl_graph.blk): a node's neighbours are hits of its own event, so they sit
-    in its own tile and the neighbour gathers find the lines the tile's own reads brought
-    into L2, instead of reaching across the whole batch."""
+    tile = T > 0 (T <= 256): the nodes azimuth-sorted inside sort windows (an event of a
+    batch), then cut into tiles of T one- / two-edge (bucket-0) nodes and whatever lies
+    between them, each tile with its bucket-0 nodes first: one 256-thread block per tile
+    record (gtf_kl_graph.blk) loads its nodes' sender lists and the coordinates of a window
+    of consecutive nodes around the tile -- where a hit's neighbours lie -- in one round,
+    and reads the neighbours from LDS. The 3..4, 5..8 and > 8 buckets go by node list."""
 
     def __init__(self, slot_ptr, slot_src, gnn, truth=None, device="cuda", with_single=False, ordered=False,
                  tile=0, sort_window=8192):
@@ -80,15 +83,16 @@ class ParabolicKL:
             rank = np.full(d.size, len(keys), np.int64)
             for q in reversed(range(len(keys))):
                 rank[keys[q]] = q
-            if self.tile > 0:   # azimuth order in sort windows, cut into tiles, buckets inside a tile
+            if self.tile > 0:   # azimuth order in sort windows, cut into tiles of T bucket-0 nodes
                 if not 0 < self.tile <= TILE_MAX:
                     raise ValueError("tile must be in 1..%d" % TILE_MAX)
                 xy = np.asarray(gnn, np.float64).reshape(-1, 4)
                 phi = np.arctan2(xy[:, 1], xy[:, 0])
                 idx = np.arange(d.size, dtype=np.int64)
                 o1 = np.lexsort((idx, phi, idx // sort_window))
+                b0 = rank[o1] < 2                                   # one- and two-edge nodes
                 tid = np.empty(d.size, np.int64)
-                tid[o1] = np.arange(d.size) // self.tile
+                tid[o1] = (np.cumsum(b0) - b0) // self.tile         # a tile: T bucket-0 nodes and the rest between
                 order = np.lexsort((np.argsort(o1), rank, tid))
                 self._tiles = (tid[order], rank[order])
             else:
@@ -128,14 +132,16 @@ class ParabolicKL:
         self.lists = [t(x) for x in lists]
         self.device = dev
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)
-        if self.tile > 0:   # one block record per wavefront (gtf_kl_graph.blk)
+        if self.tile > 0:   # one block record per tile (gtf_kl_graph.blk); buckets 1..3 by list
             blk = self._block_table(d, pair_ptr)
             self.blk = t(blk)
             self.n_blk = int(blk.size // 12)
             self._g = nat.GtfKlGraph(self.n_nodes, self.n_slots, _ptr(self.slot_ptr), _ptr(self.slot_src),
                                      _ptr(self.gnn), _ptr(self.truth), _ptr(self.pair_ptr),
-                                     (ctypes.c_void_p * 4)(), (ctypes.c_int32 * 4)(), (ctypes.c_int32 * 4)(), 0, 2,
-                                     0, 0, _ptr(self.blk), self.n_blk)
+                                     (ctypes.c_void_p * 4)(None, *[x.data_ptr() if x.numel() else None
+                                                                   for x in self.lists[1:]]),
+                                     (ctypes.c_int32 * 4)(0, *[x.numel() for x in self.lists[1:]]),
+                                     (ctypes.c_int32 * 4)(), 0, 2, 0, 0, _ptr(self.blk), self.n_blk)
         elif ordered:   # bucket ranges, no lists
             n1, n2 = self._ranges[0], self._ranges[1]
             counts = [n1 + n2] + [int(x.size) for x in lists[1:]]
@@ -150,22 +156,26 @@ class ParabolicKL:
                                      (ctypes.c_void_p * 4)(*[x.data_ptr() if x.numel() else None for x in self.lists]),
                                      (ctypes.c_int32 * 4)(*[x.numel() for x in self.lists]), gnn_stride=2)
 
-    def _block_table(self, d, pair_ptr):
+    def _block_table(self, d, pair_ptr, margin=WIN_MARGIN):
         """gtf_kl_graph.blk of the tiled layout: one record of 12 int32 per tile (first node,
-        bucket-0 count, its one-edge count, bucket 1 / 2 / 3 counts, bucket 0's first slot,
-        its first pair lo / hi, the window [previous tile's first node, next tile's end), 0)"""
+        bucket-0 count, its one-edge count, 0, 0, 0, bucket 0's first slot, its first pair
+        lo / hi, the window [lo, hi) -- the tile's nodes and `margin` nodes either side, at
+        most WIN_NODES -- 0)"""
         tid, rank = self._tiles
         sp = self.slot_ptr_host
-        nt = int(tid.max()) + 1 if tid.size else 0
+        n = tid.size
+        nt = int(tid.max()) + 1 if n else 0
         bounds = np.searchsorted(tid, np.arange(nt + 1))
-        recs = np.zeros((nt, 12), np.int64)
-        for t_ in range(nt):
-            a, b = int(bounds[t_]), int(bounds[t_ + 1])
-            cut = a + np.searchsorted(rank[a:b], np.arange(6))      # rank runs inside the tile
-            n1, n0 = int(cut[1] - cut[0]), int(cut[2] - cut[0])
-            pr = int(pair_ptr[a + n1]) if n1 < n0 else 0
-            recs[t_] = (a, n0, n1, cut[3] - cut[2], cut[4] - cut[3], cut[5] - cut[4], sp[a],
-                        pr & 0xFFFFFFFF, pr >> 32, bounds[max(t_ - 1, 0)], bounds[min(t_ + 2, nt)], 0)
+        a, b = bounds[:-1], bounds[1:]
+        n1 = np.searchsorted(tid * 8 + rank, tid[a] * 8 + 1) - a if nt else a   # rank-0 run at the tile head
+        n0 = np.searchsorted(tid * 8 + rank, tid[a] * 8 + 2) - a if nt else a
+        pr = np.where(n1 < n0, pair_ptr[np.minimum(a + n1, n)], 0)
+        span = b - a
+        m = np.clip((WIN_NODES - span) // 2, 0, margin)
+        wlo = np.maximum(a - m, 0)
+        whi = np.minimum(np.minimum(b + m, n), wlo + WIN_NODES)
+        z = np.zeros(nt, np.int64)
+        recs = np.stack([a, n0, n1, z, z, z, sp[a], pr & 0xFFFFFFFF, pr >> 32, wlo, whi, z], 1)
         recs = np.where(recs >= 2**31, recs - 2**32, recs)   # low words as int32 bits
         return recs.astype(np.int32).reshape(-1)
 

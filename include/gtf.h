@@ -556,13 +556,14 @@ typedef struct gtf_kl_graph {
                                  the kernel reads only x and y, so half the gathered bytes) */
     int64_t slot0;
     int64_t pair0;
-    /* tiled layout (gtf.parabolic.ParabolicKL(tile=T)): the nodes in tiles of <= 256 consecutive
-     * nodes cut from an azimuth-sorted order, each tile ordered by bucket (one- then two-edge,
-     * 3..4, 5..8, > 8 in-edges, then the unlisted nodes). One block per tile record of 12 int32:
-     * (first node, bucket-0 count, its one-edge count, bucket 1 / 2 / 3 counts, bucket 0's first
-     * slot, its first pair low / high 32 bits, window [lo, hi) of at most 768 nodes holding the
-     * tile's neighbours, 0); the block copies the window's x, y and truth ids into LDS and reads
-     * the neighbours there. blk != NULL overrides list / first / count. */
+    /* tiled layout (gtf.parabolic.ParabolicKL(tile=T)): the nodes azimuth-sorted per event and
+     * cut into tiles of <= 256 one- / two-edge (bucket-0) nodes and the nodes between them, bucket
+     * 0 first inside a tile (one-edge, then two-edge nodes, consecutive slots and one pair each).
+     * One 256-thread block per tile record of 12 int32: (first node, bucket-0 count, its one-edge
+     * count, 0, 0, 0, bucket 0's first slot, its first pair low / high 32 bits, window [lo, hi) of
+     * at most 1024 consecutive nodes holding the tile's neighbours, 0); the block loads its
+     * sender lists and the window's x, y and truth ids in one round and reads the neighbours from
+     * LDS. Buckets 1..3 come from list[1..3] / count[1..3] (count[0] and list[0] are ignored). */
     const int32_t* blk;       /* [12 * n_blk] or NULL */
     int32_t n_blk;
     int32_t pad_blk_;

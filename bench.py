@@ -224,11 +224,14 @@ def bench_c5(dev, steps, warmup, n_events=256, n_batches=8, hot=True, dtypes=("f
     if kl_tile is None:
         kl_tile = int(os.environ.get("GTF_KL_TILE", "0"))   # 0: the ordered layout (the tiled one measured no faster)
     # tiled: azimuth-sorted per event (sort window = one event's nodes), then tiles
-    k = parabolic.ParabolicKL(ptr, src, gnn, tr, dev, ordered=True, tile=kl_tile, sort_window=ptr0.size - 1)
+    tile_b1 = os.environ.get("GTF_KL_TILE_B1", "1") != "0"   # tiled: the 3- / 4-edge nodes in the tiles too
+    k = parabolic.ParabolicKL(ptr, src, gnn, tr, dev, ordered=True, tile=kl_tile, sort_window=ptr0.size - 1,
+                              tile_b1=tile_b1)
     ks = [k] + [k.replica(gnn=parabolic.batch(ptr0, src0, g.node["gnn"], truth, n_events, seed=e)[2])
                 for e in range(1, n_batches)]
     res = {"workload": "%d x committed vol-7 134 event (jittered copies)" % n_events, "nodes": k.n_nodes,
-           "layout": "tiled, %d nodes per tile" % kl_tile if kl_tile else "ordered (bucket ranges over the batch)",
+           "layout": ("tiled, %d %s nodes per tile, LDS window" % (kl_tile, "1..4-edge" if tile_b1 else "1..2-edge")
+                      if kl_tile else "ordered (bucket ranges over the batch)"),
            "in_edges": k.n_slots, "pairs": k.n_pairs, "listed_nodes": k.n_listed, "batches_rotated": n_batches}
     outs = {}
     launches = max(steps, 2 * n_batches) // n_batches * n_batches

@@ -451,16 +451,12 @@ __device__ __forceinline__ void pkl_node1(const gtf_kl_graph& g, const gtf_kl_ou
 #ifndef GTF_KL_B1_LANES
 #define GTF_KL_B1_LANES 0
 #endif
+// node v with d in 1..4 in-edges from slot lo (senders u[0..d)) and pairs from base
 template <typename T, bool STATES, typename S>
-__device__ __forceinline__ void pkl_node4_body(const gtf_kl_graph& g, const gtf_kl_out& o, const S& src, int v) {
-    const int lo = g.slot_ptr[v], d = g.slot_ptr[v + 1] - lo;
-    const int64_t base = g.pair_ptr[v];
+__device__ __forceinline__ void pkl_node4_core(const gtf_kl_graph& g, const gtf_kl_out& o, const S& src, int v, int lo,
+                                               int d, int64_t base, const int (&u)[4]) {
     const double xv = src.x(v), yv = src.y(v);
     const long long tv = (o.truth && g.truth) ? src.t(v) : 0;
-    if (d < 1 || d > 4) return;
-    int u[4];
-#pragma unroll
-    for (int q = 0; q < 4; q++) u[q] = q < d ? g.slot_src[lo + q] : 0;
     double xb[4], yb[4];
     long long tu[4];
 #pragma unroll
@@ -508,6 +504,17 @@ __device__ __forceinline__ void pkl_node4_body(const gtf_kl_graph& g, const gtf_
                 if (o.truth) st_out(o.truth + (base + t), (int8_t)(tv == tu[i] && tu[i] == tu[j] && tv == tu[j]));
                 t++;
             }
+}
+
+template <typename T, bool STATES, typename S>
+__device__ __forceinline__ void pkl_node4_body(const gtf_kl_graph& g, const gtf_kl_out& o, const S& src, int v) {
+    const int lo = g.slot_ptr[v], d = g.slot_ptr[v + 1] - lo;
+    const int64_t base = g.pair_ptr[v];
+    if (d < 1 || d > 4) return;
+    int u[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) u[q] = q < d ? g.slot_src[lo + q] : 0;
+    pkl_node4_core<T, STATES>(g, o, src, v, lo, d, base, u);
 }
 
 template <typename T, bool STATES>
@@ -599,7 +606,7 @@ __device__ __forceinline__ void pkl_tile(const gtf_kl_graph& g, const gtf_kl_out
     double* sy = sx + WWIN;
     long long* st = (long long*)(sy + WWIN);
     const int32_t* r = g.blk + 12 * (int64_t)tile;
-    const int node_lo = r[0], n0 = r[1], n1 = r[2];
+    const int node_lo = r[0], n0 = r[1], n1 = r[2], n3 = r[3], n4 = r[4];
     const int64_t slot_lo = (int64_t)(uint32_t)r[6];
     const int64_t pair_lo = (int64_t)(uint32_t)r[7] | ((int64_t)r[8] << 32);
     const int wlo = r[9], wn = min(r[10], r[9] + WWIN) - r[9];
@@ -611,6 +618,18 @@ __device__ __forceinline__ void pkl_tile(const gtf_kl_graph& g, const gtf_kl_out
     if (mine) {
         u0 = ld_list(g.slot_src + l);
         u1 = two ? ld_list(g.slot_src + l + 1) : u0;
+    }
+    // threads n0 .. n0 + n3 + n4: the tile's three-, then four-edge nodes (tile_b1), their
+    // slots and pairs by arithmetic after bucket 0's
+    const int i4 = t - n0;
+    const bool mine4 = i4 >= 0 && i4 < n3 + n4;
+    const int d4 = i4 < n3 ? 3 : 4;
+    const int64_t l4 = slot_lo + n1 + 2 * (int64_t)(n0 - n1) + (i4 < n3 ? 3 * (int64_t)i4 : 3 * (int64_t)n3 + 4 * (int64_t)(i4 - n3));
+    const int64_t p4 = pair_lo + (n0 - n1) + (i4 < n3 ? 3 * (int64_t)i4 : 3 * (int64_t)n3 + 6 * (int64_t)(i4 - n3));
+    int u4[4] = {0, 0, 0, 0};
+    if (mine4) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) u4[q] = q < d4 ? ld_list(g.slot_src + l4 + q) : 0;
     }
     double wx[WPT], wy[WPT];
     long long wt[WPT];
@@ -633,9 +652,9 @@ __device__ __forceinline__ void pkl_tile(const gtf_kl_graph& g, const gtf_kl_out
         }
     }
     __syncthreads();
-    if (!mine) return;
     const WSrc src{&g, sx, sy, st, wlo, wlo + wn};
-    pkl_b0_body<T, STATES>(g, o, src, node_lo + t, two, l, pair_lo + (t - n1), u0, u1);
+    if (mine) pkl_b0_body<T, STATES>(g, o, src, node_lo + t, two, l, pair_lo + (t - n1), u0, u1);
+    else if (mine4) pkl_node4_core<T, STATES>(g, o, src, node_lo + t, (int)l4, d4, p4, u4);
 }
 
 template <typename T, bool STATES>

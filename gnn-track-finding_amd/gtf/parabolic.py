@@ -67,7 +67,7 @@ class ParabolicKL:
     and reads the neighbours from LDS. The 3..4, 5..8 and > 8 buckets go by node list."""
 
     def __init__(self, slot_ptr, slot_src, gnn, truth=None, device="cuda", with_single=False, ordered=False,
-                 tile=0, sort_window=8192):
+                 tile=0, sort_window=8192, tile_b1=True):
         slot_ptr = np.ascontiguousarray(slot_ptr, np.int32)
         self.n_nodes = int(slot_ptr.shape[0] - 1)
         self.n_slots = int(slot_ptr[-1])
@@ -78,8 +78,8 @@ class ParabolicKL:
         ordered = ordered or self.tile > 0
         if ordered:
             sp = slot_ptr.astype(np.int64)
-            keys = [d == 1 if lo == 1 else np.zeros(d.size, bool), d == 2] + \
-                   [(d >= a) & (d <= b) for a, b in BUCKETS[1:]]
+            keys = [d == 1 if lo == 1 else np.zeros(d.size, bool), d == 2, d == 3, d == 4] + \
+                   [(d >= a) & (d <= b) for a, b in BUCKETS[2:]]   # (bucket 1 as its 3- then 4-edge nodes)
             rank = np.full(d.size, len(keys), np.int64)
             for q in reversed(range(len(keys))):
                 rank[keys[q]] = q
@@ -90,9 +90,10 @@ class ParabolicKL:
                 phi = np.arctan2(xy[:, 1], xy[:, 0])
                 idx = np.arange(d.size, dtype=np.int64)
                 o1 = np.lexsort((idx, phi, idx // sort_window))
-                b0 = rank[o1] < 2                                   # one- and two-edge nodes
+                self.tile_b1 = bool(tile_b1)
+                b0 = rank[o1] < (4 if self.tile_b1 else 2)          # the nodes a tile's threads take
                 tid = np.empty(d.size, np.int64)
-                tid[o1] = (np.cumsum(b0) - b0) // self.tile         # a tile: T bucket-0 nodes and the rest between
+                tid[o1] = (np.cumsum(b0) - b0) // self.tile         # a tile: T such nodes and the rest between
                 order = np.lexsort((np.argsort(o1), rank, tid))
                 self._tiles = (tid[order], rank[order])
             else:
@@ -136,11 +137,12 @@ class ParabolicKL:
             blk = self._block_table(d, pair_ptr)
             self.blk = t(blk)
             self.n_blk = int(blk.size // 12)
+            by_list = [q >= (2 if self.tile_b1 else 1) and self.lists[q].numel() > 0 for q in range(4)]
             self._g = nat.GtfKlGraph(self.n_nodes, self.n_slots, _ptr(self.slot_ptr), _ptr(self.slot_src),
                                      _ptr(self.gnn), _ptr(self.truth), _ptr(self.pair_ptr),
-                                     (ctypes.c_void_p * 4)(None, *[x.data_ptr() if x.numel() else None
-                                                                   for x in self.lists[1:]]),
-                                     (ctypes.c_int32 * 4)(0, *[x.numel() for x in self.lists[1:]]),
+                                     (ctypes.c_void_p * 4)(*[x.data_ptr() if b else None
+                                                             for x, b in zip(self.lists, by_list)]),
+                                     (ctypes.c_int32 * 4)(*[x.numel() if b else 0 for x, b in zip(self.lists, by_list)]),
                                      (ctypes.c_int32 * 4)(), 0, 2, 0, 0, _ptr(self.blk), self.n_blk)
         elif ordered:   # bucket ranges, no lists
             n1, n2 = self._ranges[0], self._ranges[1]
@@ -158,9 +160,9 @@ class ParabolicKL:
 
     def _block_table(self, d, pair_ptr, margin=WIN_MARGIN):
         """gtf_kl_graph.blk of the tiled layout: one record of 12 int32 per tile (first node,
-        bucket-0 count, its one-edge count, 0, 0, 0, bucket 0's first slot, its first pair
-        lo / hi, the window [lo, hi) -- the tile's nodes and `margin` nodes either side, at
-        most WIN_NODES -- 0)"""
+        bucket-0 count, its one-edge count, the three- and four-edge counts that follow (0 and
+        0 unless tile_b1), 0, bucket 0's first slot, its first pair lo / hi, the window
+        [lo, hi) -- the tile's nodes and `margin` nodes either side, at most WIN_NODES -- 0)"""
         tid, rank = self._tiles
         sp = self.slot_ptr_host
         n = tid.size
@@ -169,13 +171,17 @@ class ParabolicKL:
         a, b = bounds[:-1], bounds[1:]
         n1 = np.searchsorted(tid * 8 + rank, tid[a] * 8 + 1) - a if nt else a   # rank-0 run at the tile head
         n0 = np.searchsorted(tid * 8 + rank, tid[a] * 8 + 2) - a if nt else a
-        pr = np.where(n1 < n0, pair_ptr[np.minimum(a + n1, n)], 0)
+        z = np.zeros(nt, np.int64)
+        n3 = n4 = z
+        if self.tile_b1 and nt:
+            n3 = np.searchsorted(tid * 8 + rank, tid[a] * 8 + 3) - a - n0
+            n4 = np.searchsorted(tid * 8 + rank, tid[a] * 8 + 4) - a - n0 - n3
+        pr = pair_ptr[a]   # (one-edge nodes have no pairs: the first two-edge node's, then the 3- / 4-edge nodes')
         span = b - a
         m = np.clip((WIN_NODES - span) // 2, 0, margin)
         wlo = np.maximum(a - m, 0)
         whi = np.minimum(np.minimum(b + m, n), wlo + WIN_NODES)
-        z = np.zeros(nt, np.int64)
-        recs = np.stack([a, n0, n1, z, z, z, sp[a], pr & 0xFFFFFFFF, pr >> 32, wlo, whi, z], 1)
+        recs = np.stack([a, n0, n1, n3, n4, z, sp[a], pr & 0xFFFFFFFF, pr >> 32, wlo, whi, z], 1)
         recs = np.where(recs >= 2**31, recs - 2**32, recs)   # low words as int32 bits
         return recs.astype(np.int32).reshape(-1)
 

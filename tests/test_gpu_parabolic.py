@@ -196,14 +196,15 @@ def test_gpu_beyond_lds_recompute_path():
     assert _rel(kl, ref).max() < 1e-6
 
 
-@pytest.mark.parametrize("tile", [0, 256, 100])
+@pytest.mark.parametrize("tile", [0, 256, 100, -256])
 @pytest.mark.parametrize("with_single", [False, True])
 def test_gpu_ordered_layout_equals_lists(with_single, tile):
     """ParabolicKL(ordered=True) (bucket node ranges, the two-edge bucket by arithmetic) and
-    ParabolicKL(tile=T) (the same inside tiles of T nodes, one block record per wavefront:
-    T = one event, and tiles that cut events) give the list layout's pair rows, truth
-    flags, gradient moments and states bit for bit once mapped back to the caller's order
-    (16 jittered copies of the vol-7 event)"""
+    ParabolicKL(tile=T) (tiles of T one- to four-edge nodes with their LDS windows, one
+    256-thread block each, the larger buckets by list; -T: tiles of T one- / two-edge nodes,
+    the 3- / 4-edge bucket by list too) give the list layout's pair rows, truth flags,
+    gradient moments and states bit for bit once mapped back to the caller's order (16
+    jittered copies of the vol-7 event)"""
     from gtf import io, parabolic
     kat = os.path.join(GOLDEN, "kat134")
     g = io.load_event(os.path.join(kat, "event_1_filtered_graph_"), 7, 7)
@@ -213,7 +214,7 @@ def test_gpu_ordered_layout_equals_lists(with_single, tile):
     res = []
     for ordered in (False, True):
         k = parabolic.ParabolicKL(ptr, src, gnn, tr, with_single=with_single, ordered=ordered,
-                                  tile=tile if ordered else 0)
+                                  tile=abs(tile) if ordered else 0, tile_b1=tile > 0)
         out = k.run(k.alloc("f64", emp=True, states=with_single), "f64")
         node, i, j = k.pair_index()
         key = np.lexsort((j, i, node))

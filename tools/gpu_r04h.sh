@@ -13,6 +13,7 @@ for i in 1 2; do
   for t in 0 256 128; do
     GTF_KL_TILE=$t timeout -k 10 120 python tools/pkl_time.py 48 >> $O/kl_ab.jsonl || exit 1
   done
+  GTF_KL_TILE_B1=0 GTF_KL_TILE=256 timeout -k 10 120 python tools/pkl_time.py 48 >> $O/kl_ab.jsonl || exit 1
   for v in klw4 klw768; do
     GTF_LIB=$L/libgtf_$v.so GTF_KL_TILE=256 timeout -k 10 120 python tools/pkl_time.py 48 >> $O/kl_ab.jsonl || exit 1
   done

@@ -229,6 +229,12 @@ def bench_c5(dev, steps, warmup, n_events=256, n_batches=8, hot=True, dtypes=("f
                               tile_b1=tile_b1)
     ks = [k] + [k.replica(gnn=parabolic.batch(ptr0, src0, g.node["gnn"], truth, n_events, seed=e)[2])
                 for e in range(1, n_batches)]
+    keep = os.environ.get("GTF_KL_KEEP")   # diagnostics: launch only these buckets ("0", "123", ...)
+    if keep is not None:
+        for kk in ks:
+            for q in range(4):
+                if str(q) not in keep:
+                    kk._g.count[q] = 0
     res = {"workload": "%d x committed vol-7 134 event (jittered copies)" % n_events, "nodes": k.n_nodes,
            "layout": ("tiled, %d %s nodes per tile, LDS window" % (kl_tile, "1..4-edge" if tile_b1 else "1..2-edge")
                       if kl_tile else "ordered (bucket ranges over the batch)"),

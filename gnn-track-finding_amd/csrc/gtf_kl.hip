@@ -311,39 +311,86 @@ constexpr int NPT = GTF_KL_NPT;
 
 // ordered layout (gtf_kl_graph.first / n_d1 / slot0 / pair0): node, slots and pair of
 // bucket-0 entry gi by arithmetic, so the node's own fields and its in-edges' senders are
-// one round of independent loads and the senders' coordinates the second
+// one round of independent loads and the senders' coordinates the second. A thread takes
+// NPT_ORD entries (gi = (bid * NPT_ORD + j) * BLOCK + lane), their loads issued round by
+// round, so NPT_ORD gather chains per lane are in flight at once.
+#ifndef GTF_KL_NPT_ORD
+#define GTF_KL_NPT_ORD 1
+#endif
+constexpr int NPT_ORD = GTF_KL_NPT_ORD;
+struct B0Node {
+    int v, u0, u1;
+    bool ok, two;
+    int64_t l, pp;
+    double xv, yv, x0, y0, x1, y1;
+    long long tv, t0, t1;
+};
+
+template <typename T, bool STATES>
+__device__ __forceinline__ void pkl_b0_finish(const gtf_kl_out& o, const B0Node& n) {
+    const Frame f = node_frame_xy(n.xv, n.yv);
+    bool s0, s1 = false;
+    const PState<T> a = pstate<T>(f, n.x0, n.y0, s0, STATES ? o.sv + 3 * n.l : nullptr, STATES ? o.cov + 9 * n.l : nullptr);
+    PState<T> b = a;
+    if (n.two)
+        b = pstate<T>(f, n.x1, n.y1, s1, STATES ? o.sv + 3 * (n.l + 1) : nullptr, STATES ? o.cov + 9 * (n.l + 1) : nullptr);
+    if ((s0 || s1) && o.err) atomicOr(o.err, (uint32_t)GTF_ERR_SINGULAR_H);
+    const double g0 = (f.y - n.y0) / (f.x - n.x0);
+    const double g1 = n.two ? (f.y - n.y1) / (f.x - n.x1) : g0;
+    // / 2 and / 1 as exact scalings
+    const double mean = n.two ? (g0 + g1) * 0.5 : g0;
+    if (o.emp_var)
+        st_out(o.emp_var + (n.v), (double)(n.two ? ((g0 - mean) * (g0 - mean) + (g1 - mean) * (g1 - mean)) * 0.5
+                                                 : 0.0 * (g0 - mean)));
+    if (o.emp_mean) st_out(o.emp_mean + (n.v), (double)(mean));
+    if (n.two) {
+        st_out((T*)o.kl + (n.pp), (T)(pkl<T>(b, a)));   // pair (i, j) = (1, 0)
+        if (o.truth) st_out(o.truth + (n.pp), (int8_t)(n.tv == n.t1 && n.t1 == n.t0 && n.tv == n.t0));
+    }
+}
+
 template <typename T, bool STATES>
 __device__ __forceinline__ void pkl_node1_ordered(const gtf_kl_graph& g, const gtf_kl_out& o, int bid) {
-    const int gi = bid * BLOCK + (int)threadIdx.x;
-    if (gi >= g.count[0]) return;
-    const int v = g.first[0] + gi;
-    const bool two = gi >= g.n_d1;
-    const int64_t l = g.slot0 + (two ? g.n_d1 + 2 * (int64_t)(gi - g.n_d1) : gi);
-    const int64_t pp = g.pair0 + (gi - g.n_d1);
-    const double xv = ld_own(g.gnn + gnn_row(g, v)), yv = ld_own(g.gnn + gnn_row(g, v) + 1);
-    const long long tv = (o.truth && g.truth) ? ld_own(g.truth + v) : 0;
-    const int u0 = ld_list(g.slot_src + l);
-    const int u1 = two ? ld_list(g.slot_src + l + 1) : u0;
-    const double x0 = gx(g, u0), y0 = gy(g, u0);
-    const double x1 = gx(g, u1), y1 = gy(g, u1);
-    long long t0 = 0, t1 = 0;
-    if (o.truth && g.truth) { t0 = g.truth[u0]; t1 = g.truth[u1]; }
-    const Frame f = node_frame_xy(xv, yv);
-    bool s0, s1 = false;
-    const PState<T> a = pstate<T>(f, x0, y0, s0, STATES ? o.sv + 3 * l : nullptr, STATES ? o.cov + 9 * l : nullptr);
-    PState<T> b = a;
-    if (two) b = pstate<T>(f, x1, y1, s1, STATES ? o.sv + 3 * (l + 1) : nullptr, STATES ? o.cov + 9 * (l + 1) : nullptr);
-    if ((s0 || s1) && o.err) atomicOr(o.err, (uint32_t)GTF_ERR_SINGULAR_H);
-    const double g0 = (f.y - y0) / (f.x - x0);
-    const double g1 = two ? (f.y - y1) / (f.x - x1) : g0;
-    // / 2 and / 1 as exact scalings
-    const double mean = two ? (g0 + g1) * 0.5 : g0;
-    if (o.emp_var) st_out(o.emp_var + (v), (double)(two ? ((g0 - mean) * (g0 - mean) + (g1 - mean) * (g1 - mean)) * 0.5 : 0.0 * (g0 - mean)));
-    if (o.emp_mean) st_out(o.emp_mean + (v), (double)(mean));
-    if (two) {
-        st_out((T*)o.kl + (pp), (T)(pkl<T>(b, a)));   // pair (i, j) = (1, 0)
-        if (o.truth) st_out(o.truth + (pp), (int8_t)(tv == t1 && t1 == t0 && tv == t0));
+    B0Node n[NPT_ORD];
+    const bool tr = o.truth && g.truth;
+#pragma unroll
+    for (int j = 0; j < NPT_ORD; j++) {   // round 1: own fields and sender lists
+        const int gi = (bid * NPT_ORD + j) * BLOCK + (int)threadIdx.x;
+        n[j].ok = gi < g.count[0];
+        if (!n[j].ok) continue;
+        n[j].v = g.first[0] + gi;
+        n[j].two = gi >= g.n_d1;
+        n[j].l = g.slot0 + (n[j].two ? g.n_d1 + 2 * (int64_t)(gi - g.n_d1) : gi);
+        n[j].pp = g.pair0 + (gi - g.n_d1);
+        n[j].xv = ld_own(g.gnn + gnn_row(g, n[j].v));
+        n[j].yv = ld_own(g.gnn + gnn_row(g, n[j].v) + 1);
+        n[j].tv = tr ? ld_own(g.truth + n[j].v) : 0;
+        n[j].u0 = ld_list(g.slot_src + n[j].l);
+        n[j].u1 = n[j].two ? ld_list(g.slot_src + n[j].l + 1) : n[j].u0;
     }
+#pragma unroll
+    for (int j = 0; j < NPT_ORD; j++) {   // round 2: the senders' coordinates
+        if (!n[j].ok) continue;
+#ifdef GTF_KL_DIAG_NODEP   // diagnostics (wrong results): neighbours v -+ 1, no dependent round
+        const int w0 = max(n[j].v - 1, 0), w1 = min(n[j].v + 1, g.n_nodes - 1);
+#else
+        const int w0 = n[j].u0, w1 = n[j].u1;
+#endif
+        n[j].x0 = gx(g, w0);
+        n[j].y0 = gy(g, w0);
+        n[j].x1 = gx(g, w1);
+        n[j].y1 = gy(g, w1);
+        n[j].t0 = tr ? g.truth[w0] : 0;
+        n[j].t1 = tr ? g.truth[w1] : 0;
+    }
+#pragma unroll
+    for (int j = 0; j < NPT_ORD; j++)
+        if (n[j].ok) {
+            pkl_b0_finish<T, STATES>(o, n[j]);
+#ifdef GTF_KL_DIAG_NODEP
+            asm volatile("" ::"v"(n[j].u0), "v"(n[j].u1));   // (the sender-list loads stay)
+#endif
+        }
 }
 
 // one- or two-edge node v (two: its slots l, l + 1 with senders u0, u1 and pair pp; else
@@ -713,7 +760,7 @@ int launch(const gtf_kl_graph* g, const gtf_kl_out* o, hipStream_t st) {
     bk.ordered = !g->list[0] && !g->list[1] && !g->list[2] && !g->list[3];
     int total = 0;
     for (int i = 0; i < 4; i++) {
-        int per_block = i == 0 ? (bk.ordered ? BLOCK : BLOCK * NPT) : BLOCK / BG[i];   // nodes per block
+        int per_block = i == 0 ? (bk.ordered ? BLOCK * NPT_ORD : BLOCK * NPT) : BLOCK / BG[i];   // nodes per block
         if (i == 1 && !GTF_KL_B1_LANES) per_block = BLOCK;
         bk.blocks[i] = gtf::pad8((g->count[i] + per_block - 1) / per_block);
         total += bk.blocks[i];

@@ -138,9 +138,17 @@ struct PState {
 
 // parabolic state of the edge from neighbour (xb, yb) in the node's frame
 // (utils.py:273-283); optional full fp64 outputs
+// the Lagrange denominator D = x0 xB (x0 - xB) of the state from neighbour (xb, yb), as
+// pstate forms it in type T
+template <typename T>
+__device__ __forceinline__ T pstate_den(const Frame& f, double xb, double yb) {
+    const T X0 = (T)f.x0, XB = (T)((xb * f.ca - yb * f.sa) - f.xt);
+    return X0 * XB * (X0 - XB);
+}
+
 template <typename T>
 __device__ __forceinline__ PState<T> pstate(const Frame& f, double xb, double yb, bool& singular, double* sv_out,
-                                            double* cov_out) {
+                                            double* cov_out, const T* rd_given = nullptr) {
     const double xB = (xb * f.ca - yb * f.sa) - f.xt;
     const double mB = (xb * f.sa + yb * f.ca) - f.yt;
     const double x0 = f.x0;
@@ -161,7 +169,7 @@ __device__ __forceinline__ PState<T> pstate(const Frame& f, double xb, double yb
     const T X0 = (T)x0, XB = (T)xB, MB = (T)mB;
     const T s0 = (T)s0d, s1 = (T)s1d;
     // the three Lagrange denominators share one reciprocal: D = x0 xB (x0 - xB)
-    const T rD = T(1) / (X0 * XB * (X0 - XB));
+    const T rD = rd_given ? *rd_given : T(1) / (X0 * XB * (X0 - XB));
     const T r0 = XB * rD, r1 = (X0 - XB) * rD, r2 = -X0 * rD;
     const T a0 = r0, b0 = -XB * r0;
     const T a1 = r1, b1 = -(X0 + XB) * r1;
@@ -326,17 +334,46 @@ struct B0Node {
     long long tv, t0, t1;
 };
 
+// GTF_KL_RCP (fp64): the node's two Lagrange denominators and two gradient run lengths share
+// ONE division -- R = 1 / (Da Db E0 E1), each reciprocal R times the product of the other
+// three -- instead of four; within a few ulp of the divisions (the a17 outputs stay within
+// the tests' tolerances of the reference's), and the divisions themselves wherever the
+// product is zero, subnormal or not finite (a singular state or a zero run, whose infinities
+// must stay the reference's)
+#ifndef GTF_KL_RCP
+#define GTF_KL_RCP 0
+#endif
 template <typename T, bool STATES>
 __device__ __forceinline__ void pkl_b0_finish(const gtf_kl_out& o, const B0Node& n) {
     const Frame f = node_frame_xy(n.xv, n.yv);
     bool s0, s1 = false;
-    const PState<T> a = pstate<T>(f, n.x0, n.y0, s0, STATES ? o.sv + 3 * n.l : nullptr, STATES ? o.cov + 9 * n.l : nullptr);
+    const double e0 = f.x - n.x0, e1 = n.two ? f.x - n.x1 : 1.0;
+    double re0 = 0.0, re1 = 0.0;
+    T rda = T(0), rdb = T(0);
+    bool shared = false;
+    if constexpr (GTF_KL_RCP && sizeof(T) == 8 && !STATES) {
+        const double da = pstate_den<double>(f, n.x0, n.y0), db = n.two ? pstate_den<double>(f, n.x1, n.y1) : 1.0;
+        const double p1 = da * db, p2 = p1 * e0, P = p2 * e1;
+        shared = fabs(P) >= 2.2250738585072014e-308 && fabs(P) <= 1.7976931348623157e308;
+        if (shared) {
+            const double R = 1.0 / P;
+            re1 = R * p2;
+            const double t1 = R * e1;
+            re0 = t1 * p1;
+            const double t2 = t1 * e0;
+            rdb = t2 * da;
+            rda = t2 * db;
+        }
+    }
+    const PState<T> a = pstate<T>(f, n.x0, n.y0, s0, STATES ? o.sv + 3 * n.l : nullptr, STATES ? o.cov + 9 * n.l : nullptr,
+                                  shared ? &rda : nullptr);
     PState<T> b = a;
     if (n.two)
-        b = pstate<T>(f, n.x1, n.y1, s1, STATES ? o.sv + 3 * (n.l + 1) : nullptr, STATES ? o.cov + 9 * (n.l + 1) : nullptr);
+        b = pstate<T>(f, n.x1, n.y1, s1, STATES ? o.sv + 3 * (n.l + 1) : nullptr, STATES ? o.cov + 9 * (n.l + 1) : nullptr,
+                      shared ? &rdb : nullptr);
     if ((s0 || s1) && o.err) atomicOr(o.err, (uint32_t)GTF_ERR_SINGULAR_H);
-    const double g0 = (f.y - n.y0) / (f.x - n.x0);
-    const double g1 = n.two ? (f.y - n.y1) / (f.x - n.x1) : g0;
+    const double g0 = shared ? (f.y - n.y0) * re0 : (f.y - n.y0) / e0;
+    const double g1 = n.two ? (shared ? (f.y - n.y1) * re1 : (f.y - n.y1) / e1) : g0;
     // / 2 and / 1 as exact scalings
     const double mean = n.two ? (g0 + g1) * 0.5 : g0;
     if (o.emp_var)
@@ -398,27 +435,17 @@ __device__ __forceinline__ void pkl_node1_ordered(const gtf_kl_graph& g, const g
 template <typename T, bool STATES, typename S>
 __device__ __forceinline__ void pkl_b0_body(const gtf_kl_graph& g, const gtf_kl_out& o, const S& src, int v, bool two,
                                             int64_t l, int64_t pp, int u0, int u1) {
-    const double xv = src.x(v), yv = src.y(v);
-    const long long tv = (o.truth && g.truth) ? src.t(v) : 0;
-    const double x0 = src.x(u0), y0 = src.y(u0);
-    const double x1 = src.x(u1), y1 = src.y(u1);
-    long long t0 = 0, t1 = 0;
-    if (o.truth && g.truth) { t0 = src.t(u0); t1 = src.t(u1); }
-    const Frame f = node_frame_xy(xv, yv);
-    bool s0, s1 = false;
-    const PState<T> a = pstate<T>(f, x0, y0, s0, STATES ? o.sv + 3 * l : nullptr, STATES ? o.cov + 9 * l : nullptr);
-    PState<T> b = a;
-    if (two) b = pstate<T>(f, x1, y1, s1, STATES ? o.sv + 3 * (l + 1) : nullptr, STATES ? o.cov + 9 * (l + 1) : nullptr);
-    if ((s0 || s1) && o.err) atomicOr(o.err, (uint32_t)GTF_ERR_SINGULAR_H);
-    const double g0 = (f.y - y0) / (f.x - x0);
-    const double g1 = two ? (f.y - y1) / (f.x - x1) : g0;
-    const double mean = two ? (g0 + g1) * 0.5 : g0;   // / 2 and / 1 as exact scalings
-    if (o.emp_var) st_out(o.emp_var + (v), (double)(two ? ((g0 - mean) * (g0 - mean) + (g1 - mean) * (g1 - mean)) * 0.5 : 0.0 * (g0 - mean)));
-    if (o.emp_mean) st_out(o.emp_mean + (v), (double)(mean));
-    if (two) {
-        st_out((T*)o.kl + (pp), (T)(pkl<T>(b, a)));   // pair (i, j) = (1, 0)
-        if (o.truth) st_out(o.truth + (pp), (int8_t)(tv == t1 && t1 == t0 && tv == t0));
-    }
+    const bool tr = o.truth && g.truth;
+    B0Node n;
+    n.ok = true;
+    n.v = v, n.two = two, n.l = l, n.pp = pp, n.u0 = u0, n.u1 = u1;
+    n.xv = src.x(v), n.yv = src.y(v);
+    n.tv = tr ? src.t(v) : 0;
+    n.x0 = src.x(u0), n.y0 = src.y(u0);
+    n.x1 = src.x(u1), n.y1 = src.y(u1);
+    n.t0 = tr ? src.t(u0) : 0;
+    n.t1 = tr ? src.t(u1) : 0;
+    pkl_b0_finish<T, STATES>(o, n);
 }
 
 template <typename T, bool STATES>
@@ -465,29 +492,16 @@ __device__ __forceinline__ void pkl_node1(const gtf_kl_graph& g, const gtf_kl_ou
             }
         }
 #pragma unroll
-    for (int j = 0; j < NPT; j++) {
+    for (int j = 0; j < NPT; j++) {   // (the ordered and tiled layouts' bucket-0 arithmetic, bit for bit)
         if (!d[j]) continue;
-        const Frame f = node_frame_xy(xv[j], yv[j]);
-        const int l = lo[j];
-        bool s0, s1 = false;
-        const PState<T> a = pstate<T>(f, x0[j], y0[j], s0, STATES ? o.sv + 3 * (int64_t)l : nullptr,
-                                      STATES ? o.cov + 9 * (int64_t)l : nullptr);
-        PState<T> b = a;
-        if (d[j] == 2)
-            b = pstate<T>(f, x1[j], y1[j], s1, STATES ? o.sv + 3 * (int64_t)(l + 1) : nullptr,
-                          STATES ? o.cov + 9 * (int64_t)(l + 1) : nullptr);
-        if ((s0 || s1) && o.err) atomicOr(o.err, (uint32_t)GTF_ERR_SINGULAR_H);
-        const double g0 = (f.y - y0[j]) / (f.x - x0[j]);
-        const double g1 = d[j] == 2 ? (f.y - y1[j]) / (f.x - x1[j]) : g0;
-        const double mean = (d[j] == 2 ? g0 + g1 : g0) / (double)d[j];
-        if (o.emp_var)
-            o.emp_var[v[j]] = (d[j] == 2 ? (g0 - mean) * (g0 - mean) + (g1 - mean) * (g1 - mean)
-                                         : 0.0 * (g0 - mean)) / (double)d[j];
-        if (o.emp_mean) o.emp_mean[v[j]] = mean;
-        if (d[j] == 2) {
-            ((T*)o.kl)[pp[j]] = pkl<T>(b, a);   // pair (i, j) = (1, 0)
-            if (o.truth) o.truth[pp[j]] = (int8_t)(tv[j] == t1[j] && t1[j] == t0[j] && tv[j] == t0[j]);
-        }
+        B0Node n;
+        n.ok = true;
+        n.v = v[j], n.two = d[j] == 2, n.l = lo[j], n.pp = pp[j], n.u0 = u0[j], n.u1 = u1[j];
+        n.xv = xv[j], n.yv = yv[j], n.x0 = x0[j], n.y0 = y0[j], n.x1 = x1[j], n.y1 = y1[j];
+        n.tv = tv[j];
+        n.t0 = (o.truth && g.truth) ? t0[j] : 0;
+        n.t1 = (o.truth && g.truth) ? t1[j] : 0;
+        pkl_b0_finish<T, STATES>(o, n);
     }
 }
 

@@ -8,12 +8,12 @@ mkdir -p $O
 L=$R/gnn-track-finding_amd/gtf
 timeout -k 10 300 python -u -m pytest tests/test_gpu_parabolic.py -x -q --timeout 200 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
-for v in npt2 npt3; do
+for v in npt2 npt3 rcp rcpnpt2; do
   GTF_LIB=$L/libgtf_$v.so timeout -k 10 300 python -u -m pytest tests/test_gpu_parabolic.py -x -q --timeout 200 --timeout-method thread > $O/pytest_$v.log 2>&1 || { tail -30 $O/pytest_$v.log; exit 1; }
   echo "$v: $(tail -1 $O/pytest_$v.log)"
 done
-for i in 1 2; do
-  for v in libgtf libgtf_npt2 libgtf_npt3 libgtf_klwv6 libgtf_klwv4 libgtf_klb128; do
+for i in 1; do
+  for v in libgtf libgtf_npt2 libgtf_npt3 libgtf_rcp libgtf_rcpnpt2 libgtf_klwv6 libgtf_klwv4 libgtf_klb128; do
     GTF_LIB=$L/$v.so timeout -k 10 120 python tools/pkl_time.py 48 >> $O/kl_ab.jsonl || exit 1
   done
   for keep in 0 123; do
@@ -22,4 +22,5 @@ for i in 1 2; do
   done
 done
 cat $O/kl_ab.jsonl
+PROG="tools/pkl_time.py 24" bash tools/gpu_sqmix.sh r04/i/sq_pkl || exit 1
 echo r04i-done

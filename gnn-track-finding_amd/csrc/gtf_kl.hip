@@ -228,9 +228,8 @@ constexpr size_t stage_bytes(int G, size_t t) { return (size_t)(BLOCK / G) * G *
 // the wavefront bucket beyond 64 in-edges, where pair lanes recompute both states)
 // node v on G lanes (lane gl), its states staged at stg
 template <typename T, int G, bool STATES, typename S>
-__device__ __forceinline__ void pkl_node_body(const gtf_kl_graph& g, const gtf_kl_out& o, const S& src, int v, int gl,
-                                              KlStage<T, G>* stg) {
-    const int lo = g.slot_ptr[v], d = g.slot_ptr[v + 1] - lo;
+__device__ __forceinline__ void pkl_node_core(const gtf_kl_graph& g, const gtf_kl_out& o, const S& src, int v, int lo,
+                                              int d, int64_t base, int gl, KlStage<T, G>* stg) {
     if (d < 1) return;
     const Frame f = node_frame_xy(src.x(v), src.y(v));
 
@@ -276,7 +275,6 @@ __device__ __forceinline__ void pkl_node_body(const gtf_kl_graph& g, const gtf_k
     // pairs i > j, row-major, round-robin over the lanes: consecutive lanes write
     // consecutive distances (calc_pairwise_distances, :19-25)
     const int np = d * (d - 1) / 2;
-    const int64_t base = g.pair_ptr[v];
     const long long tv = g.truth ? src.t(v) : 0;
     T* kl = (T*)o.kl;
     for (int t = gl; t < np; t += G) {
@@ -298,6 +296,14 @@ __device__ __forceinline__ void pkl_node_body(const gtf_kl_graph& g, const gtf_k
         st_out(kl + (base + t), (T)(pkl<T>(a, b)));
         if (o.truth) st_out(o.truth + (base + t), (int8_t)(tv == ti && ti == tj && tv == tj));  // (:84-95)
     }
+}
+
+template <typename T, int G, bool STATES, typename S>
+__device__ __forceinline__ void pkl_node_body(const gtf_kl_graph& g, const gtf_kl_out& o, const S& src, int v, int gl,
+                                              KlStage<T, G>* stg) {
+    const int lo = g.slot_ptr[v], d = g.slot_ptr[v + 1] - lo;
+    if (d < 1) return;
+    pkl_node_core<T, G, STATES>(g, o, src, v, lo, d, g.pair_ptr[v], gl, stg);
 }
 
 template <typename T, int G, bool STATES>
@@ -590,7 +596,42 @@ __device__ __forceinline__ void pkl_node4(const gtf_kl_graph& g, const gtf_kl_ou
 struct KlBuckets {
     int32_t blocks[4];
     int32_t ordered;   // gtf_kl_graph's ordered layout (every list NULL)
+    int32_t runs;      // ... with degree runs (gtf_kl_graph.deg_runs): buckets 1 / 2 by arithmetic
+    int32_t n3;        // bucket 1's three-edge nodes (its first run)
+    int32_t r2[4];     // bucket 2's runs of 5..8 in-edges: first entry of each
+    int64_t slot1, pair1;        // bucket 1's first slot / pair
+    int64_t slot2[4], pair2[4];  // each bucket-2 run's first slot / pair
 };
+
+// ordered layout with degree runs: bucket-1 entry gi (three- then four-edge nodes), its
+// slots, senders and pairs by arithmetic -- the node's own fields and its sender list are
+// one round of independent loads, the senders' coordinates the second
+template <typename T, bool STATES>
+__device__ __forceinline__ void pkl_node4_runs(const gtf_kl_graph& g, const gtf_kl_out& o, const KlBuckets& bk, int bid) {
+    const int gi = bid * BLOCK + (int)threadIdx.x;
+    if (gi >= g.count[1]) return;
+    const bool three = gi < bk.n3;
+    const int d = three ? 3 : 4;
+    const int64_t lo = bk.slot1 + (three ? 3 * (int64_t)gi : 3 * (int64_t)bk.n3 + 4 * (int64_t)(gi - bk.n3));
+    const int64_t pp = bk.pair1 + (three ? 3 * (int64_t)gi : 3 * (int64_t)bk.n3 + 6 * (int64_t)(gi - bk.n3));
+    int u[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) u[q] = q < d ? ld_list(g.slot_src + lo + q) : 0;
+    pkl_node4_core<T, STATES>(g, o, GSrc(g), g.first[1] + gi, (int)lo, d, pp, u);
+}
+
+// ... and bucket-2 group gi (runs of 5, 6, 7, 8 in-edges) on G = 8 lanes
+template <typename T, bool STATES>
+__device__ __forceinline__ void pkl_node8_runs(const gtf_kl_graph& g, const gtf_kl_out& o, const KlBuckets& bk, int bid,
+                                               char* smem) {
+    const int gi = (bid * BLOCK + (int)threadIdx.x) / 8;
+    if (gi >= g.count[2]) return;   // group-uniform
+    const int k = gi >= bk.r2[3] ? 3 : gi >= bk.r2[2] ? 2 : gi >= bk.r2[1] ? 1 : 0;
+    const int d = 5 + k, i = gi - bk.r2[k];
+    pkl_node_core<T, 8, STATES>(g, o, GSrc(g), g.first[2] + gi, (int)(bk.slot2[k] + (int64_t)i * d), d,
+                                bk.pair2[k] + (int64_t)i * (d * (d - 1) / 2), (int)threadIdx.x & 7,
+                                (KlStage<T, 8>*)smem + (int)threadIdx.x / 8);
+}
 
 // one launch over the four buckets; wavefront-bucket blocks first (longest-running)
 // 5 waves per SIMD (96 VGPRs, 6 spilled in the fp64 kernel): the compiler's default pick
@@ -615,12 +656,14 @@ __global__ void __launch_bounds__(BLOCK) KL_ATTR k_parabolic_kl(gtf_kl_graph g, 
     }
     b -= bk.blocks[3];
     if (b < bk.blocks[2]) {
-        pkl_node<T, 8, STATES>(g, o, g.list[2], g.count[2], gtf::xcd_local(b, bk.blocks[2]), smem, g.first[2]);
+        if (bk.runs) pkl_node8_runs<T, STATES>(g, o, bk, gtf::xcd_local(b, bk.blocks[2]), smem);
+        else pkl_node<T, 8, STATES>(g, o, g.list[2], g.count[2], gtf::xcd_local(b, bk.blocks[2]), smem, g.first[2]);
         return;
     }
     b -= bk.blocks[2];
     if (b < bk.blocks[1]) {
         if (GTF_KL_B1_LANES) pkl_node<T, 4, STATES>(g, o, g.list[1], g.count[1], gtf::xcd_local(b, bk.blocks[1]), smem, g.first[1]);
+        else if (bk.runs) pkl_node4_runs<T, STATES>(g, o, bk, gtf::xcd_local(b, bk.blocks[1]));
         else pkl_node4<T, STATES>(g, o, g.list[1], g.count[1], gtf::xcd_local(b, bk.blocks[1]), g.first[1]);
         return;
     }
@@ -772,6 +815,19 @@ int launch(const gtf_kl_graph* g, const gtf_kl_out* o, hipStream_t st) {
     }
     KlBuckets bk;
     bk.ordered = !g->list[0] && !g->list[1] && !g->list[2] && !g->list[3];
+    bk.runs = bk.ordered && g->deg_runs == 1;
+    bk.n3 = g->n_deg[0];
+    bk.slot1 = g->slot0 + g->n_d1 + 2 * (int64_t)(g->count[0] - g->n_d1);
+    bk.pair1 = g->pair0 + (g->count[0] - g->n_d1);
+    bk.r2[0] = 0;
+    bk.slot2[0] = bk.slot1 + 3 * (int64_t)g->n_deg[0] + 4 * (int64_t)g->n_deg[1];
+    bk.pair2[0] = bk.pair1 + 3 * (int64_t)g->n_deg[0] + 6 * (int64_t)g->n_deg[1];
+    for (int k = 1; k < 4; k++) {
+        const int dp = 4 + k;   // the previous run's in-degree
+        bk.r2[k] = bk.r2[k - 1] + g->n_deg[1 + k];
+        bk.slot2[k] = bk.slot2[k - 1] + (int64_t)dp * g->n_deg[1 + k];
+        bk.pair2[k] = bk.pair2[k - 1] + (int64_t)(dp * (dp - 1) / 2) * g->n_deg[1 + k];
+    }
     int total = 0;
     for (int i = 0; i < 4; i++) {
         int per_block = i == 0 ? (bk.ordered ? BLOCK * NPT_ORD : BLOCK * NPT) : BLOCK / BG[i];   // nodes per block
@@ -813,6 +869,17 @@ extern "C" int gtf_parabolic_kl(const gtf_kl_graph* g, int32_t dtype, const gtf_
                   g->slot0 + g->n_d1 + 2 * (int64_t)(g->count[0] - g->n_d1) <= g->n_slots;
         for (int i = 0; i < 4; i++)
             ok = ok && g->first[i] >= 0 && (int64_t)g->first[i] + g->count[i] <= g->n_nodes;
+        if (ok && g->deg_runs == 1) {   // the runs add up to buckets 1 and 2 and stay inside the slots / pairs
+            int64_t slots = g->slot0 + g->n_d1 + 2 * (int64_t)(g->count[0] - g->n_d1), c1 = 0, c2 = 0;
+            for (int k = 0; k < 6; k++) {
+                ok = ok && g->n_deg[k] >= 0;
+                slots += (int64_t)(3 + k) * g->n_deg[k];
+                (k < 2 ? c1 : c2) += g->n_deg[k];
+            }
+            ok = ok && c1 == g->count[1] && c2 == g->count[2] && slots <= g->n_slots;
+        } else if (g->deg_runs != 0) {
+            ok = false;
+        }
         if (!ok) { gtf::set_error("gtf_parabolic_kl: bad ordered layout"); return -2; }
     }
     if (g->gnn_stride != 0 && g->gnn_stride != 2 && g->gnn_stride != 4) {

@@ -103,7 +103,7 @@ class GtfKlGraph(ctypes.Structure):
     _fields_ = [("n_nodes", I32), ("n_slots", I32), ("slot_ptr", P), ("slot_src", P), ("gnn", P), ("truth", P),
                 ("pair_ptr", P), ("list", P * 4), ("count", I32 * 4), ("first", I32 * 4), ("n_d1", I32),
                 ("gnn_stride", I32), ("slot0", ctypes.c_int64), ("pair0", ctypes.c_int64), ("blk", P),
-                ("n_blk", I32), ("pad_blk_", I32)]
+                ("n_blk", I32), ("deg_runs", I32), ("n_deg", I32 * 6), ("pad_deg_", I32)]
 
 
 class GtfDiag(ctypes.Structure):

@@ -19,6 +19,7 @@ multiset is what parity is checked on.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 import torch
@@ -78,8 +79,8 @@ class ParabolicKL:
         ordered = ordered or self.tile > 0
         if ordered:
             sp = slot_ptr.astype(np.int64)
-            keys = [d == 1 if lo == 1 else np.zeros(d.size, bool), d == 2, d == 3, d == 4] + \
-                   [(d >= a) & (d <= b) for a, b in BUCKETS[2:]]   # (bucket 1 as its 3- then 4-edge nodes)
+            # buckets 1 and 2 as runs of one in-degree each (3, 4 | 5, 6, 7, 8), then the > 8 bucket
+            keys = [d == 1 if lo == 1 else np.zeros(d.size, bool)] + [d == q for q in range(2, 9)] + [d > 8]
             rank = np.full(d.size, len(keys), np.int64)
             for q in reversed(range(len(keys))):
                 rank[keys[q]] = q
@@ -152,13 +153,17 @@ class ParabolicKL:
                                      _ptr(self.gnn), _ptr(self.truth), _ptr(self.pair_ptr),
                                      (ctypes.c_void_p * 4)(), (ctypes.c_int32 * 4)(*counts),
                                      (ctypes.c_int32 * 4)(*first.tolist()), n1, 2, 0, 0)
+            if os.environ.get("GTF_KL_DEG_RUNS", "1") != "0":   # degree runs (0: the round-3 ordered form)
+                self._g.deg_runs = 1
+                for q in range(6):
+                    self._g.n_deg[q] = self._ranges[2 + q]
         else:
             self._g = nat.GtfKlGraph(self.n_nodes, self.n_slots, _ptr(self.slot_ptr), _ptr(self.slot_src),
                                      _ptr(self.gnn), _ptr(self.truth), _ptr(self.pair_ptr),
                                      (ctypes.c_void_p * 4)(*[x.data_ptr() if x.numel() else None for x in self.lists]),
                                      (ctypes.c_int32 * 4)(*[x.numel() for x in self.lists]), gnn_stride=2)
 
-    def _block_table(self, d, pair_ptr, margin=WIN_MARGIN):
+    def _block_table(self, d, pair_ptr, margin=WIN_MARGIN):   # (rank < 16: 10 keys)
         """gtf_kl_graph.blk of the tiled layout: one record of 12 int32 per tile (first node,
         bucket-0 count, its one-edge count, the three- and four-edge counts that follow (0 and
         0 unless tile_b1), 0, bucket 0's first slot, its first pair lo / hi, the window
@@ -169,13 +174,13 @@ class ParabolicKL:
         nt = int(tid.max()) + 1 if n else 0
         bounds = np.searchsorted(tid, np.arange(nt + 1))
         a, b = bounds[:-1], bounds[1:]
-        n1 = np.searchsorted(tid * 8 + rank, tid[a] * 8 + 1) - a if nt else a   # rank-0 run at the tile head
-        n0 = np.searchsorted(tid * 8 + rank, tid[a] * 8 + 2) - a if nt else a
+        n1 = np.searchsorted(tid * 16 + rank, tid[a] * 16 + 1) - a if nt else a   # rank-0 run at the tile head
+        n0 = np.searchsorted(tid * 16 + rank, tid[a] * 16 + 2) - a if nt else a
         z = np.zeros(nt, np.int64)
         n3 = n4 = z
         if self.tile_b1 and nt:
-            n3 = np.searchsorted(tid * 8 + rank, tid[a] * 8 + 3) - a - n0
-            n4 = np.searchsorted(tid * 8 + rank, tid[a] * 8 + 4) - a - n0 - n3
+            n3 = np.searchsorted(tid * 16 + rank, tid[a] * 16 + 3) - a - n0
+            n4 = np.searchsorted(tid * 16 + rank, tid[a] * 16 + 4) - a - n0 - n3
         pr = pair_ptr[a]   # (one-edge nodes have no pairs: the first two-edge node's, then the 3- / 4-edge nodes')
         span = b - a
         m = np.clip((WIN_NODES - span) // 2, 0, margin)

@@ -566,7 +566,14 @@ typedef struct gtf_kl_graph {
      * LDS. Buckets 1..3 come from list[1..3] / count[1..3] (count[0] and list[0] are ignored). */
     const int32_t* blk;       /* [12 * n_blk] or NULL */
     int32_t n_blk;
-    int32_t pad_blk_;
+    /* ordered layout, degree runs (round 4): deg_runs = 1 when buckets 1 and 2 hold their nodes
+     * sorted by in-degree, n_deg[k] nodes of in-degree 3 + k (k = 0..5) one run after another
+     * (sum n_deg[0..1] = count[1], sum n_deg[2..5] = count[2]), with consecutive slots and pairs
+     * after bucket 0's: the kernel then finds their slots and pairs by arithmetic as well (one
+     * dependent round of loads fewer). 0: slot_ptr / pair_ptr are read per node. */
+    int32_t deg_runs;
+    int32_t n_deg[6];
+    int32_t pad_deg_;
 } gtf_kl_graph;
 
 enum { GTF_F64 = 0, GTF_F32 = 1 };

@@ -14,7 +14,7 @@ disp = collections.defaultdict(set)
 for f in glob.glob(d + "/sq*/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         n = r["Kernel_Name"]
-        if not any(s in n for s in ("k_sender", "k_extrapolate", "k_node")):
+        if not any(s in n for s in ("k_sender", "k_extrapolate", "k_node", "k_parabolic")):
             continue
         n = n.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0]
         acc[n][r["Counter_Name"]] += float(r["Counter_Value"])

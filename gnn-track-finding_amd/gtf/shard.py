@@ -550,10 +550,14 @@ class SplitDeviceGraph:
         return f
 
     # ------------------------------------------------------------------ the pass
-    def step(self, p, exchange=True, join=True):
+    def step(self, p, exchange=True, join=True, linear=False):
         """the pass of the whole event: both halves concurrently, then the halo exchange
         through device memory, then the two streams join (every later call on either
-        stream sees the whole pass). exchange / join False: diagnostics timings only."""
+        stream sees the whole pass). exchange / join False: diagnostics timings only.
+        linear: the exchange joined into the first stream instead -- it waits for the second
+        half's pack and runs both unpacks, and the second stream then waits for it -- one
+        cross-stream dependency at a time (the mutual mid-capture waits of the default form
+        crash hipStreamEndCapture on this stack, profiles/r04/capture/)."""
         (a, b), (sa, sb) = self.parts, self.streams
         packed, done = self._ev
         for r, sd in enumerate(self.parts):
@@ -561,6 +565,14 @@ class SplitDeviceGraph:
             if exchange:
                 sd.halo_pack()
                 packed[r].record(self.streams[r])
+        if exchange and linear:
+            sa.wait_event(packed[1])
+            a.halo_unpack(ctypes.c_void_p(b.send_buf.data_ptr()))
+            b.halo_unpack(ctypes.c_void_p(a.send_buf.data_ptr()), stream=sa)
+            if join:
+                done[0].record(sa)
+                sb.wait_event(done[0])
+            return
         if exchange:
             sa.wait_event(packed[1])
             a.halo_unpack(ctypes.c_void_p(b.send_buf.data_ptr()))

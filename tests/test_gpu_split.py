@@ -27,14 +27,16 @@ def _single(g, passes):
     return outs
 
 
+@pytest.mark.parametrize("linear", [False, True])
 @pytest.mark.parametrize("workload", ["c4", "tiny300"])
-def test_split_pass_equals_one_stream_pass(workload):
+def test_split_pass_equals_one_stream_pass(workload, linear):
+    """linear: the exchange joined into the first stream (SplitDeviceGraph.step(linear=True))"""
     g = synth.workload(workload, seed=0)
     ref = _single(g, 2)
     sp = SplitDeviceGraph(g)
     sp.clear_errors()
     for k in range(2):
-        sp.step(Params())
+        sp.step(Params(), linear=linear)
         got = sp.download(g.copy())
         errs = compare(got, ref[k], rtol=0.0, atol=0.0)
         assert errs == [], "pass %d: %s" % (k + 1, errs[:10])

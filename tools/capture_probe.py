@@ -14,6 +14,8 @@ MODE (each a superset of the previous):
            waits (each stream waits on the other's event, then launches) -- a runtime repro
   linear   the exchange joined into one stream instead (stream 0 waits on stream 1's pack, both
            unpacks on stream 0, stream 1 forked back): one kernel node with two dependencies
+  linstep  SplitDeviceGraph.step(linear=True) with its join (stream 1 waits for stream 0's
+           unpacks): the capture-safe form of the split step
 Each mode captures, instantiates (capture_end), replays once and checks the outputs against
 the same calls run directly. Prints one JSON line."""
 import ctypes
@@ -129,7 +131,7 @@ elif mode == "linear":
         joins[0].record(sa)
         cap.wait_event(joins[0])
     say(step="captured")
-elif mode in ("fork", "exchange", "step"):
+elif mode in ("fork", "exchange", "step", "linstep"):
     with torch.cuda.graph(gr, stream=cap, capture_error_mode="thread_local"):
         fork.record(cap)
         sa.wait_event(fork)
@@ -137,6 +139,8 @@ elif mode in ("fork", "exchange", "step"):
         if mode == "fork":
             a.pass_(p)
             b.pass_(p)
+        elif mode == "linstep":
+            sp.step(p, join=True, linear=True)
         else:
             sp.step(p, join=(mode == "step"))
         joins[0].record(sa)

@@ -39,13 +39,13 @@ def run_one():
     return (time.perf_counter() - t0) / K
 
 
-def run_split(exchange=True, join=True):
+def run_split(exchange=True, join=True, linear=False):
     sp.fill_inputs(ssnap)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(K):
         sp.use_inputs(i)
-        sp.step(p, exchange, join)
+        sp.step(p, exchange, join, linear)
     torch.cuda.synchronize()
     sp.use_inputs(None)
     return (time.perf_counter() - t0) / K
@@ -54,7 +54,7 @@ def run_split(exchange=True, join=True):
 for f in (run_one, run_split):
     f()
 out = {"one_stream_ms": [], "split_ms": [], "split_no_exchange_ms": [], "split_no_join_ms": [],
-       "split_passes_only_ms": []}
+       "split_passes_only_ms": [], "split_linear_ms": []}
 host = []
 for _ in range(R):
     out["one_stream_ms"].append(run_one() * 1e3)
@@ -62,6 +62,7 @@ for _ in range(R):
     out["split_no_exchange_ms"].append(run_split(False, True) * 1e3)
     out["split_no_join_ms"].append(run_split(True, False) * 1e3)
     out["split_passes_only_ms"].append(run_split(False, False) * 1e3)
+    out["split_linear_ms"].append(run_split(linear=True) * 1e3)
 # host time to enqueue one split step (no synchronize)
 sp.fill_inputs(ssnap)
 torch.cuda.synchronize()
@@ -104,7 +105,7 @@ if os.environ.get("GTF_SPLIT_GRAPH", "0") == "1":
                 # capture's join below orders both streams, and the two mutual waits -- each stream
                 # made to depend on the other's last node -- crashed hipStreamEndCapture (rc 139,
                 # tools/capture_probe.py modes "exchange" vs "step", profiles/r04/capture/)
-                sp.step(p, join=False)
+                sp.step(p, join=False, linear=os.environ.get("GTF_SPLIT_LINEAR", "0") == "1")
                 for r_, s_ in enumerate(sp.streams):
                     joins[i][r_].record(s_)
                     cap.wait_event(joins[i][r_])
@@ -125,4 +126,5 @@ if os.environ.get("GTF_SPLIT_GRAPH", "0") == "1":
         torch.cuda.synchronize()
         res.append((time.perf_counter() - t0) / K * 1e3)
     # the replayed passes against the one-stream pass: same outputs after K passes
-    print(json.dumps({"split_graph_ms": res, "flags": sp.errors(), "capture_mode": mode}), flush=True)
+    print(json.dumps({"split_graph_ms": res, "flags": sp.errors(), "capture_mode": mode,
+                      "linear": os.environ.get("GTF_SPLIT_LINEAR", "0") == "1"}), flush=True)

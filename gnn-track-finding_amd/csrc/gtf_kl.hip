@@ -876,7 +876,9 @@ extern "C" int gtf_parabolic_kl(const gtf_kl_graph* g, int32_t dtype, const gtf_
                 slots += (int64_t)(3 + k) * g->n_deg[k];
                 (k < 2 ? c1 : c2) += g->n_deg[k];
             }
-            ok = ok && c1 == g->count[1] && c2 == g->count[2] && slots <= g->n_slots;
+            // (a bucket left out -- count 0 -- launches nothing; the runs still place the next one)
+            ok = ok && (c1 == g->count[1] || g->count[1] == 0) && (c2 == g->count[2] || g->count[2] == 0) &&
+                 slots <= g->n_slots;
         } else if (g->deg_runs != 0) {
             ok = false;
         }

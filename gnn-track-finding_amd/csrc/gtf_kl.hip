@@ -672,6 +672,22 @@ __global__ void __launch_bounds__(BLOCK) KL_ATTR k_parabolic_kl(gtf_kl_graph g, 
     else pkl_node1<T, STATES>(g, o, g.list[0], g.count[0], gtf::xcd_local(b, bk.blocks[0]));
 }
 
+// GTF_KL_SPLIT_B0 (ordered layout): the one-/two-edge bucket in a launch of its own at
+// GTF_KL_B0_WAVES waves per SIMD (its path needs far fewer registers than the 3..4-edge
+// bucket's register-resident states, which set the one-launch kernel's budget), after the
+// launch of the other buckets on the same stream
+#ifndef GTF_KL_SPLIT_B0
+#define GTF_KL_SPLIT_B0 0
+#endif
+#ifndef GTF_KL_B0_WAVES
+#define GTF_KL_B0_WAVES 8
+#endif
+template <typename T, bool STATES>
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(GTF_KL_B0_WAVES)))
+k_parabolic_kl_b0(gtf_kl_graph g, gtf_kl_out o, int nblk) {
+    pkl_node1_ordered<T, STATES>(g, o, gtf::xcd_local(blockIdx.x, nblk));
+}
+
 // Tiled layout (gtf_kl_graph.blk, gtf.parabolic.ParabolicKL(tile=T)): the nodes
 // azimuth-sorted per event and cut into tiles of <= 256 one- / two-edge (bucket-0) nodes
 // and the other nodes between them, bucket 0 first inside a tile. One block of WBLOCK
@@ -835,11 +851,23 @@ int launch(const gtf_kl_graph* g, const gtf_kl_out* o, hipStream_t st) {
         bk.blocks[i] = gtf::pad8((g->count[i] + per_block - 1) / per_block);
         total += bk.blocks[i];
     }
+    int b0_blocks = 0;
+    if (GTF_KL_SPLIT_B0 && bk.ordered && bk.blocks[0] > 0) {   // bucket 0 in its own launch, after the others
+        b0_blocks = bk.blocks[0];
+        total -= b0_blocks;
+        bk.blocks[0] = 0;
+    }
     if (total > 0) {
         if (o->sv || o->cov)
             hipLaunchKernelGGL((k_parabolic_kl<T, true>), dim3(total), dim3(BLOCK), 0, st, *g, *o, bk);
         else
             hipLaunchKernelGGL((k_parabolic_kl<T, false>), dim3(total), dim3(BLOCK), 0, st, *g, *o, bk);
+    }
+    if (b0_blocks > 0) {
+        if (o->sv || o->cov)
+            hipLaunchKernelGGL((k_parabolic_kl_b0<T, true>), dim3(b0_blocks), dim3(BLOCK), 0, st, *g, *o, b0_blocks);
+        else
+            hipLaunchKernelGGL((k_parabolic_kl_b0<T, false>), dim3(b0_blocks), dim3(BLOCK), 0, st, *g, *o, b0_blocks);
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) {

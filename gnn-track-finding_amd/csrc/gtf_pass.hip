@@ -274,8 +274,17 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(GTF_SEND
 // ---------------------------------------------------------------------------
 // k_extrapolate: one slot (edge u -> v) per thread
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(BLOCK) k_extrapolate(gtf_graph g, gtf_nodes n, gtf_states uts, gtf_edges e,
-                                                       gtf_params p, Ws w, int slot_lo, int slot_hi) {
+#ifndef GTF_EXTRAP_WAVES
+#define GTF_EXTRAP_WAVES 0   // > 0: amdgpu_waves_per_eu lower bound (register budget) of k_extrapolate
+#endif
+#if GTF_EXTRAP_WAVES > 0
+#define GTF_EXTRAP_ATTR __attribute__((amdgpu_waves_per_eu(GTF_EXTRAP_WAVES)))
+#else
+#define GTF_EXTRAP_ATTR
+#endif
+__global__ void __launch_bounds__(BLOCK) GTF_EXTRAP_ATTR k_extrapolate(gtf_graph g, gtf_nodes n, gtf_states uts,
+                                                                       gtf_edges e, gtf_params p, Ws w, int slot_lo,
+                                                                       int slot_hi) {
     const int k = slot_lo + xcd_local(blockIdx.x, gridDim.x) * BLOCK + threadIdx.x;
     if (k >= slot_hi) return;
     // Two levels of loads instead of a chain: everything indexed by the slot, then

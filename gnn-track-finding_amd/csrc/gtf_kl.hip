@@ -648,8 +648,29 @@ __global__ void __launch_bounds__(BLOCK) KL_ATTR k_parabolic_kl(gtf_kl_graph g, 
                                                           ? stage_bytes(4, sizeof(T))
                                                           : stage_bytes(64, sizeof(T))];
     // bucket block ranges are multiples of 8, each remapped XCD-contiguous on its own:
-    // neighbouring nodes (one event's hits) share an L2
+    // neighbouring nodes (one event's hits) share an L2. GTF_KL_ORDER (diagnostics): 0 the
+    // > 8, 5..8, 3..4-edge buckets' blocks first, then bucket 0; 1 bucket 0 first; 2 the
+    // other buckets' blocks spread evenly among bucket 0's
     int b = blockIdx.x;
+#ifndef GTF_KL_ORDER
+#define GTF_KL_ORDER 0
+#endif
+    if (GTF_KL_ORDER == 1 && bk.ordered) {
+        if (b < bk.blocks[0]) {
+            pkl_node1_ordered<T, STATES>(g, o, gtf::xcd_local(b, bk.blocks[0]));
+            return;
+        }
+        b -= bk.blocks[0];
+    } else if (GTF_KL_ORDER == 2 && bk.ordered) {
+        const int64_t rest = (int64_t)bk.blocks[3] + bk.blocks[2] + bk.blocks[1];
+        const int64_t tot = rest + bk.blocks[0];
+        const int upto = (int)(((int64_t)b + 1) * rest / tot);   // other-bucket blocks among [0, b]
+        if (upto == (int)((int64_t)b * rest / tot)) {           // b is a bucket-0 block
+            pkl_node1_ordered<T, STATES>(g, o, b - upto);
+            return;
+        }
+        b = upto - 1;
+    }
     if (b < bk.blocks[3]) {
         pkl_node<T, 64, STATES>(g, o, g.list[3], g.count[3], gtf::xcd_local(b, bk.blocks[3]), smem, g.first[3]);
         return;
@@ -668,6 +689,7 @@ __global__ void __launch_bounds__(BLOCK) KL_ATTR k_parabolic_kl(gtf_kl_graph g, 
         return;
     }
     b -= bk.blocks[1];
+    if (GTF_KL_ORDER != 0 && bk.ordered) return;   // (bucket 0 taken above)
     if (bk.ordered) pkl_node1_ordered<T, STATES>(g, o, gtf::xcd_local(b, bk.blocks[0]));
     else pkl_node1<T, STATES>(g, o, g.list[0], g.count[0], gtf::xcd_local(b, bk.blocks[0]));
 }

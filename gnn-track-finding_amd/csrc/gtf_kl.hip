@@ -650,7 +650,7 @@ __global__ void __launch_bounds__(BLOCK) KL_ATTR k_parabolic_kl(gtf_kl_graph g, 
     // bucket block ranges are multiples of 8, each remapped XCD-contiguous on its own:
     // neighbouring nodes (one event's hits) share an L2. GTF_KL_ORDER (diagnostics): 0 the
     // > 8, 5..8, 3..4-edge buckets' blocks first, then bucket 0; 1 bucket 0 first; 2 the
-    // other buckets' blocks spread evenly among bucket 0's
+    // other buckets' blocks spread evenly among bucket 0's; 3 the same in chunks of 8 blocks
     int b = blockIdx.x;
 #ifndef GTF_KL_ORDER
 #define GTF_KL_ORDER 0
@@ -670,6 +670,16 @@ __global__ void __launch_bounds__(BLOCK) KL_ATTR k_parabolic_kl(gtf_kl_graph g, 
             return;
         }
         b = upto - 1;
+    } else if (GTF_KL_ORDER == 3 && bk.ordered) {   // as 2 in chunks of 8 blocks (one per XCD): the
+        const int64_t rest = ((int64_t)bk.blocks[3] + bk.blocks[2] + bk.blocks[1]) / 8;   // XCD-contiguous
+        const int64_t tot = rest + bk.blocks[0] / 8;                                      // maps stay intact
+        const int ch = b / 8, x = b % 8;
+        const int upto = (int)(((int64_t)ch + 1) * rest / tot);
+        if (upto == (int)((int64_t)ch * rest / tot)) {
+            pkl_node1_ordered<T, STATES>(g, o, gtf::xcd_local((ch - upto) * 8 + x, bk.blocks[0]));
+            return;
+        }
+        b = (upto - 1) * 8 + x;
     }
     if (b < bk.blocks[3]) {
         pkl_node<T, 64, STATES>(g, o, g.list[3], g.count[3], gtf::xcd_local(b, bk.blocks[3]), smem, g.first[3]);

@@ -648,12 +648,15 @@ __global__ void __launch_bounds__(BLOCK) KL_ATTR k_parabolic_kl(gtf_kl_graph g, 
                                                           ? stage_bytes(4, sizeof(T))
                                                           : stage_bytes(64, sizeof(T))];
     // bucket block ranges are multiples of 8, each remapped XCD-contiguous on its own:
-    // neighbouring nodes (one event's hits) share an L2. GTF_KL_ORDER (diagnostics): 0 the
+    // neighbouring nodes (one event's hits) share an L2. GTF_KL_ORDER: 0 the
     // > 8, 5..8, 3..4-edge buckets' blocks first, then bucket 0; 1 bucket 0 first; 2 the
     // other buckets' blocks spread evenly among bucket 0's; 3 the same in chunks of 8 blocks
     int b = blockIdx.x;
 #ifndef GTF_KL_ORDER
-#define GTF_KL_ORDER 0
+#define GTF_KL_ORDER 3
+#endif
+#ifndef GTF_KL_MIX
+#define GTF_KL_MIX 100
 #endif
     if (GTF_KL_ORDER == 1 && bk.ordered) {
         if (b < bk.blocks[0]) {
@@ -671,11 +674,13 @@ __global__ void __launch_bounds__(BLOCK) KL_ATTR k_parabolic_kl(gtf_kl_graph g, 
         }
         b = upto - 1;
     } else if (GTF_KL_ORDER == 3 && bk.ordered) {   // as 2 in chunks of 8 blocks (one per XCD): the
-        const int64_t rest = ((int64_t)bk.blocks[3] + bk.blocks[2] + bk.blocks[1]) / 8;   // XCD-contiguous
-        const int64_t tot = rest + bk.blocks[0] / 8;                                      // maps stay intact
+        // XCD-contiguous maps stay intact; the other buckets' chunks spread over the first
+        // GTF_KL_MIX % of bucket 0's
+        const int64_t rest = ((int64_t)bk.blocks[3] + bk.blocks[2] + bk.blocks[1]) / 8;
+        const int64_t tot = rest + (int64_t)bk.blocks[0] / 8 * GTF_KL_MIX / 100;
         const int ch = b / 8, x = b % 8;
-        const int upto = (int)(((int64_t)ch + 1) * rest / tot);
-        if (upto == (int)((int64_t)ch * rest / tot)) {
+        const int upto = ch >= tot ? (int)rest : (int)(((int64_t)ch + 1) * rest / tot);
+        if (ch >= tot || upto == (int)((int64_t)ch * rest / tot)) {
             pkl_node1_ordered<T, STATES>(g, o, gtf::xcd_local((ch - upto) * 8 + x, bk.blocks[0]));
             return;
         }

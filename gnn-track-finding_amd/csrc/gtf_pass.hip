@@ -168,57 +168,6 @@ __device__ __forceinline__ void sender_scan_lane(const gtf_graph& g, gtf_nodes& 
     if (gl == 0) n.merged_cov[5 * (int64_t)u + 3] = fin;
 }
 
-// a sender of the 16-lane bucket: its first G out-edges from gtf_graph.out_lanes in the
-// round of its own fields (as sender_scan_lane), the rest -- senders with more than G --
-// chunk by chunk after them (as sender_scan)
-template <int G>
-__device__ __forceinline__ void sender_scan_lane_more(const gtf_graph& g, gtf_nodes& n, const gtf_edges& e,
-                                                      const gtf_params& p, const Ws& w, int u, int ob, int oe, int k,
-                                                      int v, int gl) {
-    const uint8_t hm = n.has_merged[u];
-    const double a = n.merged_state[3 * (int64_t)u + 0];
-    const double b = n.merged_state[3 * (int64_t)u + 1];
-    const double ng[4] = {g.gnn[4 * (int64_t)u], g.gnn[4 * (int64_t)u + 1], g.gnn[4 * (int64_t)u + 2],
-                          g.gnn[4 * (int64_t)u + 3]};
-    double carry = n.merged_cov[5 * (int64_t)u + 3];
-    const int kk = k >= 0 ? k : 0;
-    const double nb[4] = {g.gnn[4 * (int64_t)v], g.gnn[4 * (int64_t)v + 1], g.gnn[4 * (int64_t)v + 2],
-                          g.gnn[4 * (int64_t)v + 3]};
-    const uint8_t act = e.act[kk];
-    if (!hm || ob == oe) return;   // group-uniform
-    {
-        double vm = -1.0;
-        if (k >= 0 && act == 1) vm = highland_var_ms(a, b, ng, nb, p.endcap_boundary);
-        double c = carry;
-        for (int m = 0; m < G; m++) {
-            const double vmm = __shfl(vm, m, G);
-            if (m <= gl && vmm != -1.0) c = c + vmm;
-        }
-        if (vm != -1.0) w.vc[g.slot_outidx ? ob + gl : k] = c;
-        carry = __shfl(c, G - 1, G);   // lanes past the end carry the full sum
-    }
-    for (int base = ob + G; base < oe; base += G) {
-        const int i = base + gl;
-        double vm = -1.0;
-        int k2 = -1;
-        if (i < oe) {
-            k2 = g.out_slot[i];
-            const int v2 = g.out_dst ? g.out_dst[i] : g.slot_dst[k2];
-            const double nb2[4] = {g.gnn[4 * (int64_t)v2], g.gnn[4 * (int64_t)v2 + 1], g.gnn[4 * (int64_t)v2 + 2],
-                                   g.gnn[4 * (int64_t)v2 + 3]};
-            if (e.act[k2] == 1) vm = highland_var_ms(a, b, ng, nb2, p.endcap_boundary);
-        }
-        double c = carry;
-        for (int m = 0; m < G; m++) {
-            const double vmm = __shfl(vm, m, G);
-            if (m <= gl && vmm != -1.0) c = c + vmm;
-        }
-        if (vm != -1.0) w.vc[g.slot_outidx ? i : k2] = c;
-        carry = __shfl(c, G - 1, G);
-    }
-    if (gl == 0) n.merged_cov[5 * (int64_t)u + 3] = carry;
-}
-
 // every node (list NULL) or a list of senders (a shard's), 8 lanes per sender
 constexpr int SG = 8;
 __global__ void __launch_bounds__(BLOCK) k_sender(gtf_graph g, gtf_nodes n, gtf_edges e, gtf_params p, Ws w,
@@ -237,7 +186,7 @@ struct SendBuckets {
     const int4* list[3];
     int32_t count[3];
     int32_t blocks[3];  // padded to multiples of 8
-    const int2* lanes[3];  // gtf_graph.out_lanes of the 4-, 8- and 16-lane buckets, or NULL
+    const int2* lanes[2];  // gtf_graph.out_lanes of the 4- and 8-lane buckets, or NULL
 };
 
 template <int G>
@@ -262,18 +211,6 @@ __device__ __forceinline__ void sender_bucket_lanes(const gtf_graph& g, gtf_node
     sender_scan_lane<G>(g, n, e, p, w, en.x, en.y, kv.x, kv.y, t & (G - 1));
 }
 
-template <int G>
-__device__ __forceinline__ void sender_bucket_lanes_more(const gtf_graph& g, gtf_nodes& n, const gtf_edges& e,
-                                                         const gtf_params& p, const Ws& w, const int4* list,
-                                                         const int2* lanes, int count, int b, int nb) {
-    const int t = xcd_local(b, nb) * BLOCK + (int)threadIdx.x;
-    const int gi = t / G;
-    if (gi >= count) return;  // group-uniform
-    const int4 en = list[gi];
-    const int2 kv = lanes[t];
-    sender_scan_lane_more<G>(g, n, e, p, w, en.x, en.y, en.z, kv.x, kv.y, t & (G - 1));
-}
-
 // All arguments of k_sender_sched in one by-value struct, read through a laundered copy of
 // the kernarg-segment address (as the node kernel's NodeKArgs, gtf_node_group.h): each
 // bucket path loads only the pointers it uses. Passed as separate structs the scan kept
@@ -296,9 +233,6 @@ __device__ __forceinline__ SendKArgPtr send_kargs() {
 
 #ifndef GTF_SEND_KARGS
 #define GTF_SEND_KARGS 1
-#endif
-#ifndef GTF_SEND_LANES16
-#define GTF_SEND_LANES16 1   // the 16-lane bucket's first out-edges from gtf_graph.out_lanes too
 #endif
 #ifndef GTF_SEND_NUM_SGPR
 #define GTF_SEND_NUM_SGPR 72
@@ -333,10 +267,7 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(GTF_SEND
     }
     b -= b1;
     const SendBuckets& sb = GTF_SA(sb);
-    if (GTF_SEND_LANES16 && sb.lanes[2])
-        sender_bucket_lanes_more<16>(GTF_SA(g), GTF_SA(n), GTF_SA(e), GTF_SA(p), GTF_SA(w), sb.list[2], sb.lanes[2],
-                                     sb.count[2], b, sb.blocks[2]);
-    else sender_bucket<16>(GTF_SA(g), GTF_SA(n), GTF_SA(e), GTF_SA(p), GTF_SA(w), sb.list[2], sb.count[2], b, sb.blocks[2]);
+    sender_bucket<16>(GTF_SA(g), GTF_SA(n), GTF_SA(e), GTF_SA(p), GTF_SA(w), sb.list[2], sb.count[2], b, sb.blocks[2]);
 #undef GTF_SA
 }
 
@@ -914,7 +845,6 @@ int launch_extrap_edges(const gtf_graph* g, gtf_nodes* n, gtf_states* uts, gtf_e
 #endif
             sb.lanes[0] = ln;
             sb.lanes[1] = ln ? ln + 4 * g->n_o4 : nullptr;
-            sb.lanes[2] = ln ? ln + 4 * g->n_o4 + 8 * g->n_o8 : nullptr;
             for (int q = 0; q < 3; q++) {
                 sb.list[q] = l;
                 l += cnt[q];

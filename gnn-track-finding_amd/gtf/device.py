@@ -49,14 +49,13 @@ def sender_schedule(out_ptr, nodes=None):
 
 
 def sender_lanes(out_slot, out_dst, q, counts):
-    """gtf_graph.out_lanes: for every lane of the 4-, 8- and 16-lane entries of the sender
-    schedule `q` (sender_schedule), (slot, receiver) of the lane's out-edge -- the first 16
-    of a sender with more -- or (-1, 0)"""
+    """gtf_graph.out_lanes: for every lane of the 4- and 8-lane entries of the sender
+    schedule `q` (sender_schedule), (slot, receiver) of the lane's out-edge or (-1, 0)"""
     q = np.asarray(q, dtype=np.int64).reshape(-1, 4)
     os_ = np.asarray(out_slot, dtype=np.int64)
     od = np.asarray(out_dst, dtype=np.int64)
     parts, at = [], 0
-    for G, n in ((4, counts[0]), (8, counts[1]), (16, counts[2])):
+    for G, n in ((4, counts[0]), (8, counts[1])):
         e = q[at:at + n]
         at += n
         idx = e[:, 1:2] + np.arange(G)[None, :]

@@ -105,12 +105,11 @@ typedef struct gtf_graph {
     const int32_t* pack_ent;  /* [4*n_entries] */
     const int32_t* pack_wave; /* [n_pack_waves+1] */
     int32_t n_pack_waves;
-    /* optional per-lane view of out_sched's 4-, 8- and 16-lane buckets (v3; the 16-lane bucket
-     * since v5): for lane l of entry e of those buckets, (out_slot[o], receiver of o) with
-     * o = out_ptr[sender] + l, or (-1, 0) past the sender's last out-edge, as int32 pairs -- the
-     * scan then reads each lane's edge beside the schedule entry instead of after it (one
-     * dependent round of loads fewer; a 16-lane sender's out-edges past its 16th are read after
-     * it). [2 * (4 * n_o4 + 8 * n_o8 + 16 * n_o16)], or NULL. */
+    /* optional per-lane view of out_sched's 4- and 8-lane buckets (v3): for lane l of entry e
+     * of those buckets, (out_slot[o], receiver of o) with o = out_ptr[sender] + l, or (-1, 0)
+     * past the sender's last out-edge, as int32 pairs -- the scan then reads each lane's edge
+     * beside the schedule entry instead of after it (one dependent round of loads fewer).
+     * [2 * (4 * n_o4 + 8 * n_o8)], or NULL. */
     const int32_t* out_lanes;
     /* optional padded tile layout of the node kernel (v3; gtf.graph.padded): the nodes of
      * each lane-group size G = 2, 4, 8, 16, 32, 64 own exactly G slots (their own, then inert

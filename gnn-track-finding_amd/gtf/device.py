@@ -92,6 +92,7 @@ def pack_schedule(slot_ptr):
 
 
 CLASS_MAX = 32   # segments of up to this many slots get graph-static classes (gtf_graph.slot_class)
+CLASS_MIN_SLOTS = 1 << 16   # graphs this large get them by default (the host pass: ~4 ms on 15k slots)
 
 
 def slot_classes(g: TrackGraph):
@@ -183,10 +184,12 @@ class DeviceGraph:
     stage methods are layout-independent (the pass is equivariant under renumber)."""
 
     def __init__(self, g: TrackGraph, device: str = "cuda", schedule: bool = True, layout: str = "natural",
-                 pack: bool = False, tile: int = TILE, mem: str = "torch"):
+                 pack: bool = False, tile: int = TILE, mem: str = "torch", classes=None):
         """mem "torch": the arrays are torch tensors (every method). mem "hip": plain
         allocations from libgtf (gtf.devmem, no torch in the process): the stage methods,
-        clear_errors / errors and download only -- the drop-in CLIs' path."""
+        clear_errors / errors and download only -- the drop-in CLIs' path. classes: upload
+        the graph-static slot classes (gtf_graph.slot_class); None = on graphs of at least
+        CLASS_MIN_SLOTS slots."""
         if mem not in ("torch", "hip"):
             raise ValueError("mem must be 'torch' or 'hip'")
         self.mem = mem
@@ -231,15 +234,20 @@ class DeviceGraph:
         # stores its running values in out-edge order (GTF_NO_OUTIDX=1: by slot, for A/B)
         import os
         self.use_outidx = os.environ.get("GTF_NO_OUTIDX", "0") != "1"
-        # graph-static slot classes for the node kernel (GTF_NO_CLASSES=1: built in the kernel, A/B)
-        self.use_classes = os.environ.get("GTF_NO_CLASSES", "0") != "1"
+        # graph-static slot classes for the node kernel on graphs of >= CLASS_MIN_SLOTS slots
+        # (smaller ones -- a drop-in stage's directory -- have the kernel build them: the host
+        # pass would cost more than it saves); classes=True / False forces either way,
+        # GTF_NO_CLASSES=1 turns them off (A/B)
+        self.use_classes = (classes if classes is not None else g.n_slots >= CLASS_MIN_SLOTS) and \
+            os.environ.get("GTF_NO_CLASSES", "0") != "1"
         oidx = np.full(g.n_slots, -1, np.int32)
         if g.n_edges:
             oidx[g.out_slot] = np.arange(g.n_edges, dtype=np.int32)
         up("slot_outidx", oidx)
-        cls, sfl = slot_classes(g)
-        up("slot_class", cls.view(np.int64))
-        up("slot_sflags", sfl)
+        if self.use_classes:
+            cls, sfl = slot_classes(g)
+            up("slot_class", cls.view(np.int64))
+            up("slot_sflags", sfl)
         sub = g.node["sub_id"].astype(np.int64)
         if g.n_nodes:
             sizes = np.bincount(sub - sub.min())

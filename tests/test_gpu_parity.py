@@ -21,9 +21,18 @@ def _params(meta):
                   cluster_chi2=meta.get("chi2", 1000.0), cluster_kl=meta.get("kl", 100.0))
 
 
+@pytest.fixture(params=[False, True], ids=["kernel_classes", "static_classes"], autouse=True)
+def _classes(request):
+    """every test with the node kernel building its slot classes (the default at this size)
+    and with the graph-static classes uploaded (gtf_graph.slot_class, the large-graph default)"""
+    global CLASSES
+    CLASSES = request.param
+    yield
+
+
 def _dev(g):
     from gtf.device import DeviceGraph
-    return DeviceGraph(g)
+    return DeviceGraph(g, classes=CLASSES)
 
 
 def _run(name, fn, rtol=RTOL):

@@ -620,6 +620,21 @@ __device__ __forceinline__ void pkl_node4_runs(const gtf_kl_graph& g, const gtf_
     pkl_node4_core<T, STATES>(g, o, GSrc(g), g.first[1] + gi, (int)lo, d, pp, u);
 }
 
+// ... bucket-1 entry gi on a 4-lane group (GTF_KL_B1_LANES: the LDS-staged form, fewer
+// registers than the thread-per-node one)
+template <typename T, bool STATES>
+__device__ __forceinline__ void pkl_node4l_runs(const gtf_kl_graph& g, const gtf_kl_out& o, const KlBuckets& bk, int bid,
+                                                char* smem) {
+    const int gi = (bid * BLOCK + (int)threadIdx.x) / 4;
+    if (gi >= g.count[1]) return;   // group-uniform
+    const bool three = gi < bk.n3;
+    const int d = three ? 3 : 4;
+    const int64_t lo = bk.slot1 + (three ? 3 * (int64_t)gi : 3 * (int64_t)bk.n3 + 4 * (int64_t)(gi - bk.n3));
+    const int64_t pp = bk.pair1 + (three ? 3 * (int64_t)gi : 3 * (int64_t)bk.n3 + 6 * (int64_t)(gi - bk.n3));
+    pkl_node_core<T, 4, STATES>(g, o, GSrc(g), g.first[1] + gi, (int)lo, d, pp, (int)threadIdx.x & 3,
+                                (KlStage<T, 4>*)smem + (int)threadIdx.x / 4);
+}
+
 // ... and bucket-2 group gi (runs of 5, 6, 7, 8 in-edges) on G = 8 lanes
 template <typename T, bool STATES>
 __device__ __forceinline__ void pkl_node8_runs(const gtf_kl_graph& g, const gtf_kl_out& o, const KlBuckets& bk, int bid,
@@ -698,7 +713,8 @@ __global__ void __launch_bounds__(BLOCK) KL_ATTR k_parabolic_kl(gtf_kl_graph g, 
     }
     b -= bk.blocks[2];
     if (b < bk.blocks[1]) {
-        if (GTF_KL_B1_LANES) pkl_node<T, 4, STATES>(g, o, g.list[1], g.count[1], gtf::xcd_local(b, bk.blocks[1]), smem, g.first[1]);
+        if (GTF_KL_B1_LANES && bk.runs) pkl_node4l_runs<T, STATES>(g, o, bk, gtf::xcd_local(b, bk.blocks[1]), smem);
+        else if (GTF_KL_B1_LANES) pkl_node<T, 4, STATES>(g, o, g.list[1], g.count[1], gtf::xcd_local(b, bk.blocks[1]), smem, g.first[1]);
         else if (bk.runs) pkl_node4_runs<T, STATES>(g, o, bk, gtf::xcd_local(b, bk.blocks[1]));
         else pkl_node4<T, STATES>(g, o, g.list[1], g.count[1], gtf::xcd_local(b, bk.blocks[1]), g.first[1]);
         return;

@@ -493,6 +493,59 @@ def bench_c5_sharded(dev, steps, warmup, rank, world, backend, n_events=256):
             "collective": "none (events are independent)", "device_error_flags": flags}
 
 
+def bench_c3_section(dev, steps, warmup, params, layout="tiled", tile=4096):
+    """configs[2] beside the C4 headline: 64 C2-like events fused into one CSR (2.0 M hits /
+    5.9 M edges), K passes on staged inputs, then the same K with HIP events around the
+    kernels -- the fused node kernel's roofline on SURVEY §8(d)'s bytes at the size §8(d)
+    quotes roofline fractions on (>= 1 GB of traffic per pass)"""
+    import torch
+    from gtf import synth, roofline as rf
+    from gtf.device import DeviceGraph
+    g = synth.workload("c3", seed=0)
+    d = DeviceGraph(g, dev, layout=layout, tile=tile)
+    snap = d.snapshot(DeviceGraph.PASS_INPUTS)
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(steps)]
+    for row in evs:
+        for e in row:
+            e.record()
+    handles = [[e.cuda_event for e in row] for row in evs]
+    d.clear_errors()
+    for _ in range(warmup):
+        d.restore(snap)
+        d.full_pass(params)
+    d.stage_inputs(steps)
+
+    def run(instrumented):
+        d.fill_inputs(snap)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            d.use_inputs(i)
+            d.full_pass(params, events=handles[i] if instrumented else None)
+        torch.cuda.synchronize()
+        d.use_inputs(None)
+        return (time.perf_counter() - t0) / steps
+
+    t = run(False)
+    run(True)
+    avg = lambda a, b: float(np.mean([evs[i][a].elapsed_time(evs[i][b]) for i in range(steps)]))  # noqa: E731
+    node_ms = avg(2, 3)
+    nb = rf.node_bytes(g.n_edges, g.n_nodes)
+    pb = rf.pass_bytes(g.n_edges, g.n_nodes)
+    res = {"workload": "64 C2-like events fused into one CSR (configs[2])", "nodes": g.n_nodes,
+           "directed_edges": g.n_edges, "steps": steps, "ms_per_step": t * 1e3, "edges_per_s": g.n_edges / t,
+           "kernel_ms": {"k_sender": avg(0, 1), "k_extrapolate": avg(1, 2), NODE_KERNEL: node_ms},
+           "roofline": {"bound": "hbm", "kernel": NODE_KERNEL, "algorithmic_bytes_per_launch": nb,
+                        "achieved": nb / (node_ms * 1e-3) / 1e9, "peak": rf.HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": nb / (node_ms * 1e-3) / 1e9 / rf.HBM_PEAK_GBS,
+                        "byte_model": "SURVEY §8d (fused node kernel 89 B/edge + 186 B/node)"},
+           "pass_roofline": {"algorithmic_bytes_per_step": pb, "frac": pb / t / 1e9 / rf.HBM_PEAK_GBS},
+           "device_error_flags": d.errors()}
+    del d
+    torch.cuda.empty_cache()
+    return res
+
+
 def device_copy_gbps(dev, nbytes=1 << 30, reps=10):
     """measured device-to-device copy bandwidth (bytes read + written per second), the
     practical HBM ceiling SURVEY §8d asks the roofline to be quoted against beside the
@@ -733,6 +786,7 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-c5", action="store_true", help="skip the config-5 parabolic-KL section")
     ap.add_argument("--no-dropin", action="store_true", help="skip the drop-in stage wall time")
+    ap.add_argument("--no-c3", action="store_true", help="skip the configs[2] (C3) section beside the C4 headline")
     ap.add_argument("--layout", default="tiled", choices=["tiled", "padded", "schedule", "natural"],
                     help="device node order (DeviceGraph layout)")
     ap.add_argument("--tile", type=int, default=4096, help="nodes per tile of --layout tiled")
@@ -890,6 +944,13 @@ def main():
         except Exception as ex:   # reported, the headline stands
             c5_sharded = {"error": repr(ex)[:300]}
 
+    c3 = None
+    if rank == 0 and world == 1 and args.workload == "c4" and not args.no_c3:
+        try:
+            c3 = bench_c3_section(dev, max(10, K // 5), 2, p, args.layout, args.tile)
+        except Exception as ex:   # reported; the headline stands
+            c3 = {"error": repr(ex)[:300]}
+
     cpu = cpu_cpp = dropin = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline(args.cpu_tracks, p, g.n_edges)
@@ -939,6 +1000,7 @@ def main():
             "dropin_stage": dropin,
             "device_error_flags": flags,
             "c5_parabolic_kl": c5,
+            "c3_fused_batch": c3,
             "other_path_stages": comps,
         }
         if c5_sharded is not None:

@@ -1189,6 +1189,19 @@ __global__ void __launch_bounds__(NBLOCK) GTF_NODE_WAVES_ATTR k_node_multi(NodeK
     // the costly nodes of a node range on one XCD.
     const KArgPtr A = node_kargs();
     int b = blockIdx.x;
+#ifndef GTF_NODE_ORDER
+#define GTF_NODE_ORDER 0   // 1 (diagnostics): the buckets by measured wave life, longest first (16, 32, 8, 64, 4, 2)
+#endif
+#if GTF_NODE_ORDER == 1
+    if (b < A->bk.blocks[2]) { node_bucket<16, OPS...>(2, b, smem); return; }
+    b -= A->bk.blocks[2];
+    if (b < A->bk.blocks[1]) { node_bucket<32, OPS...>(1, b, smem); return; }
+    b -= A->bk.blocks[1];
+    if (b < A->bk.blocks[3]) { node_bucket<8, OPS...>(3, b, smem); return; }
+    b -= A->bk.blocks[3];
+    if (b < A->bk.blocks[0]) { node_bucket<64, OPS...>(0, b, smem); return; }
+    b -= A->bk.blocks[0];
+#else
     if (b < A->bk.blocks[0]) { node_bucket<64, OPS...>(0, b, smem); return; }
     b -= A->bk.blocks[0];
     if (b < A->bk.blocks[1]) { node_bucket<32, OPS...>(1, b, smem); return; }
@@ -1197,6 +1210,7 @@ __global__ void __launch_bounds__(NBLOCK) GTF_NODE_WAVES_ATTR k_node_multi(NodeK
     b -= A->bk.blocks[2];
     if (b < A->bk.blocks[3]) { node_bucket<8, OPS...>(3, b, smem); return; }
     b -= A->bk.blocks[3];
+#endif
     if (b < A->bk.blocks[4]) { node_bucket<4, OPS...>(4, b, smem); return; }
     b -= A->bk.blocks[4];
     node_bucket<2, OPS...>(5, b, smem);

@@ -563,7 +563,10 @@ typedef struct gtf_kl_graph {
      * count, 0, 0, 0, bucket 0's first slot, its first pair low / high 32 bits, window [lo, hi) of
      * at most 1024 consecutive nodes holding the tile's neighbours, 0); the block loads its
      * sender lists and the window's x, y and truth ids in one round and reads the neighbours from
-     * LDS. Buckets 1..3 come from list[1..3] / count[1..3] (count[0] and list[0] are ignored). */
+     * LDS. Buckets 1..3 come from list[1..3] / count[1..3] (count[0] and list[0] are ignored). The
+     * library clamps each window to its LDS size but does not check the records' node, slot and
+     * pair ranges against the arrays (they live in device memory): build them with
+     * gtf.parabolic.ParabolicKL(tile=T), or keep every range inside n_nodes / n_slots. */
     const int32_t* blk;       /* [12 * n_blk] or NULL */
     int32_t n_blk;
     /* ordered layout, degree runs (round 4): deg_runs = 1 when buckets 1 and 2 hold their nodes

@@ -2,23 +2,85 @@
 // Reference: tag_propagation/tag_propagation.py:97-164. The reference walks a
 // dict-of-dicts adjacency and deep-copies the whole graph every sweep; here one
 // sweep is one launch over the out-CSR, reading the previous tag array and
-// writing the next (Jacobi), with the flip count reduced per wavefront before a
-// single atomic per wave.
+// writing the next (Jacobi). Counts never go through one hot word: a device-scope atomic
+// on one address saturates near 88 per microsecond on MI355X (MI355X_MICROARCH.md,
+// dequeue), so a wave-per-atomic count over the ~20k waves of a C4 launch costs ~200 us.
+// The processed count is a separate reduction of the processed bytes (a few dozen block
+// atomics), and a sweep's flips are summed per block in LDS and added to one of
+// TAG_SHARDS counter words, each on its own 128-byte line (block % TAG_SHARDS).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+
+#include <vector>
 
 #include "../../include/gtf.h"
 #include "gtf_math.h"
 
 namespace {
 constexpr int BLOCK = 256;
+constexpr int TAG_SHARDS = 32;    // counter words of one sweep's flip count
+constexpr int TAG_STRIDE = 32;    // int32 words between two shards (one 128-byte line each)
+
+// the block's count of `mine` lanes added to ctr: one atomic per block, to shard
+// blockIdx % nsh (nsh = 1: ctr is a single word). Every thread of the block calls it.
+template <typename T>
+__device__ __forceinline__ void block_count_add(int mine, T* ctr, int nsh) {
+    __shared__ int s_cnt[BLOCK / 64];
+    const unsigned long long b = __ballot(mine);
+    if ((threadIdx.x & 63) == 0) s_cnt[threadIdx.x >> 6] = (int)__popcll(b);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int t = 0;
+#pragma unroll
+        for (int w = 0; w < BLOCK / 64; w++) t += s_cnt[w];
+        if (t) atomicAdd(ctr + (nsh > 1 ? (int)(blockIdx.x % nsh) * TAG_STRIDE : 0), (T)t);
+    }
+}
+
+// the total of a sharded counter (wave-uniform: every lane gets it)
+__device__ __forceinline__ int32_t shard_total(const int32_t* ctr, int nsh) {
+    const int lane = threadIdx.x & 63;
+    int v = lane < nsh ? ctr[lane * TAG_STRIDE] : 0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// n_processed = the number of nonzero (= 1) bytes of processed[0, n): 16 bytes per thread
+// per step over the 16-byte aligned body (block 0 also takes the head and tail bytes), a
+// block sum, one atomic per block (a few dozen blocks)
+__global__ void __launch_bounds__(BLOCK) k_count_flags(const uint8_t* f, int n, int32_t* out) {
+    const int head0 = (int)((16 - ((uintptr_t)f & 15)) & 15);
+    const int head = head0 < n ? head0 : n;
+    const int nv = (n - head) / 16;
+    const int tail = head + 16 * nv;
+    int cnt = 0;
+    const uint4* v = reinterpret_cast<const uint4*>(f + head);
+    for (int i = blockIdx.x * BLOCK + threadIdx.x; i < nv; i += gridDim.x * BLOCK) {
+        const uint4 x = v[i];   // bytes are 0 or 1: one bit each
+        cnt += __popc(x.x) + __popc(x.y) + __popc(x.z) + __popc(x.w);
+    }
+    if (blockIdx.x == 0) {
+        const int t = (int)threadIdx.x;
+        if (t < head) cnt += f[t] != 0;
+        if (t < n - tail) cnt += f[tail + t] != 0;
+    }
+    __shared__ int s_cnt[BLOCK / 64];
+    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+    if ((threadIdx.x & 63) == 0) s_cnt[threadIdx.x >> 6] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int t = 0;
+        for (int w = 0; w < BLOCK / 64; w++) t += s_cnt[w];
+        if (t) atomicAdd(out, t);
+    }
+}
 
 // keep[e] = neighbour radius <= node radius (:99-110); processed[u] = any kept (:109-110)
 __global__ void __launch_bounds__(BLOCK) k_tag_prepare(gtf_graph g, const double* radius, uint8_t* keep,
-                                                       uint8_t* processed, int32_t* n_processed) {
+                                                       uint8_t* processed) {
     const int u = gtf::xcd_local(blockIdx.x, gridDim.x) * BLOCK + threadIdx.x;
-    int mine = 0;
     if (u < g.n_nodes) {
         const double ru = radius[u];
         int any = 0;
@@ -29,21 +91,18 @@ __global__ void __launch_bounds__(BLOCK) k_tag_prepare(gtf_graph g, const double
             any |= k;
         }
         processed[u] = (uint8_t)any;
-        mine = any;
     }
-    const unsigned long long b = __ballot(mine);
-    if ((threadIdx.x & 63) == 0 && b) atomicAdd(n_processed, (int)__popcll(b));
 }
 
 // The same on the sender schedule's lane groups (gtf_graph.out_sched + out_lanes): every lane
 // reads its out-edge's neighbour radius in one round beside the node's own, a group ballot
 // gives processed[u]; nodes without an out-edge are not processed (the launch's last blocks)
 template <int G>
-__device__ __forceinline__ int prep_group(const gtf_graph& g, const double* radius, uint8_t* keep, uint8_t* processed,
+__device__ __forceinline__ void prep_group(const gtf_graph& g, const double* radius, uint8_t* keep, uint8_t* processed,
                                           const int4* list, const int2* lanes, int count, int b) {
     const int t = b * BLOCK + (int)threadIdx.x;
     const int gi = t / G, gl = t & (G - 1);
-    if (gi >= count) return 0;   // group-uniform
+    if (gi >= count) return;   // group-uniform
     const int4 en = list[gi];
     const int u = en.x;
     const double ru = radius[u];
@@ -66,7 +125,6 @@ __device__ __forceinline__ int prep_group(const gtf_graph& g, const double* radi
     const unsigned long long m = __ballot(any);
     const bool grp_any = G == 64 ? m != 0ull : ((m >> (t & 63 & ~(G - 1))) & ((1ull << G) - 1ull)) != 0ull;
     if (gl == 0) processed[u] = (uint8_t)grp_any;
-    return gl == 0 && grp_any;
 }
 
 struct PrepBuckets {
@@ -77,21 +135,18 @@ struct PrepBuckets {
 };
 
 __global__ void __launch_bounds__(BLOCK) k_tag_prepare_sched(gtf_graph g, const double* radius, uint8_t* keep,
-                                                             uint8_t* processed, int32_t* n_processed, PrepBuckets pb) {
-    int b = blockIdx.x, mine = 0;
+                                                             uint8_t* processed, PrepBuckets pb) {
+    int b = blockIdx.x;
     if (b < pb.blocks[0]) {
-        mine = prep_group<4>(g, radius, keep, processed, pb.list[0], pb.lanes[0], pb.count[0], b);
+        prep_group<4>(g, radius, keep, processed, pb.list[0], pb.lanes[0], pb.count[0], b);
     } else if ((b -= pb.blocks[0]) < pb.blocks[1]) {
-        mine = prep_group<8>(g, radius, keep, processed, pb.list[1], pb.lanes[1], pb.count[1], b);
+        prep_group<8>(g, radius, keep, processed, pb.list[1], pb.lanes[1], pb.count[1], b);
     } else if ((b -= pb.blocks[1]) < pb.blocks[2]) {
-        mine = prep_group<16>(g, radius, keep, processed, pb.list[2], nullptr, pb.count[2], b);
+        prep_group<16>(g, radius, keep, processed, pb.list[2], nullptr, pb.count[2], b);
     } else {
         const int u = (b - pb.blocks[2]) * BLOCK + (int)threadIdx.x;
         if (u < g.n_nodes && g.out_ptr[u + 1] == g.out_ptr[u]) processed[u] = 0;
-        return;
     }
-    const unsigned long long m = __ballot(mine);
-    if ((threadIdx.x & 63) == 0 && m) atomicAdd(n_processed, (int)__popcll(m));
 }
 
 // The stop rule of the sweep loop on the device (tag_propagation.py:130-164): sweep s runs
@@ -101,7 +156,7 @@ __global__ void __launch_bounds__(BLOCK) k_tag_prepare_sched(gtf_graph g, const 
 // at once. Every block takes the same decision from the finished previous sweep's count.
 struct TagCtl {
     const int32_t* total;   // processed count (gtf_tag_prepare)
-    const int32_t* prev;    // flips of the previous sweep, NULL for the first
+    const int32_t* prev;    // flips of the previous sweep (TAG_SHARDS shards), NULL for the first
     int32_t* stop;          // set once the rule stops the loop
     int32_t* nexec;         // sweeps executed
     double thr;
@@ -111,7 +166,7 @@ __device__ __forceinline__ bool tag_skip(const TagCtl& c) {
     if (!c.stop) return false;
     if (*c.stop) return true;
     if (c.prev) {
-        const int32_t tot = *c.total, f = *c.prev;
+        const int32_t tot = *c.total, f = shard_total(c.prev, TAG_SHARDS);
         const double frac = tot ? (double)f / (double)tot : 0.0;
         if (!(frac > c.thr)) {
             if (blockIdx.x == 0 && threadIdx.x == 0) atomicExch(c.stop, 1);
@@ -131,7 +186,8 @@ __global__ void __launch_bounds__(BLOCK) k_tag_final(int64_t* tags, const int64_
 
 // tags_out[u] = max(tags_in[u], tags_in[kept successors]) (:141-150 -- max, not min)
 __global__ void __launch_bounds__(BLOCK) k_tag_sweep(gtf_graph g, const uint8_t* keep, const uint8_t* processed,
-                                                     const int64_t* tin, int64_t* tout, int32_t* flips, TagCtl ctl) {
+                                                     const int64_t* tin, int64_t* tout, int32_t* flips, int nsh,
+                                                     TagCtl ctl) {
     if (tag_skip(ctl)) return;
     const int u = gtf::xcd_local(blockIdx.x, gridDim.x) * BLOCK + threadIdx.x;
     int flipped = 0;
@@ -148,8 +204,7 @@ __global__ void __launch_bounds__(BLOCK) k_tag_sweep(gtf_graph g, const uint8_t*
         }
         tout[u] = t;
     }
-    const unsigned long long b = __ballot(flipped);
-    if ((threadIdx.x & 63) == 0 && b) atomicAdd(flips, (int)__popcll(b));
+    block_count_add(flipped, flips, nsh);
 }
 // With the sender schedule (gtf_graph.out_sched + out_lanes): G lanes per node over its
 // out-edges, every lane's loads in one round (its keep flag, its neighbour's tag, the
@@ -216,7 +271,7 @@ struct TagBuckets {
 
 __global__ void __launch_bounds__(BLOCK) k_tag_sweep_sched(gtf_graph g, const uint8_t* keep, const uint8_t* processed,
                                                            const int64_t* tin, int64_t* tout, int32_t* flips,
-                                                           TagBuckets tb, TagCtl ctl) {
+                                                           int nsh, TagBuckets tb, TagCtl ctl) {
     if (tag_skip(ctl)) return;
     int b = blockIdx.x, flipped = 0;
     if (b < tb.blocks[0]) {
@@ -230,10 +285,9 @@ __global__ void __launch_bounds__(BLOCK) k_tag_sweep_sched(gtf_graph g, const ui
     } else {
         const int u = (b - tb.blocks[2]) * BLOCK + (int)threadIdx.x;
         if (u < g.n_nodes && g.out_ptr[u + 1] == g.out_ptr[u]) tout[u] = tin[u];
-        return;
+        return;   // (block-uniform: these blocks count no flips)
     }
-    const unsigned long long m = __ballot(flipped);
-    if ((threadIdx.x & 63) == 0 && m) atomicAdd(flips, (int)__popcll(m));
+    block_count_add(flipped, flips, nsh);
 }
 
 // One rank's sweep of the sharded tag propagation: the owned nodes
@@ -262,8 +316,7 @@ __global__ void __launch_bounds__(BLOCK) k_tag_sweep_owned(gtf_graph g, const ui
         }
         tout[u] = t;
     }
-    const unsigned long long b = __ballot(flipped);
-    if ((threadIdx.x & 63) == 0 && b) atomicAdd(flips, (unsigned long long)__popcll(b));
+    block_count_add(flipped, flips, 1);
 }
 }  // namespace
 
@@ -297,18 +350,24 @@ int gtf_tag_prepare(const gtf_graph* g, const double* radius, uint8_t* keep, uin
             total += pb.blocks[q];
         }
         total += (g->n_nodes + BLOCK - 1) / BLOCK;   // nodes without an out-edge
-        hipLaunchKernelGGL(k_tag_prepare_sched, dim3(total), dim3(BLOCK), 0, st, *g, radius, keep, processed,
-                           n_processed, pb);
+        hipLaunchKernelGGL(k_tag_prepare_sched, dim3(total), dim3(BLOCK), 0, st, *g, radius, keep, processed, pb);
     } else if (g->n_nodes > 0) {
         hipLaunchKernelGGL(k_tag_prepare, dim3((g->n_nodes + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, st, *g, radius,
-                           keep, processed, n_processed);
+                           keep, processed);
+    }
+    if (g->n_nodes > 0) {   // the processed count: a reduction of the processed bytes
+        int blocks = (g->n_nodes / 16 + BLOCK * 4 - 1) / (BLOCK * 4);   // ~4 steps per thread
+        blocks = blocks < 1 ? 1 : (blocks > 128 ? 128 : blocks);
+        hipLaunchKernelGGL(k_count_flags, dim3(blocks), dim3(BLOCK), 0, st, processed, g->n_nodes, n_processed);
     }
     return hipGetLastError() == hipSuccess ? 0 : hip_fail("gtf_tag_prepare launch");
 }
 
+// flips: TAG_SHARDS counter words TAG_STRIDE apart (nsh = TAG_SHARDS, zeroed by the caller)
+// or one word (nsh = 1, zeroed here)
 static int tag_sweep(const gtf_graph* g, const uint8_t* keep, const uint8_t* processed, const int64_t* tags_in,
-                     int64_t* tags_out, int32_t* flips, const TagCtl& ctl, hipStream_t st) {
-    if (hipMemsetAsync(flips, 0, sizeof(int32_t), st) != hipSuccess) return hip_fail("gtf_tag_sweep");
+                     int64_t* tags_out, int32_t* flips, int nsh, const TagCtl& ctl, hipStream_t st) {
+    if (nsh == 1 && hipMemsetAsync(flips, 0, sizeof(int32_t), st) != hipSuccess) return hip_fail("gtf_tag_sweep");
     if (g->n_nodes > 0 && g->out_sched) {   // lane groups over the sender schedule
         TagBuckets tb;
         const int cnt[3] = {g->n_o4, g->n_o8, g->n_o16}, gs[3] = {4, 8, 16};
@@ -328,10 +387,10 @@ static int tag_sweep(const gtf_graph* g, const uint8_t* keep, const uint8_t* pro
         total += tb.copy_blocks;
         if (total > 0)
             hipLaunchKernelGGL(k_tag_sweep_sched, dim3(total), dim3(BLOCK), 0, st, *g, keep, processed, tags_in,
-                               tags_out, flips, tb, ctl);
+                               tags_out, flips, nsh, tb, ctl);
     } else if (g->n_nodes > 0) {
         hipLaunchKernelGGL(k_tag_sweep, dim3((g->n_nodes + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, st, *g, keep,
-                           processed, tags_in, tags_out, flips, ctl);
+                           processed, tags_in, tags_out, flips, nsh, ctl);
     }
     return hipGetLastError() == hipSuccess ? 0 : hip_fail("gtf_tag_sweep launch");
 }
@@ -340,15 +399,16 @@ int gtf_tag_sweep(const gtf_graph* g, const uint8_t* keep, const uint8_t* proces
                   int64_t* tags_out, int32_t* flips, gtf_stream_t stream) {
     if (int rc = gtf::check_abi(g, "gtf_tag_sweep")) return rc;
     const TagCtl none{nullptr, nullptr, nullptr, nullptr, 0.0};
-    return tag_sweep(g, keep, processed, tags_in, tags_out, flips, none, (hipStream_t)stream);
+    return tag_sweep(g, keep, processed, tags_in, tags_out, flips, 1, none, (hipStream_t)stream);
 }
 
 static size_t tag_align(size_t x) { return (x + 255) & ~size_t(255); }
 
-// the stop-rule words of gtf_tag_propagate: processed count, stop flag, executed sweeps, then
-// a ring of per-sweep flip counts
-constexpr int TAG_RING = 1024;
-constexpr size_t TAG_HDR = 4 * sizeof(int32_t) + TAG_RING * sizeof(int32_t);
+// the stop-rule words of gtf_tag_propagate: processed count, stop flag, executed sweeps; then
+// a ring of per-sweep flip counters, TAG_SHARDS words each (TAG_STRIDE apart)
+constexpr int TAG_RING = 128;
+constexpr size_t TAG_CTR = (size_t)TAG_SHARDS * TAG_STRIDE;   // int32 words per sweep
+constexpr size_t TAG_HDR = 64 * sizeof(int32_t) + TAG_RING * TAG_CTR * sizeof(int32_t);
 
 size_t gtf_tag_workspace_bytes(int32_t n_nodes, int32_t n_edges) {
     const size_t n = n_nodes > 0 ? (size_t)n_nodes : 1, e = n_edges > 0 ? (size_t)n_edges : 1;
@@ -358,7 +418,7 @@ size_t gtf_tag_workspace_bytes(int32_t n_nodes, int32_t n_edges) {
 // The whole stage behind one call: prepare, then the sweeps (the loop of
 // tag_propagation.py:130-164, first sweep unconditional) in batches of 2, 4, 8, ... launches
 // whose stop test runs on the device (TagCtl), the tag arrays ping-ponging between `tags` and
-// the workspace; the host reads the batch's flip counts once per batch (one stream
+// the workspace; the host reads the batch's flip counters once per batch (one stream
 // synchronisation) and stops as soon as the rule has. The final tags land in `tags` by a
 // device copy when the executed count is odd.
 int gtf_tag_propagate(const gtf_graph* g, const double* radius, int64_t* tags, double flip_threshold,
@@ -377,8 +437,8 @@ int gtf_tag_propagate(const gtf_graph* g, const double* radius, int64_t* tags, d
     hipStream_t st = (hipStream_t)stream;
     const size_t n = g->n_nodes > 0 ? (size_t)g->n_nodes : 1, e = n_edges > 0 ? (size_t)n_edges : 1;
     char* w = static_cast<char*>(workspace);
-    int32_t* hdr = reinterpret_cast<int32_t*>(w);   // [0] processed [1] stop [2] executed [3] - [4..] flip ring
-    int32_t* ring = hdr + 4;
+    int32_t* hdr = reinterpret_cast<int32_t*>(w);   // [0] processed [1] stop [2] executed; the ring from word 64
+    int32_t* ring = hdr + 64;
     w += tag_align(TAG_HDR);
     uint8_t* keep = reinterpret_cast<uint8_t*>(w);
     w += tag_align(e);
@@ -389,26 +449,34 @@ int gtf_tag_propagate(const gtf_graph* g, const double* radius, int64_t* tags, d
     if (hipMemsetAsync(hdr, 0, 4 * sizeof(int32_t), st) != hipSuccess) return hip_fail("gtf_tag_propagate");
     if (int rc = gtf_tag_prepare(g, radius, keep, proc, hdr, stream)) return rc;
     int32_t s = 0, batch = 2, executed = 0;
-    int32_t host[4 + TAG_RING];
+    int32_t host[4];
+    std::vector<int32_t> hring(TAG_RING * TAG_CTR);
     bool stopped = false;
     while (!stopped && s < max_sweeps) {
         const int32_t at = s % TAG_RING;
         int32_t nb = batch < max_sweeps - s ? batch : max_sweeps - s;
-        if (nb > TAG_RING - at) nb = TAG_RING - at;   // the batch's counts stay contiguous in the ring
+        if (nb > TAG_RING - at) nb = TAG_RING - at;   // the batch's counters stay contiguous in the ring
+        if (hipMemsetAsync(ring + at * TAG_CTR, 0, nb * TAG_CTR * sizeof(int32_t), st) != hipSuccess)
+            return hip_fail("gtf_tag_propagate: zeroing the flip counters");
         for (int32_t i = 0; i < nb; i++) {
             const int32_t q = s + i;
-            const TagCtl ctl{hdr, q > 0 ? ring + (q - 1) % TAG_RING : nullptr, hdr + 1, hdr + 2, flip_threshold};
+            const TagCtl ctl{hdr, q > 0 ? ring + ((q - 1) % TAG_RING) * TAG_CTR : nullptr, hdr + 1, hdr + 2,
+                             flip_threshold};
             int64_t* tin = (q & 1) ? other : tags;
             int64_t* tout = (q & 1) ? tags : other;
-            if (int rc = tag_sweep(g, keep, proc, tin, tout, ring + q % TAG_RING, ctl, st)) return rc;
+            if (int rc = tag_sweep(g, keep, proc, tin, tout, ring + (q % TAG_RING) * TAG_CTR, TAG_SHARDS, ctl, st))
+                return rc;
         }
         if (hipMemcpyAsync(host, hdr, 4 * sizeof(int32_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
-            hipMemcpyAsync(host + 4 + at, ring + at, nb * sizeof(int32_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipMemcpyAsync(hring.data() + at * TAG_CTR, ring + at * TAG_CTR, nb * TAG_CTR * sizeof(int32_t),
+                           hipMemcpyDeviceToHost, st) != hipSuccess ||
             hipStreamSynchronize(st) != hipSuccess)
             return hip_fail("gtf_tag_propagate: reading the flip counts");
         executed = host[2];
         for (int32_t q = s; q < executed; q++) {
-            const int32_t f = host[4 + q % TAG_RING];
+            int32_t f = 0;
+            const int32_t* c = hring.data() + (q % TAG_RING) * TAG_CTR;
+            for (int k = 0; k < TAG_SHARDS; k++) f += c[k * TAG_STRIDE];
             if (flips_out) flips_out[q] = f;
             // the rule on the host too: the batch's last executed sweep may already stop it
             const double frac = host[0] ? (double)f / (double)host[0] : 0.0;

@@ -36,6 +36,55 @@ def unique_id(lib=None) -> bytes:
     return buf.raw
 
 
+_ID_MAGIC = b"GTFCOMM1"
+
+
+def job_token() -> str:
+    """a token that names this launch of the job: GTF_COMM_JOB, else the launcher's run id
+    (torchrun's TORCHELASTIC_RUN_ID, Slurm's SLURM_JOB_ID.SLURM_STEP_ID), else its rendezvous
+    address MASTER_ADDR:MASTER_PORT (a port is bound by one job at a time)"""
+    e = os.environ
+    if e.get("GTF_COMM_JOB"):
+        return e["GTF_COMM_JOB"]
+    if e.get("TORCHELASTIC_RUN_ID"):
+        return "torchelastic:" + e["TORCHELASTIC_RUN_ID"]
+    if e.get("SLURM_JOB_ID"):
+        return "slurm:%s.%s" % (e["SLURM_JOB_ID"], e.get("SLURM_STEP_ID", ""))
+    if e.get("MASTER_PORT"):
+        return "rdzv:%s:%s" % (e.get("MASTER_ADDR", ""), e["MASTER_PORT"])
+    raise ValueError("NativeComm.from_file needs a job token: pass job=... or set GTF_COMM_JOB "
+                     "(or run under a launcher that sets MASTER_PORT / TORCHELASTIC_RUN_ID)")
+
+
+def write_id_file(path: str, uid: bytes, job: str) -> None:
+    """the id file of this job: magic, the job token (length-prefixed), the unique id;
+    written to a temporary name and renamed over `path`"""
+    tok = job.encode()
+    tmp = "%s.%d.tmp" % (path, os.getpid())
+    with open(tmp, "wb") as fh:
+        fh.write(_ID_MAGIC + len(tok).to_bytes(4, "little") + tok + uid)
+    os.replace(tmp, path)
+
+
+def read_id_file(path: str, job: str, timeout: float = 120.0) -> bytes:
+    """wait until `path` holds THIS job's id (a stale file of another run -- other token --
+    or a missing one is waited past), then return the unique id"""
+    tok = job.encode()
+    head = _ID_MAGIC + len(tok).to_bytes(4, "little") + tok
+    t0 = time.monotonic()
+    while True:
+        try:
+            with open(path, "rb") as fh:
+                data = fh.read()
+            if data.startswith(head) and len(data) == len(head) + nat.COMM_ID_BYTES:
+                return data[len(head):]
+        except FileNotFoundError:
+            pass
+        if time.monotonic() - t0 > timeout:
+            raise TimeoutError("no RCCL unique id of job %r at %s after %.0f s" % (job, path, timeout))
+        time.sleep(0.01)
+
+
 class NativeComm:
     def __init__(self, rank: int, world: int, uid: bytes, lib=None):
         if len(uid) != nat.COMM_ID_BYTES:
@@ -53,23 +102,19 @@ class NativeComm:
         return cls(0, 1, unique_id(lib), lib)
 
     @classmethod
-    def from_file(cls, path: str, rank: int, world: int, timeout: float = 120.0, lib=None) -> "NativeComm":
+    def from_file(cls, path: str, rank: int, world: int, timeout: float = 120.0, lib=None,
+                  job: str | None = None) -> "NativeComm":
         """rank 0 writes the unique id to `path` (atomically: a temporary file renamed), the
-        other ranks wait for it; every rank then joins"""
+        other ranks wait for it; every rank then joins. The file carries a job token
+        (`job`, else :func:`job_token` from the launcher's environment) and a rank accepts
+        only a file whose token is its own, so an id file left by an earlier run is never
+        read as this run's"""
+        job = job_token() if job is None else job
         if rank == 0:
             uid = unique_id(lib)
-            tmp = "%s.%d.tmp" % (path, os.getpid())
-            with open(tmp, "wb") as fh:
-                fh.write(uid)
-            os.replace(tmp, path)
+            write_id_file(path, uid, job)
         else:
-            t0 = time.monotonic()
-            while not os.path.exists(path):
-                if time.monotonic() - t0 > timeout:
-                    raise TimeoutError("no RCCL unique id at %s after %.0f s" % (path, timeout))
-                time.sleep(0.01)
-            with open(path, "rb") as fh:
-                uid = fh.read()
+            uid = read_id_file(path, job, timeout)
         return cls(rank, world, uid, lib)
 
     @classmethod

@@ -186,6 +186,11 @@ class ParabolicKL:
         m = np.clip((WIN_NODES - span) // 2, 0, margin)
         wlo = np.maximum(a - m, 0)
         whi = np.minimum(np.minimum(b + m, n), wlo + WIN_NODES)
+        # one thread per node of the tile's bucket 0 and its in-tile 3- / 4-edge nodes: a
+        # 256-thread block (gtf_kl.hip) would skip any beyond 256 without an error
+        if nt and int((n0 + n3 + n4).max()) > 256:
+            raise ValueError("KL tile with %d one- to four-edge nodes (the block handles at most 256)"
+                             % int((n0 + n3 + n4).max()))
         recs = np.stack([a, n0, n1, n3, n4, z, sp[a], pr & 0xFFFFFFFF, pr >> 32, wlo, whi, z], 1)
         recs = np.where(recs >= 2**31, recs - 2**32, recs)   # low words as int32 bits
         return recs.astype(np.int32).reshape(-1)

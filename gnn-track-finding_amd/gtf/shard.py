@@ -314,12 +314,15 @@ class ShardedDeviceGraph:
             from .comm import NativeComm
             if comm is None:
                 import torch.distributed as dist
-                if dist.is_available() and dist.is_initialized():
-                    comm = NativeComm.from_torch(group, lib=d.lib)
-                elif world == 1:
-                    comm = NativeComm.single(lib=d.lib)
-                else:
-                    raise ValueError("backend 'native' with world > 1 needs a NativeComm (gtf.comm) or torch.distributed")
+                # gtf_comm_init binds RCCL to the CURRENT HIP device: make this rank's current
+                with torch.cuda.device(torch.device(dev)):
+                    if dist.is_available() and dist.is_initialized():
+                        comm = NativeComm.from_torch(group, lib=d.lib)
+                    elif world == 1:
+                        comm = NativeComm.single(lib=d.lib)
+                    else:
+                        raise ValueError("backend 'native' with world > 1 needs a NativeComm (gtf.comm) or "
+                                         "torch.distributed")
             if comm.world != world or comm.rank != rank:
                 raise ValueError("NativeComm is rank %d of %d, the shard rank %d of %d" % (comm.rank, comm.world, rank, world))
             self.comm = comm
@@ -558,6 +561,10 @@ class SplitDeviceGraph:
         half's pack and runs both unpacks, and the second stream then waits for it -- one
         cross-stream dependency at a time (the mutual mid-capture waits of the default form
         crash hipStreamEndCapture on this stack, profiles/r04/capture/)."""
+        if not linear and self.torch.cuda.is_current_stream_capturing():
+            # the joined form's mutual mid-capture waits crash hipStreamEndCapture on this stack:
+            # a capture always records the one-way (linear) form, which replays bit-equal
+            linear = True
         (a, b), (sa, sb) = self.parts, self.streams
         packed, done = self._ev
         for r, sd in enumerate(self.parts):

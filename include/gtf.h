@@ -559,9 +559,14 @@ typedef struct gtf_kl_graph {
     /* tiled layout (gtf.parabolic.ParabolicKL(tile=T)): the nodes azimuth-sorted per event and
      * cut into tiles of <= 256 one- / two-edge (bucket-0) nodes and the nodes between them, bucket
      * 0 first inside a tile (one-edge, then two-edge nodes, consecutive slots and one pair each).
-     * One 256-thread block per tile record of 12 int32: (first node, bucket-0 count, its one-edge
-     * count, 0, 0, 0, bucket 0's first slot, its first pair low / high 32 bits, window [lo, hi) of
-     * at most 1024 consecutive nodes holding the tile's neighbours, 0); the block loads its
+     * One 256-thread block per tile record of 12 int32: (first node, bucket-0 count n0, its
+     * one-edge count, the in-tile three-edge count n3, the in-tile four-edge count n4, 0, bucket
+     * 0's first slot, its first pair low / high 32 bits, window [lo, hi) of at most 1024
+     * consecutive nodes holding the tile's neighbours, 0); the n3 three-edge and then n4
+     * four-edge nodes follow the tile's bucket-0 nodes (slots and pairs consecutive) and run in
+     * the tile's block, one thread per node, so n0 + n3 + n4 <= 256 (the block skips nodes past
+     * 256 without an error; gtf.parabolic.ParabolicKL._block_table refuses such tiles). n3 and
+     * n4 must be 0 when list[1] is given (bucket 1 then runs by list). The block loads its
      * sender lists and the window's x, y and truth ids in one round and reads the neighbours from
      * LDS. Buckets 1..3 come from list[1..3] / count[1..3] (count[0] and list[0] are ignored). The
      * library clamps each window to its LDS size but does not check the records' node, slot and

@@ -59,6 +59,7 @@ def test_native_comm_world1_tags_equal_reference():
 def test_native_comm_id_through_a_file(tmp_path):
     """the framework-free id hand-off (rank 0 writes, the others read): one rank here"""
     from gtf.comm import NativeComm
-    comm = NativeComm.from_file(str(tmp_path / "uid"), 0, 1)
-    assert (tmp_path / "uid").stat().st_size == 128
+    from gtf.comm import read_id_file
+    comm = NativeComm.from_file(str(tmp_path / "uid"), 0, 1, job="test-job")
+    assert len(read_id_file(str(tmp_path / "uid"), "test-job", timeout=1.0)) == 128
     comm.close()

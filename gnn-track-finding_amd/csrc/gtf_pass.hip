@@ -15,6 +15,7 @@
 //                     these stages fuse into one launch with no inter-node traffic.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "../../include/gtf.h"
@@ -36,9 +37,17 @@ struct Ws {
     uint32_t* err;    // error word (the workspace's first bytes; gtf_diag at GTF_DIAG_OFFSET)
     double* vc;       // [S] per active edge, by SLOT: the merged_cov[1,1] its extrapolation sees
     const gtf_diag* diag;   // optional diagnostics outputs (gtf_set_diagnostics), in the workspace
+    uint32_t* queue;  // the persistent node kernel's work-queue counters (WS_QUEUES, 128 B apart)
 };
 
 __host__ inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+// workspace header: [0, 256) error word + gtf_diag, [256, WS_HEAD) the node kernel's
+// work-queue counters -- zero between launches (gtf_workspace_init zeroes them once; every
+// launch leaves them zero: the wave that draws a queue's last ticket resets it)
+constexpr int WS_QUEUES = 64;
+constexpr int WS_QSTRIDE = 32;   // uint32 words between two counters: one 128-byte line each
+constexpr size_t WS_HEAD = 256 + (size_t)WS_QUEUES * WS_QSTRIDE * sizeof(uint32_t);
 
 __host__ inline Ws carve(void* base, int32_t n_nodes, int32_t n_slots) {
     (void)n_nodes;
@@ -46,8 +55,8 @@ __host__ inline Ws carve(void* base, int32_t n_nodes, int32_t n_slots) {
     Ws w;
     w.err = (uint32_t*)p;
     w.diag = (const gtf_diag*)(p + GTF_DIAG_OFFSET);
-    p += 256;
-    w.vc = (double*)p;
+    w.queue = (uint32_t*)(p + 256);
+    w.vc = (double*)(p + WS_HEAD);
     return w;
 }
 
@@ -950,6 +959,41 @@ int launch_ops(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* ut
     return err == hipSuccess ? 0 : fail("node kernel launch", err);
 }
 
+// the persistent node kernel (k_node_persist) unless GTF_NODE_PERSIST=0 in the environment
+// (A/B runs; the launch-per-item form k_node_multi is bit-identical)
+bool node_persist_enabled() {
+    static const bool on = [] {
+        const char* v = getenv("GTF_NODE_PERSIST");
+        return !(v && v[0] == '0');
+    }();
+    return on;
+}
+
+// resident blocks of a persistent kernel on the current device: CUs x blocks per CU (its
+// occupancy), at most one block per 4 items, at least 8 (every work queue needs waves)
+int persist_grid(const void* kernel, int items) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    static int cus[64] = {0};
+    int& c = cus[dev & 63];
+    if (c == 0 && hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) c = 256;
+    static const void* ks[16] = {nullptr};   // occupancy per kernel, asked once
+    static int occ[16] = {0};
+    int per_cu = 0;
+    for (int i = 0; i < 16 && ks[i]; i++)
+        if (ks[i] == kernel) per_cu = occ[i];
+    if (per_cu == 0) {
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, NBLOCK, 0) != hipSuccess || per_cu < 1)
+            per_cu = 1;
+        for (int i = 0; i < 16; i++)
+            if (!ks[i]) { ks[i] = kernel; occ[i] = per_cu; break; }
+    }
+    int grid = c * per_cu;
+    const int need = (items + NODE_WPB - 1) / NODE_WPB;
+    if (grid > need) grid = need;
+    return grid < 8 ? 8 : grid;
+}
+
 // compile-time op sequence (the stage entry points)
 template <int... OPS>
 int launch_seq(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts, gtf_edges* e, const gtf_params* p,
@@ -992,9 +1036,20 @@ int launch_seq(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* ut
                 bk.blocks[q] = (bk.count[q] + NBLOCK / gs[q] - 1) / (NBLOCK / gs[q]);
                 total += bk.blocks[q];
             }
+            // persistent form: one work item per wavefront's worth of lane groups, in bucket order
+            int items = 0;
+            for (int q = 0; q < 6; q++) {
+                bk.wstart[q] = items;
+                items += (bk.count[q] + 64 / gs[q] - 1) / (64 / gs[q]);
+            }
+            bk.wstart[6] = items;
+            const bool persist = node_persist_enabled() && g->pad_tiles == 0;
             if (g->pack_ent && g->pack_wave && g->n_pack_waves > 0)   // every <= 64-slot node, packed
                 hipLaunchKernelGGL((k_node_pack<OPS...>), dim3((g->n_pack_waves + NBLOCK / 64 - 1) / (NBLOCK / 64)),
                                    dim3(NBLOCK), 0, st, *g, *n, T, U, *e, *p, w, chi2, kl);
+            else if (persist && items > 0)
+                hipLaunchKernelGGL((k_node_persist<OPS...>), dim3(persist_grid((const void*)k_node_persist<OPS...>, items)),
+                                   dim3(NBLOCK), 0, st, NodeKArgs{*g, *n, T, U, *e, *p, w, chi2, kl, bk});
             else if (total > 0)
                 hipLaunchKernelGGL((k_node_multi<OPS...>), dim3(total), dim3(NBLOCK), 0, st,
                                    NodeKArgs{*g, *n, T, U, *e, *p, w, chi2, kl, bk});
@@ -1064,11 +1119,12 @@ extern "C" {
 
 size_t gtf_workspace_bytes(int32_t n_nodes, int32_t n_slots) {
     (void)n_nodes;
-    return 256 + align256(sizeof(double) * (size_t)(n_slots > 0 ? n_slots : 1));
+    return WS_HEAD + align256(sizeof(double) * (size_t)(n_slots > 0 ? n_slots : 1));
 }
 
 int gtf_workspace_init(void* ws, gtf_stream_t stream) {
-    hipError_t e = hipMemsetAsync(ws, 0, 256, (hipStream_t)stream);   // error word + gtf_diag (no diagnostics)
+    // error word + gtf_diag (no diagnostics) + the node kernel's work-queue counters
+    hipError_t e = hipMemsetAsync(ws, 0, WS_HEAD, (hipStream_t)stream);
     return e == hipSuccess ? 0 : fail("workspace init", e);
 }
 

@@ -209,8 +209,11 @@ enum {
 };
 
 /* Workspace: caller allocates gtf_workspace_bytes() bytes of device memory and initialises
- * it once with gtf_workspace_init (or allocates it zeroed). Its first 256 bytes are a
- * header: the error word at offset 0, the gtf_diag record at GTF_DIAG_OFFSET. */
+ * it once with gtf_workspace_init (or allocates it zeroed). Its first 8448 bytes are a
+ * header: the error word at offset 0, the gtf_diag record at GTF_DIAG_OFFSET, and from byte
+ * 256 the fused node kernel's work-queue counters (the kernel leaves them zero at the end of
+ * every launch; only gtf_workspace_init or a zeroed allocation sets them up). One pass at a
+ * time per workspace. */
 size_t gtf_workspace_bytes(int32_t n_nodes, int32_t n_slots);
 
 /* Zero the whole header (stream-ordered): no error flags, no diagnostics registered.

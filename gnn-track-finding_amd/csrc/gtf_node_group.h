@@ -141,6 +141,40 @@ struct Grp<0> {
     __device__ __forceinline__ int stage_base() const { return gbase; }
 };
 
+// Correctly rounded reciprocals 1/n (n = 1..64) in LDS: the persistent node kernel fills the
+// table once per block, and the ops' integer reciprocals (priors 1/count, mixture weights
+// 1/count, the side norm's divisor through qdiv) read it instead of running an fp64 division
+// (~10 VALU instructions each) -- the same bits (the table holds 1.0 / n itself)
+#ifndef GTF_RCP_TABLE
+#define GTF_RCP_TABLE 1
+#endif
+__shared__ double g_rcp_lds[65];
+// (i, j) of lower-triangle pair t (pair_ij) for t < 120 (15 states: 105 pairs), i | j << 8:
+// the clustering's pair loop reads its pairs here instead of solving t = i (i - 1) / 2 + j
+// (a float square root and two correction loops, ~40 VALU instructions per pair)
+__shared__ uint16_t g_pair_lds[120];
+// every node kernel fills both tables at its start, before its block barrier
+__device__ __forceinline__ void node_tables_init() {
+#if GTF_RCP_TABLE
+    const int t = (int)threadIdx.x;
+    if (t < 65) g_rcp_lds[t] = t ? 1.0 / (double)t : 0.0;
+    if (t < 120) {
+        int i, j;
+        pair_ij(t, i, j);
+        g_pair_lds[t] = (uint16_t)(i | (j << 8));
+    }
+#endif
+}
+__device__ __forceinline__ void pair_of(int t, int& i, int& j) {
+#if GTF_RCP_TABLE
+    const int e = g_pair_lds[t];
+    i = e & 0xff;
+    j = e >> 8;
+#else
+    pair_ij(t, i, j);
+#endif
+}
+
 // per-lane (per-slot) registers of one state dict
 enum : uint8_t { D_RANK = 1, D_MW = 2, D_PRIOR = 4 };  // LaneDict.dirty: fields to store
 
@@ -181,7 +215,15 @@ struct NodeCtx {
     double xa, za, ra;         // node attribute xyzr x, z, r (clustering tau geometry)
     uint8_t solo;              // node alone in its subgraph (mixture weights)
     bool staged;               // clustering operands already in the group's LDS stage (slot lanes)
+    int lri;                   // the side norm's divisor as an integer (1 for lr = 1.0)
 };
+
+// 1.0 / n for a count n >= 1 (<= 64): the LDS table or a division
+template <int G>
+__device__ __forceinline__ double rcp_count(const NodeCtx<G>& c, int n) {
+    (void)c;
+    return GTF_RCP_TABLE ? g_rcp_lds[n] : 1.0 / (double)n;
+}
 
 // highest set bit index of m (m != 0)
 __device__ __forceinline__ int hibit(unsigned long long m) { return 63 - __clzll((long long)m); }
@@ -219,11 +261,20 @@ __device__ __forceinline__ int dict_pos(const NodeCtx<G>& c, LaneDict& st) {
 #ifndef GTF_CHUNKED_SUM
 #define GTF_CHUNKED_SUM 1
 #endif
+#ifndef GTF_SUM_ZFILL
+#define GTF_SUM_ZFILL 1
+#endif
 template <int G>
 __device__ __forceinline__ double ordered_sum(NodeCtx<G>& c, double* sval, LaneDict& st, bool take,
                                              double term) {
     const int pos = dict_pos(c, st);
     const int npres = c.grp.count(c.valid && st.rank >= 0);
+#if GTF_SUM_ZFILL
+    // the group's line zeroed first (every lane its own entry), then the terms at their dict
+    // positions (the same wave's LDS stores land in issue order): the entries past the last
+    // key read +0.0, so the chunked sum needs no per-entry select
+    if constexpr (G > 0) sval[c.grp.gbase + c.grp.gl] = 0.0;
+#endif
     if (pos >= 0) sval[c.grp.gbase + pos] = take ? term : 0.0;
     wave_lds_sync();
     double s = 0.0;
@@ -237,7 +288,7 @@ __device__ __forceinline__ double ordered_sum(NodeCtx<G>& c, double* sval, LaneD
 #pragma unroll
         for (int j = 0; j < CH; j++) v[j] = sval[c.grp.gbase + i + j];
 #pragma unroll
-        for (int j = 0; j < CH; j++) s = s + ((i + j < npres) ? v[j] : 0.0);
+        for (int j = 0; j < CH; j++) s = s + ((GTF_SUM_ZFILL && G > 0) || i + j < npres ? v[j] : 0.0);
     }
 #else
     for (int i = 0; i < npres; i++) s = s + sval[c.grp.gbase + i];
@@ -313,7 +364,7 @@ __device__ __forceinline__ void g_priors(NodeCtx<G>& c, LaneDict& st, double* sv
     const bool act = lane_active(c, st.rank);
     const unsigned long long A = c.grp.bits(act);
     if (act) {
-        st.prior = 1.0 / (double)__popcll(A & c.same_layer);
+        st.prior = rcp_count(c, __popcll(A & c.same_layer));
         st.dirty |= D_PRIOR;
     }
 }
@@ -391,6 +442,7 @@ __device__ __forceinline__ void g_reweight(NodeCtx<G>& c, double* sval, const gt
         if (!last_is_edge && c.grp.gl == 0) raise_node(err, c.v, GTF_ERR_STALE_KEY_NO_EDGE);
         if (act) {
             c.side = left ? 0 : 1;
+            c.lri = (last_is_edge && last_act == 1) ? (left ? dl : dr) : 1;
             c.lr = (last_is_edge && last_act == 1) ? (double)(left ? dl : dr) : 1.0;
             c.uts_dirty_lr = true;
         }
@@ -398,7 +450,7 @@ __device__ __forceinline__ void g_reweight(NodeCtx<G>& c, double* sval, const gt
     const double denom = ordered_sum(c, sval, st, act, st.mw * c.lik);
     if (act) {
         double wgt = (st.mw * c.lik * st.prior) / denom;
-        wgt = wgt / c.lr;
+        wgt = GTF_RCP_TABLE ? qdiv(wgt, c.lr, g_rcp_lds[c.lri]) : wgt / c.lr;   // (lr = lri exactly)
         st.mw = wgt;
         st.dirty |= D_MW;
         c.edge_mw = wgt;
@@ -437,7 +489,7 @@ __device__ __forceinline__ void g_mixture_weights(NodeCtx<G>& c, LaneDict& st, b
         return;
     }
     if (c.valid && st.rank >= 0) {
-        st.mw = 1.0 / (double)cnt;
+        st.mw = rcp_count(c, cnt);
         st.dirty |= D_MW;
     }
 }
@@ -627,7 +679,7 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const int tu = t + u * step;
-            pair_ij(tu < npairs ? tu : t, iv[u], jv[u]);
+            pair_of(tu < npairs ? tu : t, iv[u], jv[u]);
             Dv[u] = pair_d(iv[u], jv[u]);
         }
 #pragma unroll
@@ -637,7 +689,7 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
 #else
     for (int t = c.grp.gl; t < npairs; t += c.grp.size()) {
         int i, j;
-        pair_ij(t, i, j);
+        pair_of(t, i, j);
         fold(pair_d(i, j), t, i, j);
     }
 #endif
@@ -656,8 +708,8 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
     const int t1 = c.grp.min_i(tl ? (lt0 == t0 ? lt1 : lt0) : (1 << 20));
     const unsigned tiemask = c.grp.or_u(tl ? lmask : 0u);
     int ti0, tj0, ti1 = 0, tj1;
-    pair_ij(t0, ti0, tj0);
-    if (t1 < (1 << 20)) pair_ij(t1, ti1, tj1);
+    pair_of(t0, ti0, tj0);
+    if (t1 < (1 << 20)) pair_of(t1, ti1, tj1);
     // merged pair = (idx[0], idx[1]) of concatenate((rows, cols)) (:231-233)
     const int p0 = ti0, p1 = (t1 < (1 << 20)) ? ti1 : tj0;
 #if GTF_KL_LEAN
@@ -891,6 +943,7 @@ __device__ __forceinline__ bool node_fields(NodeCtx<G>& c, const gtf_graph& g, c
     c.lik = 0; c.lr = 0; c.edge_mw = 0; c.side = -1; c.fresh = 0;
     c.uts_dirty_lr = false; c.edge_mw_dirty = false; c.degree = 0; c.degree_set = false;
     c.staged = false;
+    c.lri = 1;
 #if GTF_HOIST
     // the node's own scalars, in the same round of loads as the slot fields (loaded inside
     // an op, after its LDS fences, each one's latency would add to every wave's life)
@@ -961,11 +1014,17 @@ __device__ __forceinline__ void node_flush(NodeCtx<G>& c, gtf_states& tse, gtf_s
     c.uts_dirty_lr = false;
 }
 
+#ifndef GTF_ASM_MARK
+#define GTF_ASM_MARK 0   // assembly-listing builds only: a comment line before every op (tools/asm_ops.py)
+#endif
 template <int G, int OP, typename Stage>
 __device__ __forceinline__ void node_op(NodeCtx<G>& c, const gtf_graph& g, gtf_nodes& n, gtf_states& tse,
                                         gtf_states& uts, gtf_edges& e, const gtf_params& p, const Ws& w,
                                         double* sval, Stage* stg, double chi2_thr, double kl_thr, bool has_tse,
                                         bool has_uts) {
+#if GTF_ASM_MARK
+    asm volatile("; GTF_OP_MARK G=%0 OP=%1" ::"i"(G), "i"(OP));
+#endif
     if constexpr (OP == OP_FLUSH) node_flush(c, tse, uts, e);
     if constexpr (OP == OP_FRESH) g_fresh(c);
     if constexpr (OP == OP_RANKS) g_ranks(c);
@@ -1101,7 +1160,13 @@ __device__ __forceinline__ void node_seq_body(const gtf_graph& g, gtf_nodes& n, 
 #else
     (node_op<G, OPS, Stage>(c, g, n, tse, uts, e, p, w, sval, stg, chi2_thr, kl_thr, has_tse, has_uts), ...);
 #endif
+#if GTF_ASM_MARK
+    asm volatile("; GTF_OP_MARK G=%0 OP=99" ::"i"(G));
+#endif
     node_store(c, n, tse, uts, e);
+#if GTF_ASM_MARK
+    asm volatile("; GTF_OP_MARK G=%0 OP=100" ::"i"(G));
+#endif
 #if GTF_OP_TIMING
     {
         const uint64_t t = __builtin_readcyclecounter();
@@ -1191,6 +1256,8 @@ __global__ void __launch_bounds__(NBLOCK) GTF_NODE_WAVES_ATTR k_node_multi(NodeK
     // (gtf::xcd_local) made this kernel 35 % slower on config 4, presumably by putting
     // the costly nodes of a node range on one XCD.
     const KArgPtr A = node_kargs();
+    node_tables_init();
+    __syncthreads();
     int b = blockIdx.x;
 #ifndef GTF_NODE_ORDER
 #define GTF_NODE_ORDER 0   // 1 (diagnostics): the buckets by measured wave life, longest first (16, 32, 8, 64, 4, 2)
@@ -1300,6 +1367,8 @@ __global__ void __launch_bounds__(NBLOCK) GTF_NODE_WAVES_ATTR k_node_persist(Nod
     using Q = OpSeq<OPS...>;
     __shared__ __attribute__((aligned(16))) char smem[Q::cluster ? node_smem_bytes() : NBLOCK * sizeof(double)];
     const KArgPtr A = node_kargs();
+    node_tables_init();
+    __syncthreads();
     const int lane = (int)threadIdx.x & 63;
     const int xcd = (int)(blockIdx.x & 7);
     const int qid = xcd * NODE_WPB + ((int)threadIdx.x >> 6);
@@ -1368,6 +1437,8 @@ __global__ void __launch_bounds__(NBLOCK) k_node_pack(gtf_graph g, gtf_nodes n, 
     __shared__ __attribute__((aligned(16))) char smem[NBLOCK * sizeof(double) +
                                                       (Q::cluster ? (NBLOCK / 64) * sizeof(Stage) : 0)];
     __shared__ uint8_t s_start[NBLOCK];
+    node_tables_init();
+    __syncthreads();
     const int wv = blockIdx.x * (NBLOCK / 64) + (int)threadIdx.x / 64;
     if (wv >= g.n_pack_waves) return;  // wavefront-uniform
     const int lane = threadIdx.x & 63;
@@ -1412,6 +1483,8 @@ __global__ void __launch_bounds__(NBLOCK) k_node_group(gtf_graph g, gtf_nodes n,
     using Stage = StageT<G>;
     __shared__ double s_val[NBLOCK];
     __shared__ Stage s_stage[NBLOCK / G];
+    node_tables_init();
+    __syncthreads();
     NodeCtx<G> c;
     const int gi = (blockIdx.x * NBLOCK + (int)threadIdx.x) / G;
     const Need nd{(bool)ops.uses_tse, (bool)ops.uses_tse, (bool)ops.uses_uts, (bool)ops.uses_uts,

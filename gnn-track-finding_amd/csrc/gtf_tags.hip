@@ -329,11 +329,11 @@ static int hip_fail(const char* what) {
     return -1;
 }
 
-int gtf_tag_prepare(const gtf_graph* g, const double* radius, uint8_t* keep, uint8_t* processed,
-                    int32_t* n_processed, gtf_stream_t stream) {
-    if (int rc = gtf::check_abi(g, "gtf_tag_prepare")) return rc;
-    hipStream_t st = (hipStream_t)stream;
-    if (hipMemsetAsync(n_processed, 0, sizeof(int32_t), st) != hipSuccess) return hip_fail("gtf_tag_prepare");
+// zero_count: n_processed zeroed here (else the caller has)
+static int tag_prepare(const gtf_graph* g, const double* radius, uint8_t* keep, uint8_t* processed,
+                       int32_t* n_processed, bool zero_count, hipStream_t st) {
+    if (zero_count && hipMemsetAsync(n_processed, 0, sizeof(int32_t), st) != hipSuccess)
+        return hip_fail("gtf_tag_prepare");
     if (g->n_nodes > 0 && g->out_sched) {   // lane groups over the sender schedule
         PrepBuckets pb;
         const int cnt[3] = {g->n_o4, g->n_o8, g->n_o16}, gs[3] = {4, 8, 16};
@@ -361,6 +361,12 @@ int gtf_tag_prepare(const gtf_graph* g, const double* radius, uint8_t* keep, uin
         hipLaunchKernelGGL(k_count_flags, dim3(blocks), dim3(BLOCK), 0, st, processed, g->n_nodes, n_processed);
     }
     return hipGetLastError() == hipSuccess ? 0 : hip_fail("gtf_tag_prepare launch");
+}
+
+int gtf_tag_prepare(const gtf_graph* g, const double* radius, uint8_t* keep, uint8_t* processed,
+                    int32_t* n_processed, gtf_stream_t stream) {
+    if (int rc = gtf::check_abi(g, "gtf_tag_prepare")) return rc;
+    return tag_prepare(g, radius, keep, processed, n_processed, true, (hipStream_t)stream);
 }
 
 // flips: TAG_SHARDS counter words TAG_STRIDE apart (nsh = TAG_SHARDS, zeroed by the caller)
@@ -446,17 +452,21 @@ int gtf_tag_propagate(const gtf_graph* g, const double* radius, int64_t* tags, d
     w += tag_align(n);
     int64_t* other = reinterpret_cast<int64_t*>(w);
     *sweeps_out = 0;
-    if (hipMemsetAsync(hdr, 0, 4 * sizeof(int32_t), st) != hipSuccess) return hip_fail("gtf_tag_propagate");
-    if (int rc = gtf_tag_prepare(g, radius, keep, proc, hdr, stream)) return rc;
+    // the header words and the first pass over the ring's counters zeroed in one memset
+    const int32_t ring0 = max_sweeps < TAG_RING ? max_sweeps : TAG_RING;
+    if (hipMemsetAsync(hdr, 0, (64 + ring0 * TAG_CTR) * sizeof(int32_t), st) != hipSuccess)
+        return hip_fail("gtf_tag_propagate");
+    if (int rc = tag_prepare(g, radius, keep, proc, hdr, false, st)) return rc;
     int32_t s = 0, batch = 2, executed = 0;
-    int32_t host[4];
-    std::vector<int32_t> hring(TAG_RING * TAG_CTR);
+    std::vector<int32_t> host(64 + TAG_RING * TAG_CTR);   // the header words, then the ring
+    int32_t* hring = host.data() + 64;
     bool stopped = false;
     while (!stopped && s < max_sweeps) {
         const int32_t at = s % TAG_RING;
         int32_t nb = batch < max_sweeps - s ? batch : max_sweeps - s;
         if (nb > TAG_RING - at) nb = TAG_RING - at;   // the batch's counters stay contiguous in the ring
-        if (hipMemsetAsync(ring + at * TAG_CTR, 0, nb * TAG_CTR * sizeof(int32_t), st) != hipSuccess)
+        if (s >= TAG_RING &&   // (a later pass over the ring: its counters zeroed again)
+            hipMemsetAsync(ring + at * TAG_CTR, 0, nb * TAG_CTR * sizeof(int32_t), st) != hipSuccess)
             return hip_fail("gtf_tag_propagate: zeroing the flip counters");
         for (int32_t i = 0; i < nb; i++) {
             const int32_t q = s + i;
@@ -467,15 +477,15 @@ int gtf_tag_propagate(const gtf_graph* g, const double* radius, int64_t* tags, d
             if (int rc = tag_sweep(g, keep, proc, tin, tout, ring + (q % TAG_RING) * TAG_CTR, TAG_SHARDS, ctl, st))
                 return rc;
         }
-        if (hipMemcpyAsync(host, hdr, 4 * sizeof(int32_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
-            hipMemcpyAsync(hring.data() + at * TAG_CTR, ring + at * TAG_CTR, nb * TAG_CTR * sizeof(int32_t),
-                           hipMemcpyDeviceToHost, st) != hipSuccess ||
+        // one read-back: the header words through the batch's last counter
+        if (hipMemcpyAsync(host.data(), hdr, (64 + (at + nb) * TAG_CTR) * sizeof(int32_t), hipMemcpyDeviceToHost,
+                           st) != hipSuccess ||
             hipStreamSynchronize(st) != hipSuccess)
             return hip_fail("gtf_tag_propagate: reading the flip counts");
         executed = host[2];
         for (int32_t q = s; q < executed; q++) {
             int32_t f = 0;
-            const int32_t* c = hring.data() + (q % TAG_RING) * TAG_CTR;
+            const int32_t* c = hring + (q % TAG_RING) * TAG_CTR;
             for (int k = 0; k < TAG_SHARDS; k++) f += c[k * TAG_STRIDE];
             if (flips_out) flips_out[q] = f;
             // the rule on the host too: the batch's last executed sweep may already stop it

@@ -619,9 +619,11 @@ def bench_sharded(workload, rank, world, dev, steps, warmup, params, backend="nc
         for i in range(steps):
             sd.d.use_inputs(i)
             if exchange:
-                sd.step(params)
+                sd.step(params)   # (the previous step's halo exchanged beside this pass's phase 1a)
             else:
                 sd.pass_(params, events=handles[i] if instrumented else None)
+        if exchange:
+            sd.flush()     # the last pass's halo, inside the timed region
         t_issue = time.perf_counter() - t0     # host time to enqueue the K steps
         torch.cuda.synchronize()
         dist.barrier()
@@ -684,6 +686,9 @@ def bench_sharded(workload, rank, world, dev, steps, warmup, params, backend="nc
             "host_issue_ms_per_step_no_exchange": issue[False] / steps * 1e3,
             "host_issue_note": "host time to enqueue the steps (max over ranks); close to ms_per_step = host-bound",
             "halo_bytes_per_rank_max": hb, "owned_slots_max": pl.cap_slots,
+            "overlap": ("the halo exchange of pass i beside pass i+1's phase 1a (the senders whose state and "
+                        "out-edge activations are all the rank's own, and the slots they send to; gtf_shard.phases)"),
+            "rank0_split": sd.split_sizes,
             "owned_slots_min": int((pl.slot_hi - pl.slot_lo).min()),
             "owned_directed_edges_max": own_edges_max, "owned_nodes_max": own_nodes_max,
             "collective": ("gtf_halo_exchange: per-destination halo segments, grouped ncclSend / ncclRecv inside "

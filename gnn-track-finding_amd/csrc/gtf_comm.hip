@@ -126,13 +126,12 @@ int gtf_comm_destroy(gtf_comm* comm) {
 int gtf_comm_rank(const gtf_comm* comm) { return comm ? comm->rank : -1; }
 int gtf_comm_size(const gtf_comm* comm) { return comm ? comm->nranks : -1; }
 
-int gtf_halo_exchange(gtf_comm* comm, gtf_nodes* n, gtf_edges* e, const gtf_halo* send, const gtf_halo* recv,
-                      void* send_buf, void* recv_buf, const int64_t* send_bytes, const int64_t* recv_bytes,
-                      gtf_stream_t stream) {
-    if (!comm || !send_bytes || !recv_bytes) return fail("gtf_halo_exchange: bad arguments");
-    if (int rc = gtf_halo_pack(n, e, send, send_buf, stream)) return rc;
+// the all-to-all of the halo segments: per-destination segments back to back, in rank
+// order, on both sides (grouped ncclSend / ncclRecv on `stream`)
+int gtf_halo_alltoall(gtf_comm* comm, const void* send_buf, void* recv_buf, const int64_t* send_bytes,
+                      const int64_t* recv_bytes, gtf_stream_t stream) {
+    if (!comm || !send_bytes || !recv_bytes) return fail("gtf_halo_alltoall: bad arguments");
     hipStream_t st = (hipStream_t)stream;
-    // the all-to-all: per-destination segments back to back, in rank order, on both sides
     int64_t so = 0, ro = 0;
     ncclResult_t r = g_rccl.group_start();
     for (int p = 0; p < comm->nranks && r == ncclSuccess; p++) {
@@ -144,8 +143,17 @@ int gtf_halo_exchange(gtf_comm* comm, gtf_nodes* n, gtf_edges* e, const gtf_halo
         ro += recv_bytes[p];
     }
     const ncclResult_t r2 = g_rccl.group_end();
-    if (r != ncclSuccess) return nccl_fail("gtf_halo_exchange send/recv", r);
-    if (r2 != ncclSuccess) return nccl_fail("gtf_halo_exchange group", r2);
+    if (r != ncclSuccess) return nccl_fail("gtf_halo_alltoall send/recv", r);
+    if (r2 != ncclSuccess) return nccl_fail("gtf_halo_alltoall group", r2);
+    return 0;
+}
+
+int gtf_halo_exchange(gtf_comm* comm, gtf_nodes* n, gtf_edges* e, const gtf_halo* send, const gtf_halo* recv,
+                      void* send_buf, void* recv_buf, const int64_t* send_bytes, const int64_t* recv_bytes,
+                      gtf_stream_t stream) {
+    if (!comm || !send_bytes || !recv_bytes) return fail("gtf_halo_exchange: bad arguments");
+    if (int rc = gtf_halo_pack(n, e, send, send_buf, stream)) return rc;
+    if (int rc = gtf_halo_alltoall(comm, send_buf, recv_buf, send_bytes, recv_bytes, stream)) return rc;
     return gtf_halo_unpack(n, e, recv, recv_buf, stream);
 }
 

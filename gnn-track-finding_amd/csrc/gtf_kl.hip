@@ -227,9 +227,24 @@ constexpr size_t stage_bytes(int G, size_t t) { return (size_t)(BLOCK / G) * G *
 // one node per group of G lanes; states staged in LDS when d <= G (always, except in
 // the wavefront bucket beyond 64 in-edges, where pair lanes recompute both states)
 // node v on G lanes (lane gl), its states staged at stg
+// (i, j) of pair t < 120 (i | j << 8) in LDS, filled by the block of a lane-group bucket
+// (pair_table_fill): read instead of solved per pair (a float square root and two
+// correction loops, ~40 VALU instructions)
+constexpr int PTAB = 120;
+__device__ __forceinline__ void pair_table_fill(uint16_t* tab) {
+    for (int t = (int)threadIdx.x; t < PTAB; t += BLOCK) {
+        int i, j;
+        gtf::pair_ij(t, i, j);
+        tab[t] = (uint16_t)(i | (j << 8));
+    }
+    if (BLOCK == 64) gtf::wave_lds_sync();
+    else __syncthreads();
+}
+
 template <typename T, int G, bool STATES, typename S>
 __device__ __forceinline__ void pkl_node_core(const gtf_kl_graph& g, const gtf_kl_out& o, const S& src, int v, int lo,
-                                              int d, int64_t base, int gl, KlStage<T, G>* stg) {
+                                              int d, int64_t base, int gl, KlStage<T, G>* stg,
+                                              const uint16_t* ptab = nullptr) {
     if (d < 1) return;
     const Frame f = node_frame_xy(src.x(v), src.y(v));
 
@@ -279,7 +294,13 @@ __device__ __forceinline__ void pkl_node_core(const gtf_kl_graph& g, const gtf_k
     T* kl = (T*)o.kl;
     for (int t = gl; t < np; t += G) {
         int i, j;
-        gtf::pair_ij(t, i, j);
+        if (ptab && np <= PTAB) {   // (np: group-uniform)
+            const int e = ptab[t];
+            i = e & 0xff;
+            j = e >> 8;
+        } else {
+            gtf::pair_ij(t, i, j);
+        }
         PState<T> a, b;
         long long ti = 0, tj = 0;
         if (d <= G) {
@@ -300,20 +321,21 @@ __device__ __forceinline__ void pkl_node_core(const gtf_kl_graph& g, const gtf_k
 
 template <typename T, int G, bool STATES, typename S>
 __device__ __forceinline__ void pkl_node_body(const gtf_kl_graph& g, const gtf_kl_out& o, const S& src, int v, int gl,
-                                              KlStage<T, G>* stg) {
+                                              KlStage<T, G>* stg, const uint16_t* ptab = nullptr) {
     const int lo = g.slot_ptr[v], d = g.slot_ptr[v + 1] - lo;
     if (d < 1) return;
-    pkl_node_core<T, G, STATES>(g, o, src, v, lo, d, g.pair_ptr[v], gl, stg);
+    pkl_node_core<T, G, STATES>(g, o, src, v, lo, d, g.pair_ptr[v], gl, stg, ptab);
 }
 
 template <typename T, int G, bool STATES>
 __device__ __forceinline__ void pkl_node(const gtf_kl_graph& g, const gtf_kl_out& o, const int32_t* list, int count,
-                                         int bid, char* smem, int first = 0, int tid = -1) {
+                                         int bid, char* smem, int first = 0, int tid = -1,
+                                         const uint16_t* ptab = nullptr) {
     if (tid < 0) tid = (int)threadIdx.x;   // (tid: the thread in a BLOCK-thread (sub)block)
     const int gi = (bid * BLOCK + tid) / G;
     if (gi >= count) return;  // group-uniform
     const int v = list ? list[gi] : first + gi;   // (ordered layout: the bucket is a node range)
-    pkl_node_body<T, G, STATES>(g, o, GSrc(g), v, tid & (G - 1), (KlStage<T, G>*)smem + tid / G);
+    pkl_node_body<T, G, STATES>(g, o, GSrc(g), v, tid & (G - 1), (KlStage<T, G>*)smem + tid / G, ptab);
 }
 
 // d <= 2: one thread per node, both states in registers (the bulk of a TrackML
@@ -638,14 +660,14 @@ __device__ __forceinline__ void pkl_node4l_runs(const gtf_kl_graph& g, const gtf
 // ... and bucket-2 group gi (runs of 5, 6, 7, 8 in-edges) on G = 8 lanes
 template <typename T, bool STATES>
 __device__ __forceinline__ void pkl_node8_runs(const gtf_kl_graph& g, const gtf_kl_out& o, const KlBuckets& bk, int bid,
-                                               char* smem) {
+                                               char* smem, const uint16_t* ptab = nullptr) {
     const int gi = (bid * BLOCK + (int)threadIdx.x) / 8;
     if (gi >= g.count[2]) return;   // group-uniform
     const int k = gi >= bk.r2[3] ? 3 : gi >= bk.r2[2] ? 2 : gi >= bk.r2[1] ? 1 : 0;
     const int d = 5 + k, i = gi - bk.r2[k];
     pkl_node_core<T, 8, STATES>(g, o, GSrc(g), g.first[2] + gi, (int)(bk.slot2[k] + (int64_t)i * d), d,
                                 bk.pair2[k] + (int64_t)i * (d * (d - 1) / 2), (int)threadIdx.x & 7,
-                                (KlStage<T, 8>*)smem + (int)threadIdx.x / 8);
+                                (KlStage<T, 8>*)smem + (int)threadIdx.x / 8, ptab);
 }
 
 // one launch over the four buckets; wavefront-bucket blocks first (longest-running)
@@ -701,14 +723,19 @@ __global__ void __launch_bounds__(BLOCK) KL_ATTR k_parabolic_kl(gtf_kl_graph g, 
         }
         b = (upto - 1) * 8 + x;
     }
+    __shared__ uint16_t s_pair[PTAB];   // (filled by the lane-group buckets' blocks only)
     if (b < bk.blocks[3]) {
-        pkl_node<T, 64, STATES>(g, o, g.list[3], g.count[3], gtf::xcd_local(b, bk.blocks[3]), smem, g.first[3]);
+        pair_table_fill(s_pair);
+        pkl_node<T, 64, STATES>(g, o, g.list[3], g.count[3], gtf::xcd_local(b, bk.blocks[3]), smem, g.first[3], -1,
+                                s_pair);
         return;
     }
     b -= bk.blocks[3];
     if (b < bk.blocks[2]) {
-        if (bk.runs) pkl_node8_runs<T, STATES>(g, o, bk, gtf::xcd_local(b, bk.blocks[2]), smem);
-        else pkl_node<T, 8, STATES>(g, o, g.list[2], g.count[2], gtf::xcd_local(b, bk.blocks[2]), smem, g.first[2]);
+        pair_table_fill(s_pair);
+        if (bk.runs) pkl_node8_runs<T, STATES>(g, o, bk, gtf::xcd_local(b, bk.blocks[2]), smem, s_pair);
+        else pkl_node<T, 8, STATES>(g, o, g.list[2], g.count[2], gtf::xcd_local(b, bk.blocks[2]), smem, g.first[2],
+                                    -1, s_pair);
         return;
     }
     b -= bk.blocks[2];

@@ -534,7 +534,8 @@ __device__ __forceinline__ void g_ranks(NodeCtx<G>& c) {
 // which keys are present and in what order (GTF_EARLY_STAGE).
 template <int CAP>
 #ifndef GTF_STAGE_NOINV
-#define GTF_STAGE_NOINV 2   // (with GTF_KL_LEAN) no inverses in LDS: 1 = in the owning lane's registers,
+#define GTF_STAGE_NOINV 3   // (with GTF_KL_LEAN) 3 = 2x2-block inverses staged after the pair loop (below);
+                            // no inverses in LDS: 1 = in the owning lane's registers,
                             // 2 = recomputed from the staged covariances where used
 #endif
 struct StageT {
@@ -544,6 +545,9 @@ struct StageT {
     double i00[CAP], i01[CAP], i10[CAP], i11[CAP], i22[CAP];
 #endif
     double q[CAP], w[CAP], tg[CAP], prior[CAP];   // (early staging parks x, z, r in q, w, tg)
+#if GTF_STAGE_NOINV == 3
+    double x4[CAP];   // with q, w, tg after the pair loop: the state's 2x2-block inverse
+#endif
     uint8_t ec[CAP];  // neighbour in the endcap (|x| >= boundary): picks its sigma_z / sigma_r pair
     uint8_t ord[CAP]; // slot lane of the state at each dict position
 };
@@ -720,7 +724,20 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
     double mm[4];
     Cov5 mc;
     const int l0 = sb + stg->ord[sb + p0], l1 = sb + stg->ord[sb + p1];
-#if GTF_STAGE_NOINV == 2
+#if GTF_STAGE_NOINV == 3
+    // every present state's 2x2-block inverse (np.linalg.inv of its covariance: the same value
+    // wherever the reference recomputes it) computed once and staged in the tau-geometry
+    // entries the pair loop has finished with (q, w, tg) and x4; only its (2, 2) entry
+    // 1 / c22 is recomputed where used: one division instead of three per use
+    wave_lds_sync();   // (every lane's pair loop has read its q, w, tg)
+    if (pres) {
+        double i00, i01, i10, i11;
+        inv2(stg->c00[me_l], stg->c01[me_l], stg->c10[me_l], stg->c11[me_l], i00, i01, i10, i11);
+        stg->q[me_l] = i00; stg->w[me_l] = i01; stg->tg[me_l] = i10; stg->x4[me_l] = i11;
+    }
+    wave_lds_sync();
+    auto inv_of = [&](int l) { return Cov5{stg->q[l], stg->w[l], stg->tg[l], stg->x4[l], 1.0 / stg->c22[l]}; };
+#elif GTF_STAGE_NOINV == 2
     // inverses recomputed from the staged covariances where they are used (np.linalg.inv of a
     // state's covariance is the same value wherever the reference recomputes it): no register
     // holds one across the loop
@@ -759,7 +776,9 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
             if (me) {
                 const double js_me[3] = {stg->a[me_l], stg->b[me_l], stg->tau[me_l]};
                 const double jm[3] = {mm[0], mm[1], mm[3]};
-#if GTF_STAGE_NOINV == 2
+#if GTF_STAGE_NOINV == 3
+                D = kl_with_inv(js_me, stage_cov(stg, me_l), inv_of(me_l), jm, mc, im);
+#elif GTF_STAGE_NOINV == 2
                 const Cov5 cme = stage_cov(stg, me_l);
                 D = kl_with_inv(js_me, cme, inv_cov5(cme), jm, mc, im);
 #elif GTF_STAGE_NOINV

@@ -291,11 +291,13 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(GTF_SEND
 #else
 #define GTF_EXTRAP_ATTR
 #endif
+// slots [slot_lo, slot_hi), or (list) the slot_hi - slot_lo listed slots list[0, ...)
 __global__ void __launch_bounds__(BLOCK) GTF_EXTRAP_ATTR k_extrapolate(gtf_graph g, gtf_nodes n, gtf_states uts,
                                                                        gtf_edges e, gtf_params p, Ws w, int slot_lo,
-                                                                       int slot_hi) {
-    const int k = slot_lo + xcd_local(blockIdx.x, gridDim.x) * BLOCK + threadIdx.x;
-    if (k >= slot_hi) return;
+                                                                       int slot_hi, const int32_t* list) {
+    const int i = xcd_local(blockIdx.x, gridDim.x) * BLOCK + threadIdx.x;
+    if (slot_lo + i >= slot_hi) return;
+    const int k = list ? list[i] : slot_lo + i;
     // Two levels of loads instead of a chain: everything indexed by the slot, then
     // everything indexed by its sender / receiver, issued before any early exit (the
     // exits would otherwise serialise each load behind the previous one's branch).
@@ -839,7 +841,9 @@ int launch_extrap_edges(const gtf_graph* g, gtf_nodes* n, gtf_states* uts, gtf_e
                         Ws w, hipStream_t st, const gtf_shard* sh = nullptr, void* const* events = nullptr) {
     const int32_t* list = sh ? sh->senders : nullptr;
     const int count = sh ? sh->n_senders : g->n_nodes;
-    const int slot_lo = sh ? sh->slot_lo : 0, slot_hi = sh ? sh->slot_hi : g->n_slots;
+    const int32_t* slots = sh ? sh->slot_list : nullptr;   // (a phase-1 call's listed slots)
+    const int slot_lo = slots ? 0 : (sh ? sh->slot_lo : 0);
+    const int slot_hi = slots ? sh->n_slot_list : (sh ? sh->slot_hi : g->n_slots);
     if (events) (void)hipEventRecord((hipEvent_t)events[0], st);
     if (g->n_slots > 0 && count > 0) {
         if (g->out_sched) {   // (a shard's graph view carries its own senders' schedule)
@@ -871,7 +875,7 @@ int launch_extrap_edges(const gtf_graph* g, gtf_nodes* n, gtf_states* uts, gtf_e
     if (events) (void)hipEventRecord((hipEvent_t)events[1], st);
     if (slot_hi > slot_lo)
         hipLaunchKernelGGL(k_extrapolate, dim3(grid(slot_hi - slot_lo)), dim3(BLOCK), 0, st, *g, *n, *uts, *e, *p,
-                           w, slot_lo, slot_hi);
+                           w, slot_lo, slot_hi, slots);
     if (events) (void)hipEventRecord((hipEvent_t)events[2], st);
     hipError_t err = hipGetLastError();
     return err == hipSuccess ? 0 : fail("extrapolate launch", err);
@@ -1072,8 +1076,10 @@ int launch_seq(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* ut
 int run_pass(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts, gtf_edges* e,
              const gtf_params* p, const gtf_shard* sh, void* ws, hipStream_t st, void* const* events) {
     Ws w = carve(ws, g->n_nodes, g->n_slots);
-    int rc = launch_extrap_edges(g, n, uts, e, p, w, st, sh, events);
-    if (rc) return rc;
+    const int phases = (sh && sh->phases) ? sh->phases : 3;   // (gtf_shard.phases: 1 edges, 2 nodes)
+    int rc = 0;
+    if (phases & 1) rc = launch_extrap_edges(g, n, uts, e, p, w, st, sh, events);
+    if (rc || !(phases & 2)) return rc;
 #if GTF_SPLIT_NODE
     rc = launch_seq<EXTRAP_OPS, UPDATE_OPS>(g, n, tse, uts, e, p, w, 0.0, 0.0, st);
     if (rc) return rc;
@@ -1232,7 +1238,8 @@ int gtf_pass_shard(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states
     if (rc) return rc;
     if (!sh || sh->n_senders < 0 || (sh->n_senders > 0 && !sh->senders) || sh->slot_lo < 0 ||
         sh->slot_hi < sh->slot_lo || sh->slot_hi > g->n_slots || sh->node_lo < 0 || sh->node_hi < sh->node_lo ||
-        sh->node_hi > g->n_nodes) {
+        sh->node_hi > g->n_nodes || sh->phases < 0 || sh->phases > 3 || sh->n_slot_list < 0 ||
+        (sh->n_slot_list > 0 && !sh->slot_list)) {
         snprintf(g_err, sizeof(g_err), "gtf_pass_shard: bad shard");
         return -2;
     }

@@ -16,7 +16,7 @@ F64 = ctypes.c_double
 
 
 U32 = ctypes.c_uint32
-ABI_VERSION = 5   # GTF_ABI_VERSION of include/gtf.h
+ABI_VERSION = 6   # GTF_ABI_VERSION of include/gtf.h
 
 
 class GtfGraph(ctypes.Structure):
@@ -60,7 +60,7 @@ class GtfParams(ctypes.Structure):
 
 class GtfShard(ctypes.Structure):
     _fields_ = [("senders", P), ("n_senders", I32), ("node_lo", I32), ("node_hi", I32), ("slot_lo", I32),
-                ("slot_hi", I32)]
+                ("slot_hi", I32), ("phases", I32), ("slot_list", P), ("n_slot_list", I32), ("pad_", I32)]
 
 
 class GtfHalo(ctypes.Structure):
@@ -150,7 +150,8 @@ SYMBOLS = ["gtf_workspace_bytes", "gtf_workspace_init", "gtf_uts_materialize", "
            "gtf_device_init", "gtf_malloc", "gtf_free", "gtf_memcpy_htod", "gtf_memcpy_dtoh", "gtf_memcpy_dtod",
            "gtf_memset", "gtf_stream_synchronize",
            "gtf_comm_unique_id", "gtf_comm_init", "gtf_comm_destroy", "gtf_comm_rank", "gtf_comm_size",
-           "gtf_halo_exchange", "gtf_allreduce_max_i64", "gtf_allgather_bytes", "gtf_tag_shard_workspace_bytes",
+           "gtf_halo_exchange", "gtf_halo_alltoall", "gtf_allreduce_max_i64", "gtf_allgather_bytes",
+           "gtf_tag_shard_workspace_bytes",
            "gtf_tag_propagate_shard",
            "gtf_last_error",
            "gtf_version"]
@@ -244,6 +245,7 @@ def lib(lean: bool = False):
     L.gtf_comm_rank.argtypes = [P]
     L.gtf_comm_size.argtypes = [P]
     L.gtf_halo_exchange.argtypes = [P, N, E, HA, HA, P, P, P, P, P]
+    L.gtf_halo_alltoall.argtypes = [P, P, P, P, P, P]
     L.gtf_allreduce_max_i64.argtypes = [P, P, I64, P]
     L.gtf_allgather_bytes.argtypes = [P, P, P, I64, P]
     L.gtf_tag_shard_workspace_bytes.restype = ctypes.c_size_t
@@ -260,7 +262,8 @@ def lib(lean: bool = False):
                "gtf_set_diagnostics", "gtf_build_event_csr_device", "gtf_device_init", "gtf_malloc", "gtf_free",
                "gtf_memcpy_htod", "gtf_memcpy_dtoh", "gtf_memcpy_dtod", "gtf_memset", "gtf_stream_synchronize",
                "gtf_comm_unique_id", "gtf_comm_init", "gtf_comm_destroy", "gtf_comm_rank", "gtf_comm_size",
-               "gtf_halo_exchange", "gtf_allreduce_max_i64", "gtf_allgather_bytes", "gtf_tag_propagate_shard"):
+               "gtf_halo_exchange", "gtf_halo_alltoall", "gtf_allreduce_max_i64", "gtf_allgather_bytes",
+               "gtf_tag_propagate_shard"):
         getattr(L, fn).restype = ctypes.c_int
     _lib = L
     return L

@@ -119,6 +119,31 @@ class ShardPlan:
         own = own[np.diff(g.out_ptr.astype(np.int64))[own] > 0]
         return np.unique(np.concatenate([halo.astype(np.int64), own])).astype(np.int32)
 
+    def split(self, r: int):
+        """rank r's pass in two edge phases (gtf_shard.phases, SURVEY §8e overlap): the
+        INTERIOR senders -- owned by r with every out-edge receiver owned by r, so their
+        merged state and every activation their scan reads are r's own after its pass --
+        with the owned slots they send to, and the other senders with the other owned slots
+        (halo-dependent: what the exchange brings). Returns (interior senders, other senders,
+        interior slots, other slots), int32, ascending; every sender of senders(r) and every
+        owned slot in exactly one part."""
+        g = self._g
+        s = self.senders(r).astype(np.int64)
+        on = self.owner_of_nodes()
+        op = g.out_ptr.astype(np.int64)
+        dst = g.slot_dst()[g.out_slot.astype(np.int64)] if g.n_slots else np.zeros(0, np.int64)
+        foreign = (on[dst] != r).astype(np.int64) if dst.size else np.zeros(0, np.int64)
+        cf = np.concatenate([[0], np.cumsum(foreign)])
+        interior = (on[s] == r) & (cf[op[s + 1]] == cf[op[s]])
+        is_in = np.zeros(g.n_nodes, bool)
+        is_in[s[interior]] = True
+        lo, hi = int(self.slot_lo[r]), int(self.slot_hi[r])
+        src = g.slot["slot_src"][lo:hi].astype(np.int64)
+        k_in = (src >= 0) & is_in[np.maximum(src, 0)]
+        ks = np.arange(lo, hi, dtype=np.int64)
+        return (s[interior].astype(np.int32), s[~interior].astype(np.int32), ks[k_in].astype(np.int32),
+                ks[~k_in].astype(np.int32))
+
     def schedule(self, r: int, widen: int = 0):
         """(sched, [n_g4, n_g8, n_g16, n_g32, n_g64], n_big, n_g2) of the owned receivers:
         slot-count buckets in node order, the <= 2-slot nodes first in the <= 4 bucket.
@@ -262,6 +287,7 @@ class ShardedDeviceGraph:
         "local" (no collective: SplitDeviceGraph)."""
         import torch
         from .device import DeviceGraph, TILE, sched_segments, sender_lanes
+        from .device import sender_schedule as sender_schedule_of
         self.torch = torch
         self.rank, self.world, self.backend, self.group = rank, world, backend, group
         gd, order, slot_perm, cuts = shard_layout(g, world, TILE if tile is None else tile)
@@ -300,6 +326,33 @@ class ShardedDeviceGraph:
                                slot_sflags=p("slot_sflags") if d.use_classes else ctypes.c_void_p(0))
         self.shard = nat.GtfShard(vp(self.senders), int(self.senders.numel()), int(pl.node_lo[rank]),
                                   int(pl.node_hi[rank]), int(pl.slot_lo[rank]), int(pl.slot_hi[rank]))
+        # the pass in phases (ShardPlan.split): 1a the interior senders and their slots, 1b the
+        # rest after the halo exchange, 2 the node kernels -- so the exchange of one pass's
+        # halo overlaps the next pass's phase 1a (step)
+        self._phase_t = []
+        self.cg_phase, self.shard_phase = [], []
+        for part_s, part_k in (lambda x: ((x[0], x[2]), (x[1], x[3])))(pl.split(rank)):
+            z1 = np.zeros(1, np.int32)
+            ts, tk = up(np.concatenate([part_s, z1])), up(np.concatenate([part_k, z1]))   # int32, never empty
+            osch, n_o_ = sender_schedule_of(gd.out_ptr, part_s)
+            t_os = up(osch if osch.size else np.zeros(4, np.int32))
+            t_ol = up(sender_lanes(d.t["out_slot"].cpu().numpy(), d.t["out_dst"].cpu().numpy(), osch, n_o_))
+            self._phase_t += [ts, tk, t_os, t_ol]
+            cgp = type(self.cg).from_buffer_copy(self.cg)
+            cgp.out_sched, cgp.out_lanes = vp(t_os), vp(t_ol)
+            cgp.n_o4, cgp.n_o8, cgp.n_o16 = n_o_
+            self.cg_phase.append(cgp)
+            self.shard_phase.append(nat.GtfShard(vp(ts), int(part_s.size), int(pl.node_lo[rank]), int(pl.node_hi[rank]),
+                                                 int(pl.slot_lo[rank]), int(pl.slot_hi[rank]), 1, vp(tk),
+                                                 int(part_k.size), 0))
+        self.shard_node = nat.GtfShard(vp(self.senders), int(self.senders.numel()), int(pl.node_lo[rank]),
+                                       int(pl.node_hi[rank]), int(pl.slot_lo[rank]), int(pl.slot_hi[rank]), 2)
+        self.split_sizes = {"interior_senders": int(self.shard_phase[0].n_senders),
+                            "halo_senders": int(self.shard_phase[1].n_senders),
+                            "interior_slots": int(self.shard_phase[0].n_slot_list),
+                            "halo_slots": int(self.shard_phase[1].n_slot_list)}
+        self.overlap = True        # step(): the halo exchange beside the next pass's phase 1a
+        self._pending = False      # a pass's halo not yet exchanged
         # halo exchange buffers and lists (fixed per plan)
         self._halo_t = {}
         self.halo_send, self.halo_recv = self._halo(True), self._halo(False)
@@ -408,7 +461,8 @@ class ShardedDeviceGraph:
 
     def sync(self):
         """every owned merged state and activation to every replica (all-gather), so the
-        whole graph can be read back from any rank"""
+        whole graph can be read back from any rank (a pending halo is part of it)"""
+        self._pending = False
         d = self.d
         pl = self.plan
         nat.check(d.lib.gtf_shard_pack(ctypes.byref(d.cn), ctypes.byref(d.ce), ctypes.byref(self.shard),
@@ -423,9 +477,83 @@ class ShardedDeviceGraph:
                                              ctypes.c_void_p(self.ranges.data_ptr()), pl.cap_nodes, pl.cap_slots,
                                              d.stream))
 
-    def step(self, p, events=None):
-        self.pass_(p, events)
-        self.exchange()
+    def _phase(self, p, which):
+        """one phase of the pass: 0 = 1a (interior senders and their slots), 1 = 1b (the rest),
+        2 = the node kernels"""
+        d = self.d
+        ws, st = self._io()[:2]
+        cg, sh = (self.cg_phase[which], self.shard_phase[which]) if which < 2 else (self.cg, self.shard_node)
+        nat.check(d.lib.gtf_pass_shard(ctypes.byref(cg), ctypes.byref(d.cn), ctypes.byref(d.ctse),
+                                       ctypes.byref(d.cuts), ctypes.byref(d.ce), ctypes.byref(self._cparams(p)),
+                                       ctypes.byref(sh), ws, st, None))
+
+    def _exchange_begin(self):
+        """pack this rank's halo segments and start the all-to-all; returns what
+        _exchange_end needs. The pack is stream-ordered before anything the caller enqueues
+        next, so the next pass's phase 1a can run while the segments travel."""
+        if self.world == 1 and self.comm is None:
+            return None
+        self.halo_pack()
+        _, st, sbuf, rbuf, sview, rview = self._io()
+        if self.comm is not None:   # libgtf's RCCL group on a stream of its own
+            torch = self.torch
+            if getattr(self, "_xs", None) is None:
+                self._xs = torch.cuda.Stream(device=self.d.device)
+                self._xev = (torch.cuda.Event(), torch.cuda.Event())
+            cur = torch.cuda.current_stream(self.d.device)
+            self._xev[0].record(cur)
+            self._xs.wait_event(self._xev[0])
+            nat.check(self.d.lib.gtf_halo_alltoall(self.comm.ptr, sbuf, rbuf,
+                                                   ctypes.cast(self._sizes_c[0], ctypes.c_void_p),
+                                                   ctypes.cast(self._sizes_c[1], ctypes.c_void_p),
+                                                   ctypes.c_void_p(self._xs.cuda_stream)))
+            self._xev[1].record(self._xs)
+            return "native"
+        if self.backend == "nccl":   # torch.distributed over RCCL, asynchronous
+            import torch.distributed as dist
+            return dist.all_to_all_single(rview, sview, self.recv_sizes, self.send_sizes, group=self.group,
+                                          async_op=True)
+        return "host"   # gloo: through host memory at _exchange_end
+
+    def _exchange_end(self, h):
+        if h is None:
+            return
+        _, st, sbuf, rbuf, sview, rview = self._io()
+        if h == "native":
+            self.torch.cuda.current_stream(self.d.device).wait_event(self._xev[1])
+        elif h == "host":
+            alltoall_bytes(sview, rview, self.send_sizes, self.recv_sizes, self.backend, self.group)
+        else:
+            h.wait()
+        self.halo_unpack(rbuf)
+
+    def step(self, p, events=None, overlap=None):
+        """one pass of the owned receivers. overlap (default self.overlap = True): the pass
+        in phases -- the previous pass's halo exchange (pending) starts, phase 1a (interior
+        senders and their slots, which read nothing the exchange brings) runs while it
+        travels, then the halo is unpacked and phase 1b and the node kernels follow; this
+        pass's own halo stays pending until the next step (or flush / sync). Bit-equal to
+        overlap=False (the one-call pass, then the exchange)."""
+        if overlap is None:
+            overlap = self.overlap
+        if not overlap or events is not None:
+            self.flush()
+            self.pass_(p, events)
+            self.exchange()
+            return
+        h = self._exchange_begin() if self._pending else None
+        self._pending = False
+        self._phase(p, 0)
+        self._exchange_end(h)
+        self._phase(p, 1)
+        self._phase(p, 2)
+        self._pending = self.world > 1 or self.comm is not None   # (native: RCCL even at world 1)
+
+    def flush(self):
+        """the pending halo exchange (a step's last pass), now"""
+        if self._pending:
+            self._pending = False
+            self._exchange_end(self._exchange_begin())
 
     def tag_propagation(self, tags, radius, threshold=0.1, max_sweeps=100000):
         """Tag propagation (tag_propagation/tag_propagation.py:97-164) on the edge-sharded

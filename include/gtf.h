@@ -24,7 +24,7 @@
  *   gtf_tag_prepare  -> tag_propagation/tag_propagation.py:97-110
  *   gtf_tag_propagate -> tag_propagation/tag_propagation.py:97-164 (the whole stage)
  *   gtf_tag_sweep_shard -> one sweep (:137-164) on an edge-sharded event
- *   gtf_comm_*, gtf_halo_exchange, gtf_allreduce_max_i64, gtf_allgather_bytes,
+ *   gtf_comm_*, gtf_halo_exchange, gtf_halo_alltoall, gtf_allreduce_max_i64, gtf_allgather_bytes,
  *   gtf_tag_propagate_shard -> no reference counterpart: the collectives of one event
  *                       sharded over the GPUs of a node, in place of the
  *                       serial subgraph loop src/extrapolate/extrapolate_merged_states.py:406-451
@@ -46,7 +46,7 @@ typedef void* gtf_stream_t; /* a hipStream_t */
 /* Version of the struct layouts below. gtf_graph carries it with its own size, and every
  * entry point taking a gtf_graph refuses a caller built against another layout
  * (status -3, gtf_last_error() names both). Bumped on every layout change. */
-#define GTF_ABI_VERSION 5u
+#define GTF_ABI_VERSION 6u
 
 /* ---- graph structure (read-only on the path) ------------------------------ */
 typedef struct gtf_graph {
@@ -323,6 +323,19 @@ typedef struct gtf_shard {
     int32_t n_senders;
     int32_t node_lo, node_hi;
     int32_t slot_lo, slot_hi;
+    /* ABI v6: the pass in phases, so the halo exchange can overlap the part that does not
+     * read it (gtf.shard.ShardedDeviceGraph.step). phases = 0 (or 3): the whole pass; 1: the
+     * sender scan over `senders` and the extrapolation only; 2: the node kernels only.
+     * slot_list (device, ascending, [n_slot_list]) or NULL: phase 1 extrapolates exactly these
+     * owned slots instead of [slot_lo, slot_hi). A rank's pass as two phase-1 calls (the
+     * senders whose state and out-edge activations are all its own, with the slots they
+     * send to; then the rest, after the exchange) and one phase-2 call equals the one-call
+     * pass bit for bit: every sender is scanned once, in its own successor order, and every
+     * owned slot extrapolated once. */
+    int32_t phases;
+    const int32_t* slot_list;
+    int32_t n_slot_list;
+    int32_t pad_;
 } gtf_shard;
 
 int gtf_pass_shard(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts, gtf_edges* e,
@@ -420,6 +433,10 @@ int gtf_comm_size(const gtf_comm* comm);
 int gtf_halo_exchange(gtf_comm* comm, gtf_nodes* n, gtf_edges* e, const gtf_halo* send, const gtf_halo* recv,
                       void* send_buf, void* recv_buf, const int64_t* send_bytes, const int64_t* recv_bytes,
                       gtf_stream_t stream);
+/* the all-to-all of gtf_halo_exchange alone (no pack / unpack), for a caller that runs it on
+ * a stream of its own beside the pass's phase 1 (gtf_shard.phases) */
+int gtf_halo_alltoall(gtf_comm* comm, const void* send_buf, void* recv_buf, const int64_t* send_bytes,
+                      const int64_t* recv_bytes, gtf_stream_t stream);
 /* in-place all-reduce(MAX) of int64 words (the sharded tag sweep's exchange) */
 int gtf_allreduce_max_i64(gtf_comm* comm, int64_t* words, int64_t count, gtf_stream_t stream);
 /* all-gather of one equal-size chunk per rank into gathered (nranks chunks, rank order):

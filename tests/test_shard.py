@@ -45,6 +45,44 @@ def test_plan_partitions_receivers_and_slots(world):
         assert (q[:, 1] == g.out_ptr[q[:, 0]]).all() and (q[:, 2] == g.out_ptr[q[:, 0] + 1]).all()
 
 
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_split_phases_partition_and_interior_rule(world):
+    """ShardPlan.split (the pass in phases, gtf_shard.phases): the interior senders and the
+    others partition senders(r); the interior / other slots partition the owned slots; a
+    sender is interior exactly when the rank owns it and every receiver of its out-edges
+    (brute force), and an owned slot is interior exactly when its sender is -- so nothing
+    phase 1a reads is written by the halo exchange (HaloPlan lists) and every owned slot is
+    extrapolated once"""
+    from gtf.shard import HaloPlan, shard_layout
+    g0 = synth.event(seed=4, n_tracks=2000, fake_mean=synth.C4_FAKE)
+    g, _, _, cuts = shard_layout(g0, world, 512)
+    pl = ShardPlan(g, world, cuts)
+    hp = HaloPlan(pl)
+    owner = np.repeat(np.arange(world), pl.node_hi - pl.node_lo)
+    dst = g.slot_dst()
+    n_in = 0
+    for r in range(world):
+        s_in, s_out, k_in, k_out = pl.split(r)
+        snd = pl.senders(r)
+        assert np.array_equal(np.sort(np.concatenate([s_in, s_out])), snd)
+        assert np.array_equal(np.sort(np.concatenate([k_in, k_out])), np.arange(pl.slot_lo[r], pl.slot_hi[r]))
+        brute = [u for u in snd.tolist() if owner[u] == r and
+                 all(owner[dst[g.out_slot[i]]] == r for i in range(g.out_ptr[u], g.out_ptr[u + 1]))]
+        assert s_in.tolist() == brute
+        src = g.slot["slot_src"][k_in]
+        assert np.isin(src, s_in).all()
+        src_o = g.slot["slot_src"][k_out]
+        assert not np.isin(src_o[src_o >= 0], s_in).any()
+        # the halo this rank receives never touches an interior sender or its out-edges
+        assert not np.isin(hp.need_nodes[r], s_in).any()
+        outs = np.concatenate([g.out_slot[g.out_ptr[u]:g.out_ptr[u + 1]] for u in s_in] or [np.zeros(0, np.int64)])
+        assert not np.isin(hp.need_slots[r], outs).any()
+        n_in += s_in.size
+        if world == 1:
+            assert s_out.size == 0 or (owner[s_out] == 0).all()
+    assert n_in > 0
+
+
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_wedge_layout_is_a_permutation_with_small_halo(world):
     from gtf.graph import check_layout

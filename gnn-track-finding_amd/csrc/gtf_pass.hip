@@ -77,6 +77,18 @@ __device__ __forceinline__ void store_cov5(double* c, int64_t i, const Cov5& v) 
     p[0] = v.c00; p[1] = v.c01; p[2] = v.c10; p[3] = v.c11; p[4] = v.c22;
 }
 
+// The extrapolation's quotients by a divisor used more than once: qdiv (the correctly
+// rounded quotient, the same bits as dividing) or, with GTF_EXTRAP_FAST (A/B builds), the
+// product with the reciprocal (within 1.5 ulp). The extrapolation is compared within a
+// tolerance (numpy's vectorised cos / sin / exp are not reproducible bit for bit anyway).
+#ifndef GTF_EXTRAP_FAST
+#define GTF_EXTRAP_FAST 0
+#endif
+__device__ __forceinline__ double xdiv(double x, double d, double r) {
+    if (GTF_EXTRAP_FAST) return x * r;
+    return qdiv(x, d, r);
+}
+
 // ---------------------------------------------------------------------------
 // var_ms: Highland multiple scattering term (extrapolate_merged_states.py:114-124)
 // ---------------------------------------------------------------------------
@@ -89,7 +101,7 @@ __device__ __forceinline__ double highland_var_ms(double a, double b, const doub
     double q = (2.0 * a * nb[0]) + b;
     const double t15 = 1.0 + q * q;
     double kappa = (2.0 * a) / (t15 * sqrt(t15));  // (1 + q^2)**1.5
-    double t = qdiv((13.6 * 1e-3 * sqrt(0.02)) * kappa, 0.3, 1.0 / 0.3);   // (a constant reciprocal)
+    double t = xdiv((13.6 * 1e-3 * sqrt(0.02)) * kappa, 0.3, 1.0 / 0.3);   // (a constant reciprocal)
     double var_ms = sin_t * (t * t);
     if (fabs(ng[2]) >= boundary) {
         double tan_t = fabs(dr) / fabs(dz);
@@ -110,10 +122,21 @@ __device__ __forceinline__ double highland_var_ms(double a, double b, const doub
 // coalesced instead of gathering it through the sender's out-list (and recomputes the
 // edge's own var_ms from operands it loads anyway).
 // ---------------------------------------------------------------------------
+// the fused sender-major form (gtf_shard.phases bit 4, a shard's halo-dependent senders):
+// every scanned edge into the owned slots [lo, hi) is extrapolated by its lane right after
+// the scan, with the running value in a register instead of the workspace
+struct Fuse {
+    gtf_states uts;
+    int32_t lo, hi;
+};
+__device__ __forceinline__ void extrap_slot(const gtf_graph& g, gtf_nodes& n, gtf_states& uts, gtf_edges& e,
+                                            const gtf_params& p, const Ws& w, int k, bool have_vc, double vc_given);
+
 // one sender u over its out-list [ob, oe) with SG lanes (lane gl), chunks of SG
-template <int SG>
+template <int SG, bool FUSED = false>
 __device__ __forceinline__ void sender_scan(const gtf_graph& g, gtf_nodes& n, const gtf_edges& e,
-                                            const gtf_params& p, const Ws& w, int u, int ob, int oe, int gl) {
+                                            const gtf_params& p, const Ws& w, int u, int ob, int oe, int gl,
+                                            const Fuse* fu = nullptr) {
     // the sender's flag, state and coordinates in one round of loads
     const uint8_t hm = n.has_merged[u];
     const double a = n.merged_state[3 * (int64_t)u + 0];
@@ -122,6 +145,16 @@ __device__ __forceinline__ void sender_scan(const gtf_graph& g, gtf_nodes& n, co
                            g.gnn[4 * (int64_t)u + 3]};
     const double* ng = ngl;
     double carry = n.merged_cov[5 * (int64_t)u + 3];
+    if constexpr (FUSED) {
+        if (!hm) {   // no state to extrapolate: the owned slots still end their message passing
+            for (int i = ob + gl; i < oe; i += SG) {
+                const int k = g.out_slot[i];
+                if (k >= fu->lo && k < fu->hi) extrap_slot(g, n, *(gtf_states*)&fu->uts, *(gtf_edges*)&e, p, w, k,
+                                                            false, 0.0);
+            }
+            return;
+        }
+    }
     if (!hm || ob == oe) return;
     for (int base = ob; base < oe; base += SG) {
         const int i = base + gl;
@@ -141,7 +174,11 @@ __device__ __forceinline__ void sender_scan(const gtf_graph& g, gtf_nodes& n, co
         }
         // the running value of each active edge, stored in out-edge order (contiguous per
         // sender: coalesced stores) when the graph has slot_outidx, else at its slot
-        if (vm != -1.0) w.vc[g.slot_outidx ? i : k] = c;
+        if constexpr (FUSED) {
+            if (k >= fu->lo && k < fu->hi) extrap_slot(g, n, *(gtf_states*)&fu->uts, *(gtf_edges*)&e, p, w, k, true, c);
+        } else {
+            if (vm != -1.0) w.vc[g.slot_outidx ? i : k] = c;
+        }
         carry = __shfl(c, SG - 1, SG);  // lanes past the end carry the full sum
     }
     if (gl == 0) n.merged_cov[5 * (int64_t)u + 3] = carry;
@@ -150,10 +187,10 @@ __device__ __forceinline__ void sender_scan(const gtf_graph& g, gtf_nodes& n, co
 // one sender u whose out-edges fit the group (<= G), lane gl holding out-edge slot k
 // (-1 past the end) with receiver v from gtf_graph.out_lanes: every load of the scan
 // is issued in one round, beside the sender's own fields
-template <int G>
+template <int G, bool FUSED = false>
 __device__ __forceinline__ void sender_scan_lane(const gtf_graph& g, gtf_nodes& n, const gtf_edges& e,
                                                  const gtf_params& p, const Ws& w, int u, int ob, int k, int v,
-                                                 int gl) {
+                                                 int gl, const Fuse* fu = nullptr) {
     const uint8_t hm = n.has_merged[u];
     const double a = n.merged_state[3 * (int64_t)u + 0];
     const double b = n.merged_state[3 * (int64_t)u + 1];
@@ -164,6 +201,13 @@ __device__ __forceinline__ void sender_scan_lane(const gtf_graph& g, gtf_nodes& 
     const double nb[4] = {g.gnn[4 * (int64_t)v], g.gnn[4 * (int64_t)v + 1], g.gnn[4 * (int64_t)v + 2],
                           g.gnn[4 * (int64_t)v + 3]};
     const uint8_t act = e.act[kk];
+    if constexpr (FUSED) {
+        if (!hm) {   // no state to extrapolate: the owned slots still end their message passing
+            if (k >= fu->lo && k < fu->hi) extrap_slot(g, n, *(gtf_states*)&fu->uts, *(gtf_edges*)&e, p, w, k, false,
+                                                        0.0);
+            return;
+        }
+    }
     if (!hm) return;   // group-uniform
     double vm = -1.0;
     if (k >= 0 && act == 1) vm = highland_var_ms(a, b, ng, nb, p.endcap_boundary);
@@ -172,9 +216,12 @@ __device__ __forceinline__ void sender_scan_lane(const gtf_graph& g, gtf_nodes& 
         const double vmm = __shfl(vm, m, G);
         if (m <= gl && vmm != -1.0) c = c + vmm;
     }
-    if (vm != -1.0) w.vc[g.slot_outidx ? ob + gl : k] = c;
+    if (!FUSED && vm != -1.0) w.vc[g.slot_outidx ? ob + gl : k] = c;
     const double fin = __shfl(c, G - 1, G);   // the last lane has every active edge's term
     if (gl == 0) n.merged_cov[5 * (int64_t)u + 3] = fin;
+    if constexpr (FUSED) {
+        if (k >= fu->lo && k < fu->hi) extrap_slot(g, n, *(gtf_states*)&fu->uts, *(gtf_edges*)&e, p, w, k, true, c);
+    }
 }
 
 // every node (list NULL) or a list of senders (a shard's), 8 lanes per sender
@@ -198,26 +245,27 @@ struct SendBuckets {
     const int2* lanes[2];  // gtf_graph.out_lanes of the 4- and 8-lane buckets, or NULL
 };
 
-template <int G>
+template <int G, bool FUSED = false>
 __device__ __forceinline__ void sender_bucket(const gtf_graph& g, gtf_nodes& n, const gtf_edges& e,
                                               const gtf_params& p, const Ws& w, const int4* list, int count,
-                                              int b, int nb) {
+                                              int b, int nb, const Fuse* fu = nullptr) {
     const int gi = (xcd_local(b, nb) * BLOCK + (int)threadIdx.x) / G;
     if (gi >= count) return;  // group-uniform
     const int4 en = list[gi];
-    sender_scan<G>(g, n, e, p, w, en.x, en.y, en.z, threadIdx.x & (G - 1));
+    sender_scan<G, FUSED>(g, n, e, p, w, en.x, en.y, en.z, threadIdx.x & (G - 1), fu);
 }
 
-template <int G>
+template <int G, bool FUSED = false>
 __device__ __forceinline__ void sender_bucket_lanes(const gtf_graph& g, gtf_nodes& n, const gtf_edges& e,
                                                     const gtf_params& p, const Ws& w, const int4* list,
-                                                    const int2* lanes, int count, int b, int nb) {
+                                                    const int2* lanes, int count, int b, int nb,
+                                                    const Fuse* fu = nullptr) {
     const int t = xcd_local(b, nb) * BLOCK + (int)threadIdx.x;
     const int gi = t / G;
     if (gi >= count) return;  // group-uniform
     const int4 en = list[gi];
     const int2 kv = lanes[t];  // lane t of the bucket = lane (t % G) of entry gi
-    sender_scan_lane<G>(g, n, e, p, w, en.x, en.y, kv.x, kv.y, t & (G - 1));
+    sender_scan_lane<G, FUSED>(g, n, e, p, w, en.x, en.y, kv.x, kv.y, t & (G - 1), fu);
 }
 
 // All arguments of k_sender_sched in one by-value struct, read through a laundered copy of
@@ -232,6 +280,7 @@ struct SendKArgs {
     gtf_params p;
     Ws w;
     SendBuckets sb;
+    Fuse fu;   // (the fused form only)
 };
 typedef const __attribute__((address_space(4))) SendKArgs* SendKArgPtr;
 __device__ __forceinline__ SendKArgPtr send_kargs() {
@@ -246,6 +295,7 @@ __device__ __forceinline__ SendKArgPtr send_kargs() {
 #ifndef GTF_SEND_NUM_SGPR
 #define GTF_SEND_NUM_SGPR 72
 #endif
+template <bool FUSED>
 __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(GTF_SEND_NUM_SGPR))) k_sender_sched(SendKArgs args) {
 #if GTF_SEND_KARGS
     (void)args;
@@ -259,9 +309,10 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(GTF_SEND
     if (b < b0) {
         const SendBuckets& sb = GTF_SA(sb);
         if (sb.lanes[0])
-            sender_bucket_lanes<4>(GTF_SA(g), GTF_SA(n), GTF_SA(e), GTF_SA(p), GTF_SA(w), sb.list[0], sb.lanes[0],
-                                   sb.count[0], b, b0);
-        else sender_bucket<4>(GTF_SA(g), GTF_SA(n), GTF_SA(e), GTF_SA(p), GTF_SA(w), sb.list[0], sb.count[0], b, b0);
+            sender_bucket_lanes<4, FUSED>(GTF_SA(g), GTF_SA(n), GTF_SA(e), GTF_SA(p), GTF_SA(w), sb.list[0],
+                                          sb.lanes[0], sb.count[0], b, b0, &GTF_SA(fu));
+        else sender_bucket<4, FUSED>(GTF_SA(g), GTF_SA(n), GTF_SA(e), GTF_SA(p), GTF_SA(w), sb.list[0], sb.count[0], b,
+                                     b0, &GTF_SA(fu));
         return;
     }
     b -= b0;
@@ -269,14 +320,16 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(GTF_SEND
     if (b < b1) {
         const SendBuckets& sb = GTF_SA(sb);
         if (sb.lanes[1])
-            sender_bucket_lanes<8>(GTF_SA(g), GTF_SA(n), GTF_SA(e), GTF_SA(p), GTF_SA(w), sb.list[1], sb.lanes[1],
-                                   sb.count[1], b, b1);
-        else sender_bucket<8>(GTF_SA(g), GTF_SA(n), GTF_SA(e), GTF_SA(p), GTF_SA(w), sb.list[1], sb.count[1], b, b1);
+            sender_bucket_lanes<8, FUSED>(GTF_SA(g), GTF_SA(n), GTF_SA(e), GTF_SA(p), GTF_SA(w), sb.list[1],
+                                          sb.lanes[1], sb.count[1], b, b1, &GTF_SA(fu));
+        else sender_bucket<8, FUSED>(GTF_SA(g), GTF_SA(n), GTF_SA(e), GTF_SA(p), GTF_SA(w), sb.list[1], sb.count[1], b,
+                                     b1, &GTF_SA(fu));
         return;
     }
     b -= b1;
     const SendBuckets& sb = GTF_SA(sb);
-    sender_bucket<16>(GTF_SA(g), GTF_SA(n), GTF_SA(e), GTF_SA(p), GTF_SA(w), sb.list[2], sb.count[2], b, sb.blocks[2]);
+    sender_bucket<16, FUSED>(GTF_SA(g), GTF_SA(n), GTF_SA(e), GTF_SA(p), GTF_SA(w), sb.list[2], sb.count[2], b,
+                             sb.blocks[2], &GTF_SA(fu));
 #undef GTF_SA
 }
 
@@ -291,13 +344,11 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(GTF_SEND
 #else
 #define GTF_EXTRAP_ATTR
 #endif
-// slots [slot_lo, slot_hi), or (list) the slot_hi - slot_lo listed slots list[0, ...)
-__global__ void __launch_bounds__(BLOCK) GTF_EXTRAP_ATTR k_extrapolate(gtf_graph g, gtf_nodes n, gtf_states uts,
-                                                                       gtf_edges e, gtf_params p, Ws w, int slot_lo,
-                                                                       int slot_hi, const int32_t* list) {
-    const int i = xcd_local(blockIdx.x, gridDim.x) * BLOCK + threadIdx.x;
-    if (slot_lo + i >= slot_hi) return;
-    const int k = list ? list[i] : slot_lo + i;
+// the extrapolation of slot k (edge u -> v), k_extrapolate's per-slot body; have_vc: the
+// running merged_cov[1,1] of the edge comes from the caller (the fused sender-major form)
+// instead of the workspace
+__device__ __forceinline__ void extrap_slot(const gtf_graph& g, gtf_nodes& n, gtf_states& uts, gtf_edges& e,
+                                            const gtf_params& p, const Ws& w, int k, bool have_vc, double vc_given) {
     // Two levels of loads instead of a chain: everything indexed by the slot, then
     // everything indexed by its sender / receiver, issued before any early exit (the
     // exits would otherwise serialise each load behind the previous one's branch).
@@ -306,8 +357,8 @@ __global__ void __launch_bounds__(BLOCK) GTF_EXTRAP_ATTR k_extrapolate(gtf_graph
     const int src = g.slot_src[k], v = g.slot_dst[k];
     // written by k_sender for active edges of merged senders: in out-edge order through
     // slot_outidx (one gather beside the sender's), or by slot
-    const int oi = g.slot_outidx ? g.slot_outidx[k] : k;
-    const double vc = w.vc[oi >= 0 ? oi : 0];
+    const int oi = (have_vc || !g.slot_outidx) ? k : g.slot_outidx[k];
+    const double vc = have_vc ? vc_given : w.vc[oi >= 0 ? oi : 0];
     const double smw = e.send_mw[k];
     const int u = src >= 0 ? src : 0;   // orphan keys have no sender
     const double* ng = g.gnn + 4 * (int64_t)u;  // sender ("node" in the reference)
@@ -325,16 +376,16 @@ __global__ void __launch_bounds__(BLOCK) GTF_EXTRAP_ATTR k_extrapolate(gtf_graph
 
     // cos/sin of atan2(y, x) as x/h, y/h (h = |(x, y)|): the same angles as the
     // reference's atan2 -> cos/sin round trips, to a couple of ulps, without fp64 libm
-    // (divisors used more than once: one correctly rounded reciprocal, then qdiv() -- the
+    // (divisors used more than once: one correctly rounded reciprocal, then xdiv() -- the
     // same bits as dividing each time)
     const double rA = sqrt(node_x * node_x + node_y * node_y);
     const double irA = 1.0 / rA;
-    const double ca = rA > 0.0 ? qdiv(node_x, rA, irA) : 1.0, sa = rA > 0.0 ? qdiv(node_y, rA, irA) : 0.0;  // :41
+    const double ca = rA > 0.0 ? xdiv(node_x, rA, irA) : 1.0, sa = rA > 0.0 ? xdiv(node_y, rA, irA) : 0.0;  // :41
     const double x_A = (nbx - node_x) * ca + (nby - node_y) * sa;                              // :52
     const double py = (node_x * nby) - (node_y * nbx), px = (node_x * nbx) + (node_y * nby);  // :59
     const double hp = sqrt(px * px + py * py);
     const double ihp = 1.0 / hp;
-    const double sp = hp > 0.0 ? qdiv(py, hp, ihp) : 0.0, cp = hp > 0.0 ? qdiv(px, hp, ihp) : 1.0;
+    const double sp = hp > 0.0 ? xdiv(py, hp, ihp) : 0.0, cp = hp > 0.0 ? xdiv(px, hp, ihp) : 1.0;
     const double x_prime = x_A + (c * sp);                                        // :63
     const double Vx = cp + (b * sp);
     const double Ax = a * sp;
@@ -345,20 +396,20 @@ __global__ void __launch_bounds__(BLOCK) GTF_EXTRAP_ATTR k_extrapolate(gtf_graph
     const double d2 = denom * denom;
     const double id2 = 1.0 / d2;
     const double ds_da = -(sp * (numer * numer)) / (d2 * denom);
-    const double ds_db = qdiv((sp * numer) * (1.0 + qdiv(3.0 * a * sp * numer, d2, id2)), d2, id2);
-    const double ds_dc = (-sp * (1.0 + qdiv(2.0 * a * sp * numer, d2, id2))) / denom;
+    const double ds_db = xdiv((sp * numer) * (1.0 + xdiv(3.0 * a * sp * numer, d2, id2)), d2, id2);
+    const double ds_dc = (-sp * (1.0 + xdiv(2.0 * a * sp * numer, d2, id2))) / denom;
     denom = cp + ((2.0 * a + b) * sp);                                             // :89
     const double e2 = denom * denom;
     const double da_da = (1.0 / (e2 * denom)) * (1.0 - ((6.0 * a * sp) * (s_star + a * ds_da) / denom));
     const double e4 = e2 * e2, ie4 = 1.0 / e4;
-    const double da_db = qdiv(-3.0 * a * sp * ((2.0 * a * ds_db) + 1.0), e4, ie4);
-    const double da_dc = qdiv(-6.0 * sp * ds_dc * (a * a), e4, ie4);
+    const double da_db = xdiv(-3.0 * a * sp * ((2.0 * a * ds_db) + 1.0), e4, ie4);
+    const double da_dc = xdiv(-6.0 * sp * ds_dc * (a * a), e4, ie4);
     denom = cp + ((2.0 * a * s_star + b) * sp);                                    // :95
     const double idn = 1.0 / denom;
-    double bracket = cp - qdiv(sp * (-sp + ((2.0 * a * s_star + b) * cp)), denom, idn);
-    const double db_da = qdiv(2.0 * (s_star + a * ds_da) * bracket, denom, idn);
-    const double db_db = qdiv((1.0 + (2.0 * a * ds_da)) * bracket, denom, idn);
-    const double db_dc = qdiv(2.0 * a * ds_dc * bracket, denom, idn);
+    double bracket = cp - xdiv(sp * (-sp + ((2.0 * a * s_star + b) * cp)), denom, idn);
+    const double db_da = xdiv(2.0 * (s_star + a * ds_da) * bracket, denom, idn);
+    const double db_db = xdiv((1.0 + (2.0 * a * ds_da)) * bracket, denom, idn);
+    const double db_dc = xdiv(2.0 * a * ds_dc * bracket, denom, idn);
     bracket = (cp * (2.0 * a + b)) - sp;                                           // :102
     const double dc_da = (ds_da * bracket) + ((s_star * s_star) * cp);
     const double dc_db = (ds_db * bracket) + (s_star * cp);
@@ -421,7 +472,7 @@ __global__ void __launch_bounds__(BLOCK) GTF_EXTRAP_ATTR k_extrapolate(gtf_graph
     const double dr = nbr - node_r;
     const double dz = nbz - node_z;
     const double J0 = 1.0 / dr;
-    const double tau = qdiv(dz, dr, J0);
+    const double tau = xdiv(dz, dr, J0);
     double sigma_r = p.sigma0rz, sigma_z = p.sigma0rz2;
     if (fabs(node_z) >= p.endcap_boundary) { sigma_z = p.sigma0rz; sigma_r = p.sigma0rz2; }
     double sigma_rn = p.sigma0rz, sigma_zn = p.sigma0rz2;
@@ -446,6 +497,15 @@ __global__ void __launch_bounds__(BLOCK) GTF_EXTRAP_ATTR k_extrapolate(gtf_graph
     // marks it live instead of writing a 32-byte copy per accepted edge (gtf_uts_materialize
     // writes it when it is read back or before g.gnn changes)
     uts.fresh[k] = 3;   // the receiver's has_uts flag follows in the node kernel (OP_FRESH)
+}
+
+// slots [slot_lo, slot_hi), or (list) the slot_hi - slot_lo listed slots list[0, ...)
+__global__ void __launch_bounds__(BLOCK) GTF_EXTRAP_ATTR k_extrapolate(gtf_graph g, gtf_nodes n, gtf_states uts,
+                                                                       gtf_edges e, gtf_params p, Ws w, int slot_lo,
+                                                                       int slot_hi, const int32_t* list) {
+    const int i = xcd_local(blockIdx.x, gridDim.x) * BLOCK + threadIdx.x;
+    if (slot_lo + i >= slot_hi) return;
+    extrap_slot(g, n, uts, e, p, w, list ? list[i] : slot_lo + i, false, 0.0);
 }
 
 // gtf_uts_materialize: the stored 'xyzr' snapshot (extrapolate_merged_states.py:377) of every
@@ -841,6 +901,9 @@ int launch_extrap_edges(const gtf_graph* g, gtf_nodes* n, gtf_states* uts, gtf_e
                         Ws w, hipStream_t st, const gtf_shard* sh = nullptr, void* const* events = nullptr) {
     const int32_t* list = sh ? sh->senders : nullptr;
     const int count = sh ? sh->n_senders : g->n_nodes;
+    // phases bit 4: the fused sender-major form (the senders' owned out-edges extrapolated
+    // by the scan's lanes; needs the sender schedule), no slot-parallel extrapolation
+    const bool fused = sh && (sh->phases & 4) && g->out_sched;
     const int32_t* slots = sh ? sh->slot_list : nullptr;   // (a phase-1 call's listed slots)
     const int slot_lo = slots ? 0 : (sh ? sh->slot_lo : 0);
     const int slot_hi = slots ? sh->n_slot_list : (sh ? sh->slot_hi : g->n_slots);
@@ -865,15 +928,19 @@ int launch_extrap_edges(const gtf_graph* g, gtf_nodes* n, gtf_states* uts, gtf_e
                 sb.blocks[q] = pad8((cnt[q] + BLOCK / gs[q] - 1) / (BLOCK / gs[q]));
                 total += sb.blocks[q];
             }
-            if (total > 0)
-                hipLaunchKernelGGL(k_sender_sched, dim3(total), dim3(BLOCK), 0, st, SendKArgs{*g, *n, *e, *p, w, sb});
+            if (total > 0 && fused)
+                hipLaunchKernelGGL(k_sender_sched<true>, dim3(total), dim3(BLOCK), 0, st,
+                                   SendKArgs{*g, *n, *e, *p, w, sb, Fuse{*uts, sh->slot_lo, sh->slot_hi}});
+            else if (total > 0)
+                hipLaunchKernelGGL(k_sender_sched<false>, dim3(total), dim3(BLOCK), 0, st,
+                                   SendKArgs{*g, *n, *e, *p, w, sb, Fuse{}});
         } else {
             hipLaunchKernelGGL(k_sender, dim3((count + BLOCK / SG - 1) / (BLOCK / SG)), dim3(BLOCK), 0, st, *g, *n,
                                *e, *p, w, list, count);
         }
     }
     if (events) (void)hipEventRecord((hipEvent_t)events[1], st);
-    if (slot_hi > slot_lo)
+    if (slot_hi > slot_lo && !fused)
         hipLaunchKernelGGL(k_extrapolate, dim3(grid(slot_hi - slot_lo)), dim3(BLOCK), 0, st, *g, *n, *uts, *e, *p,
                            w, slot_lo, slot_hi, slots);
     if (events) (void)hipEventRecord((hipEvent_t)events[2], st);
@@ -1076,7 +1143,7 @@ int launch_seq(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* ut
 int run_pass(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts, gtf_edges* e,
              const gtf_params* p, const gtf_shard* sh, void* ws, hipStream_t st, void* const* events) {
     Ws w = carve(ws, g->n_nodes, g->n_slots);
-    const int phases = (sh && sh->phases) ? sh->phases : 3;   // (gtf_shard.phases: 1 edges, 2 nodes)
+    const int phases = (sh && sh->phases) ? sh->phases : 3;   // (gtf_shard.phases: 1 edges, 2 nodes, 4 fused)
     int rc = 0;
     if (phases & 1) rc = launch_extrap_edges(g, n, uts, e, p, w, st, sh, events);
     if (rc || !(phases & 2)) return rc;
@@ -1238,7 +1305,7 @@ int gtf_pass_shard(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states
     if (rc) return rc;
     if (!sh || sh->n_senders < 0 || (sh->n_senders > 0 && !sh->senders) || sh->slot_lo < 0 ||
         sh->slot_hi < sh->slot_lo || sh->slot_hi > g->n_slots || sh->node_lo < 0 || sh->node_hi < sh->node_lo ||
-        sh->node_hi > g->n_nodes || sh->phases < 0 || sh->phases > 3 || sh->n_slot_list < 0 ||
+        sh->node_hi > g->n_nodes || sh->phases < 0 || sh->phases > 7 || sh->n_slot_list < 0 ||
         (sh->n_slot_list > 0 && !sh->slot_list)) {
         snprintf(g_err, sizeof(g_err), "gtf_pass_shard: bad shard");
         return -2;

@@ -123,10 +123,10 @@ class ShardPlan:
         """rank r's pass in two edge phases (gtf_shard.phases, SURVEY §8e overlap): the
         INTERIOR senders -- owned by r with every out-edge receiver owned by r, so their
         merged state and every activation their scan reads are r's own after its pass --
-        with the owned slots they send to, and the other senders with the other owned slots
-        (halo-dependent: what the exchange brings). Returns (interior senders, other senders,
-        interior slots, other slots), int32, ascending; every sender of senders(r) and every
-        owned slot in exactly one part."""
+        with the owned slots they send to (and the owned keys without an edge), and the
+        other senders with their owned edges (halo-dependent: what the exchange brings).
+        Returns (interior senders, other senders, interior slots, other slots), int32,
+        ascending; every sender of senders(r) and every owned slot in exactly one part."""
         g = self._g
         s = self.senders(r).astype(np.int64)
         on = self.owner_of_nodes()
@@ -139,7 +139,11 @@ class ShardPlan:
         is_in[s[interior]] = True
         lo, hi = int(self.slot_lo[r]), int(self.slot_hi[r])
         src = g.slot["slot_src"][lo:hi].astype(np.int64)
-        k_in = (src >= 0) & is_in[np.maximum(src, 0)]
+        ise = g.slot["is_edge"][lo:hi].astype(bool)
+        # the other part = exactly the owned edges of the other senders (their out-edges into
+        # the rank's receivers: the fused sender-major phase 1b reaches them through the
+        # senders' out-lists); keys without an edge and orphans need nothing from anyone
+        k_in = ~(ise & (src >= 0) & ~is_in[np.maximum(src, 0)])
         ks = np.arange(lo, hi, dtype=np.int64)
         return (s[interior].astype(np.int32), s[~interior].astype(np.int32), ks[k_in].astype(np.int32),
                 ks[~k_in].astype(np.int32))
@@ -342,9 +346,11 @@ class ShardedDeviceGraph:
             cgp.out_sched, cgp.out_lanes = vp(t_os), vp(t_ol)
             cgp.n_o4, cgp.n_o8, cgp.n_o16 = n_o_
             self.cg_phase.append(cgp)
+            # phase 1b (the second part) fused: the halo senders' lanes extrapolate their owned
+            # out-edges right after the scan (gtf_shard.phases bit 4): one launch, not two
             self.shard_phase.append(nat.GtfShard(vp(ts), int(part_s.size), int(pl.node_lo[rank]), int(pl.node_hi[rank]),
-                                                 int(pl.slot_lo[rank]), int(pl.slot_hi[rank]), 1, vp(tk),
-                                                 int(part_k.size), 0))
+                                                 int(pl.slot_lo[rank]), int(pl.slot_hi[rank]),
+                                                 1 if not self.shard_phase else 5, vp(tk), int(part_k.size), 0))
         self.shard_node = nat.GtfShard(vp(self.senders), int(self.senders.numel()), int(pl.node_lo[rank]),
                                        int(pl.node_hi[rank]), int(pl.slot_lo[rank]), int(pl.slot_hi[rank]), 2)
         self.split_sizes = {"interior_senders": int(self.shard_phase[0].n_senders),

@@ -325,7 +325,10 @@ typedef struct gtf_shard {
     int32_t slot_lo, slot_hi;
     /* ABI v6: the pass in phases, so the halo exchange can overlap the part that does not
      * read it (gtf.shard.ShardedDeviceGraph.step). phases = 0 (or 3): the whole pass; 1: the
-     * sender scan over `senders` and the extrapolation only; 2: the node kernels only.
+     * sender scan over `senders` and the extrapolation only; 2: the node kernels only; 5 (1 |
+     * 4): phase 1 fused sender-major -- every out-edge of `senders` into [slot_lo, slot_hi)
+     * extrapolated by its scan lane right after the scan (one launch; needs g->out_sched;
+     * slot_list unused).
      * slot_list (device, ascending, [n_slot_list]) or NULL: phase 1 extrapolates exactly these
      * owned slots instead of [slot_lo, slot_hi). A rank's pass as two phase-1 calls (the
      * senders whose state and out-edge activations are all its own, with the slots they

@@ -69,10 +69,14 @@ def test_split_phases_partition_and_interior_rule(world):
         brute = [u for u in snd.tolist() if owner[u] == r and
                  all(owner[dst[g.out_slot[i]]] == r for i in range(g.out_ptr[u], g.out_ptr[u + 1]))]
         assert s_in.tolist() == brute
-        src = g.slot["slot_src"][k_in]
-        assert np.isin(src, s_in).all()
+        src, ise = g.slot["slot_src"][k_in], g.slot["is_edge"][k_in].astype(bool)
+        assert np.isin(src[ise & (src >= 0)], s_in).all()        # the edges of phase 1a: interior senders'
         src_o = g.slot["slot_src"][k_out]
-        assert not np.isin(src_o[src_o >= 0], s_in).any()
+        assert g.slot["is_edge"][k_out].all() and (src_o >= 0).all() and not np.isin(src_o, s_in).any()
+        # phase 1b's slots are exactly the owned out-edges of the other senders (the fused form)
+        lo, hi = pl.slot_lo[r], pl.slot_hi[r]
+        outs_o = np.concatenate([g.out_slot[g.out_ptr[u]:g.out_ptr[u + 1]] for u in s_out] or [np.zeros(0, np.int64)])
+        assert np.array_equal(np.sort(outs_o[(outs_o >= lo) & (outs_o < hi)]), k_out)
         # the halo this rank receives never touches an interior sender or its out-edges
         assert not np.isin(hp.need_nodes[r], s_in).any()
         outs = np.concatenate([g.out_slot[g.out_ptr[u]:g.out_ptr[u + 1]] for u in s_in] or [np.zeros(0, np.int64)])

@@ -19,6 +19,7 @@ import numpy as np
 NAMES = {
     "k_sender": "k_sender",
     "k_sender_sched": "k_sender",
+    "k_sender_sched<false>": "k_sender",
     "k_extrapolate": "k_extrapolate",
     "k_node_multi<1, 3, 4, 3, 4, 5, 6, 2, 3, 4>": "k_node_multi<reweight,update>",
     "k_node_multi<10, 5, 8, 3>": "k_node_multi<cluster> (KL-distance kernel)",

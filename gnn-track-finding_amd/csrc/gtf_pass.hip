@@ -125,6 +125,12 @@ __device__ __forceinline__ double highland_var_ms(double a, double b, const doub
 // the fused sender-major form (gtf_shard.phases bit 4, a shard's halo-dependent senders):
 // every scanned edge into the owned slots [lo, hi) is extrapolated by its lane right after
 // the scan, with the running value in a register instead of the workspace
+#ifndef GTF_SEND_CHUNKS
+#define GTF_SEND_CHUNKS 2   // out-edge chunks per round of loads in the chunked sender scan (> 8 out-edges)
+#endif
+#ifndef GTF_SEND_KEEP_CARRY
+#define GTF_SEND_KEEP_CARRY 1   // 1: a sender's merged_cov[1, 1] stored only when an out-edge changed it
+#endif
 struct Fuse {
     gtf_states uts;
     int32_t lo, hi;
@@ -145,6 +151,7 @@ __device__ __forceinline__ void sender_scan(const gtf_graph& g, gtf_nodes& n, co
                            g.gnn[4 * (int64_t)u + 3]};
     const double* ng = ngl;
     double carry = n.merged_cov[5 * (int64_t)u + 3];
+    const double carry0 = carry;
     if constexpr (FUSED) {
         if (!hm) {   // no state to extrapolate: the owned slots still end their message passing
             for (int i = ob + gl; i < oe; i += SG) {
@@ -156,32 +163,55 @@ __device__ __forceinline__ void sender_scan(const gtf_graph& g, gtf_nodes& n, co
         }
     }
     if (!hm || ob == oe) return;
-    for (int base = ob; base < oe; base += SG) {
-        const int i = base + gl;
-        double vm = -1.0;
-        int k = -1;
-        if (i < oe) {
-            k = g.out_slot[i];
-            const int v = g.out_dst ? g.out_dst[i] : g.slot_dst[k];
-            const double nb[4] = {g.gnn[4 * (int64_t)v], g.gnn[4 * (int64_t)v + 1], g.gnn[4 * (int64_t)v + 2],
-                                  g.gnn[4 * (int64_t)v + 3]};   // loaded beside the activation, not after it
-            if (e.act[k] == 1) vm = highland_var_ms(a, b, ng, nb, p.endcap_boundary);
+    // NC chunks of SG out-edges per round of loads: their slot / receiver indices first, then
+    // the receivers' coordinates and activations, so a sender with up to NC * SG out-edges
+    // waits on two rounds instead of two per chunk (clamped indices past the end: loads of
+    // an address the group reads anyway)
+    constexpr int NC = FUSED ? 1 : GTF_SEND_CHUNKS;   // (the fused form: one extrapolation body)
+    for (int base = ob; base < oe; base += NC * SG) {
+        int kk[NC], vv[NC];
+#pragma unroll
+        for (int j = 0; j < NC; j++) {
+            const int i = min(base + j * SG + gl, oe - 1);
+            kk[j] = g.out_slot[i];
+            vv[j] = g.out_dst ? g.out_dst[i] : -1;
         }
-        double c = carry;
-        for (int m = 0; m < SG; m++) {
-            const double vmm = __shfl(vm, m, SG);
-            if (m <= gl && vmm != -1.0) c = c + vmm;
+        double nbv[NC][4];
+        uint8_t ac[NC];
+#pragma unroll
+        for (int j = 0; j < NC; j++) {
+            const int v = g.out_dst ? vv[j] : g.slot_dst[kk[j]];
+#pragma unroll
+            for (int q = 0; q < 4; q++) nbv[j][q] = g.gnn[4 * (int64_t)v + q];
+            ac[j] = e.act[kk[j]];
         }
-        // the running value of each active edge, stored in out-edge order (contiguous per
-        // sender: coalesced stores) when the graph has slot_outidx, else at its slot
-        if constexpr (FUSED) {
-            if (k >= fu->lo && k < fu->hi) extrap_slot(g, n, *(gtf_states*)&fu->uts, *(gtf_edges*)&e, p, w, k, true, c);
-        } else {
-            if (vm != -1.0) w.vc[g.slot_outidx ? i : k] = c;
+#pragma unroll
+        for (int j = 0; j < NC; j++) {
+            if (base + j * SG >= oe) break;   // group-uniform
+            const int i = base + j * SG + gl;
+            const int k = i < oe ? kk[j] : -1;
+            double vm = -1.0;
+            if (k >= 0 && ac[j] == 1) vm = highland_var_ms(a, b, ng, nbv[j], p.endcap_boundary);
+            double c = carry;
+            for (int m = 0; m < SG; m++) {
+                const double vmm = __shfl(vm, m, SG);
+                if (m <= gl && vmm != -1.0) c = c + vmm;
+            }
+            // the running value of each active edge, stored in out-edge order (contiguous per
+            // sender: coalesced stores) when the graph has slot_outidx, else at its slot
+            if constexpr (FUSED) {
+                if (k >= fu->lo && k < fu->hi)
+                    extrap_slot(g, n, *(gtf_states*)&fu->uts, *(gtf_edges*)&e, p, w, k, true, c);
+            } else {
+                if (vm != -1.0) w.vc[g.slot_outidx ? i : k] = c;
+            }
+            carry = __shfl(c, SG - 1, SG);  // lanes past the end carry the full sum
         }
-        carry = __shfl(c, SG - 1, SG);  // lanes past the end carry the full sum
     }
-    if (gl == 0) n.merged_cov[5 * (int64_t)u + 3] = carry;
+    // the aliased merged_cov[1, 1] (:127-128) only where an active out-edge added to it
+    // (compared as bits: -0.0 + 0.0 is +0.0)
+    if (gl == 0 && (!GTF_SEND_KEEP_CARRY || __double_as_longlong(carry) != __double_as_longlong(carry0)))
+        n.merged_cov[5 * (int64_t)u + 3] = carry;
 }
 
 // one sender u whose out-edges fit the group (<= G), lane gl holding out-edge slot k
@@ -218,7 +248,8 @@ __device__ __forceinline__ void sender_scan_lane(const gtf_graph& g, gtf_nodes& 
     }
     if (!FUSED && vm != -1.0) w.vc[g.slot_outidx ? ob + gl : k] = c;
     const double fin = __shfl(c, G - 1, G);   // the last lane has every active edge's term
-    if (gl == 0) n.merged_cov[5 * (int64_t)u + 3] = fin;
+    if (gl == 0 && (!GTF_SEND_KEEP_CARRY || __double_as_longlong(fin) != __double_as_longlong(carry)))
+        n.merged_cov[5 * (int64_t)u + 3] = fin;
     if constexpr (FUSED) {
         if (k >= fu->lo && k < fu->hi) extrap_slot(g, n, *(gtf_states*)&fu->uts, *(gtf_edges*)&e, p, w, k, true, c);
     }
@@ -336,6 +367,9 @@ __global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(GTF_SEND
 // ---------------------------------------------------------------------------
 // k_extrapolate: one slot (edge u -> v) per thread
 // ---------------------------------------------------------------------------
+#ifndef GTF_EXTRAP_PRED
+#define GTF_EXTRAP_PRED 1   // 1: k_extrapolate's gathers predicated on an active edge with a sender
+#endif
 #ifndef GTF_EXTRAP_WAVES
 #define GTF_EXTRAP_WAVES 0   // > 0: amdgpu_waves_per_eu lower bound (register budget) of k_extrapolate
 #endif
@@ -358,8 +392,29 @@ __device__ __forceinline__ void extrap_slot(const gtf_graph& g, gtf_nodes& n, gt
     // written by k_sender for active edges of merged senders: in out-edge order through
     // slot_outidx (one gather beside the sender's), or by slot
     const int oi = (have_vc || !g.slot_outidx) ? k : g.slot_outidx[k];
-    const double vc = have_vc ? vc_given : w.vc[oi >= 0 ? oi : 0];
     const double smw = e.send_mw[k];
+#if GTF_EXTRAP_PRED
+    // the sender / receiver gathers only for the slots that can extrapolate (an active edge
+    // with a sender): the same second level of loads, without the ~170 bytes per slot the
+    // keys without an edge and the deactivated edges would fetch for nothing
+    const bool go = is_edge && src >= 0 && act == 1;
+    double vc = 0.0, node_x = 0.0, node_y = 0.0, node_z = 0.0, node_r = 0.0, nbx = 0.0, nby = 0.0, nbz = 0.0,
+           nbr = 0.0, a = 0.0, b = 0.0, c = 0.0, mc00 = 0.0, mc01 = 0.0, mc10 = 0.0, mc22 = 0.0;
+    uint8_t hm = 0;
+    if (go) {
+        vc = have_vc ? vc_given : w.vc[oi >= 0 ? oi : 0];
+        const double* ng = g.gnn + 4 * (int64_t)src;  // sender ("node" in the reference)
+        const double* nb = g.gnn + 4 * (int64_t)v;    // receiver ("neighbour")
+        hm = n.has_merged[src];
+        node_x = ng[0]; node_y = ng[1]; node_z = ng[2]; node_r = ng[3];
+        nbx = nb[0]; nby = nb[1]; nbz = nb[2]; nbr = nb[3];
+        a = n.merged_state[3 * src + 0]; b = n.merged_state[3 * src + 1]; c = n.merged_state[3 * src + 2];
+        const double* mcp = n.merged_cov + 5 * (int64_t)src;
+        mc00 = mcp[0]; mc01 = mcp[1]; mc10 = mcp[2]; mc22 = mcp[4];
+    }
+    if (!go || !hm) {
+#else
+    const double vc = have_vc ? vc_given : w.vc[oi >= 0 ? oi : 0];
     const int u = src >= 0 ? src : 0;   // orphan keys have no sender
     const double* ng = g.gnn + 4 * (int64_t)u;  // sender ("node" in the reference)
     const double* nb = g.gnn + 4 * (int64_t)v;  // receiver ("neighbour")
@@ -370,6 +425,7 @@ __device__ __forceinline__ void extrap_slot(const gtf_graph& g, gtf_nodes& n, gt
     const double* mcp = n.merged_cov + 5 * (int64_t)u;
     const double mc00 = mcp[0], mc01 = mcp[1], mc10 = mcp[2], mc22 = mcp[4];
     if (!is_edge || src < 0 || !hm || act != 1) {
+#endif
         if (f_old & 1) uts.fresh[k] = f_old & 2;
         return;
     }

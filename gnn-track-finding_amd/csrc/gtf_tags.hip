@@ -421,6 +421,14 @@ size_t gtf_tag_workspace_bytes(int32_t n_nodes, int32_t n_edges) {
     return tag_align(TAG_HDR) + tag_align(e) + tag_align(n) + tag_align(sizeof(int64_t) * n);
 }
 
+static int32_t* tag_readback_buffer() {
+    static thread_local int32_t* buf = nullptr;
+    if (!buf && hipHostMalloc((void**)&buf, (64 + TAG_RING * TAG_CTR) * sizeof(int32_t), hipHostMallocPortable) !=
+                    hipSuccess)
+        buf = nullptr;
+    return buf;
+}
+
 // The whole stage behind one call: prepare, then the sweeps (the loop of
 // tag_propagation.py:130-164, first sweep unconditional) in batches of 2, 4, 8, ... launches
 // whose stop test runs on the device (TagCtl), the tag arrays ping-ponging between `tags` and
@@ -458,8 +466,11 @@ int gtf_tag_propagate(const gtf_graph* g, const double* radius, int64_t* tags, d
         return hip_fail("gtf_tag_propagate");
     if (int rc = tag_prepare(g, radius, keep, proc, hdr, false, st)) return rc;
     int32_t s = 0, batch = 2, executed = 0;
-    std::vector<int32_t> host(64 + TAG_RING * TAG_CTR);   // the header words, then the ring
-    int32_t* hring = host.data() + 64;
+    // the header words, then the ring: read back into page-locked memory (one per host
+    // thread, kept), so the copy is a direct DMA instead of a staged pageable one
+    int32_t* host = tag_readback_buffer();
+    if (!host) return hip_fail("gtf_tag_propagate: page-locked read-back buffer");
+    int32_t* hring = host + 64;
     bool stopped = false;
     while (!stopped && s < max_sweeps) {
         const int32_t at = s % TAG_RING;
@@ -478,7 +489,7 @@ int gtf_tag_propagate(const gtf_graph* g, const double* radius, int64_t* tags, d
                 return rc;
         }
         // one read-back: the header words through the batch's last counter
-        if (hipMemcpyAsync(host.data(), hdr, (64 + (at + nb) * TAG_CTR) * sizeof(int32_t), hipMemcpyDeviceToHost,
+        if (hipMemcpyAsync(host, hdr, (64 + (at + nb) * TAG_CTR) * sizeof(int32_t), hipMemcpyDeviceToHost,
                            st) != hipSuccess ||
             hipStreamSynchronize(st) != hipSuccess)
             return hip_fail("gtf_tag_propagate: reading the flip counts");

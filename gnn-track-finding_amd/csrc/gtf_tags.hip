@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 
 #include <vector>
 
@@ -78,8 +79,16 @@ __global__ void __launch_bounds__(BLOCK) k_count_flags(const uint8_t* f, int n, 
 }
 
 // keep[e] = neighbour radius <= node radius (:99-110); processed[u] = any kept (:109-110)
+// zero (may be NULL): nzero int32 words zeroed by block 0 (the stop-rule words the count
+// kernel and the sweeps that follow add to)
+__device__ __forceinline__ void zero_words(int32_t* zero, int nzero) {
+    if (zero && blockIdx.x == 0)
+        for (int i = (int)threadIdx.x; i < nzero; i += BLOCK) zero[i] = 0;
+}
+
 __global__ void __launch_bounds__(BLOCK) k_tag_prepare(gtf_graph g, const double* radius, uint8_t* keep,
-                                                       uint8_t* processed) {
+                                                       uint8_t* processed, int32_t* zero, int nzero) {
+    zero_words(zero, nzero);
     const int u = gtf::xcd_local(blockIdx.x, gridDim.x) * BLOCK + threadIdx.x;
     if (u < g.n_nodes) {
         const double ru = radius[u];
@@ -135,7 +144,9 @@ struct PrepBuckets {
 };
 
 __global__ void __launch_bounds__(BLOCK) k_tag_prepare_sched(gtf_graph g, const double* radius, uint8_t* keep,
-                                                             uint8_t* processed, PrepBuckets pb) {
+                                                             uint8_t* processed, PrepBuckets pb, int32_t* zero,
+                                                             int nzero) {
+    zero_words(zero, nzero);
     int b = blockIdx.x;
     if (b < pb.blocks[0]) {
         prep_group<4>(g, radius, keep, processed, pb.list[0], pb.lanes[0], pb.count[0], b);
@@ -160,6 +171,7 @@ struct TagCtl {
     int32_t* stop;          // set once the rule stops the loop
     int32_t* nexec;         // sweeps executed
     double thr;
+    int32_t* next;          // the next sweep's counter shards, zeroed by block 0 (NULL: the caller zeroes)
 };
 
 __device__ __forceinline__ bool tag_skip(const TagCtl& c) {
@@ -174,7 +186,26 @@ __device__ __forceinline__ bool tag_skip(const TagCtl& c) {
         }
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(c.nexec, 1);
+    if (c.next && blockIdx.x == 0 && threadIdx.x < TAG_SHARDS) c.next[threadIdx.x * TAG_STRIDE] = 0;
     return false;
+}
+
+// the batch's stop-rule words and per-sweep flip totals into the caller's page-locked report
+// (mapped, coherent): rep[1..3] = processed, stop, executed; rep[4 + i] = flips of sweep s + i;
+// rep[0] = seq last, after a system-scope fence, so the host that sees seq sees the rest
+__global__ void __launch_bounds__(64) k_tag_report(const int32_t* hdr, const int32_t* ring, int s, int nb, int ring_n,
+                                                   int32_t* rep, int32_t seq) {
+    const int t = (int)threadIdx.x;
+    if (t < nb) {
+        const int32_t* c = ring + (size_t)((s + t) % ring_n) * TAG_SHARDS * TAG_STRIDE;
+        int f = 0;
+        for (int k = 0; k < TAG_SHARDS; k++) f += c[k * TAG_STRIDE];
+        rep[4 + t] = f;
+    }
+    if (t < 3) rep[1 + t] = hdr[t];
+    __threadfence_system();
+    __syncthreads();
+    if (t == 0) __hip_atomic_store(rep, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // the final tags into the caller's array: after an odd number of executed sweeps they sit
@@ -330,9 +361,14 @@ static int hip_fail(const char* what) {
 }
 
 // zero_count: n_processed zeroed here (else the caller has)
+// zero_count: n_processed zeroed here (else the caller has, or the prepare launch zeroes the
+// nzero words at `zero`, n_processed among them)
 static int tag_prepare(const gtf_graph* g, const double* radius, uint8_t* keep, uint8_t* processed,
-                       int32_t* n_processed, bool zero_count, hipStream_t st) {
+                       int32_t* n_processed, bool zero_count, hipStream_t st, int32_t* zero = nullptr,
+                       int nzero = 0) {
     if (zero_count && hipMemsetAsync(n_processed, 0, sizeof(int32_t), st) != hipSuccess)
+        return hip_fail("gtf_tag_prepare");
+    if (g->n_nodes <= 0 && zero && hipMemsetAsync(zero, 0, nzero * sizeof(int32_t), st) != hipSuccess)
         return hip_fail("gtf_tag_prepare");
     if (g->n_nodes > 0 && g->out_sched) {   // lane groups over the sender schedule
         PrepBuckets pb;
@@ -350,10 +386,11 @@ static int tag_prepare(const gtf_graph* g, const double* radius, uint8_t* keep, 
             total += pb.blocks[q];
         }
         total += (g->n_nodes + BLOCK - 1) / BLOCK;   // nodes without an out-edge
-        hipLaunchKernelGGL(k_tag_prepare_sched, dim3(total), dim3(BLOCK), 0, st, *g, radius, keep, processed, pb);
+        hipLaunchKernelGGL(k_tag_prepare_sched, dim3(total), dim3(BLOCK), 0, st, *g, radius, keep, processed, pb,
+                           zero, nzero);
     } else if (g->n_nodes > 0) {
         hipLaunchKernelGGL(k_tag_prepare, dim3((g->n_nodes + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, st, *g, radius,
-                           keep, processed);
+                           keep, processed, zero, nzero);
     }
     if (g->n_nodes > 0) {   // the processed count: a reduction of the processed bytes
         int blocks = (g->n_nodes / 16 + BLOCK * 4 - 1) / (BLOCK * 4);   // ~4 steps per thread
@@ -404,7 +441,7 @@ static int tag_sweep(const gtf_graph* g, const uint8_t* keep, const uint8_t* pro
 int gtf_tag_sweep(const gtf_graph* g, const uint8_t* keep, const uint8_t* processed, const int64_t* tags_in,
                   int64_t* tags_out, int32_t* flips, gtf_stream_t stream) {
     if (int rc = gtf::check_abi(g, "gtf_tag_sweep")) return rc;
-    const TagCtl none{nullptr, nullptr, nullptr, nullptr, 0.0};
+    const TagCtl none{nullptr, nullptr, nullptr, nullptr, 0.0, nullptr};
     return tag_sweep(g, keep, processed, tags_in, tags_out, flips, 1, none, (hipStream_t)stream);
 }
 
@@ -419,6 +456,73 @@ constexpr size_t TAG_HDR = 64 * sizeof(int32_t) + TAG_RING * TAG_CTR * sizeof(in
 size_t gtf_tag_workspace_bytes(int32_t n_nodes, int32_t n_edges) {
     const size_t n = n_nodes > 0 ? (size_t)n_nodes : 1, e = n_edges > 0 ? (size_t)n_edges : 1;
     return tag_align(TAG_HDR) + tag_align(e) + tag_align(n) + tag_align(sizeof(int64_t) * n);
+}
+
+// batches of sweeps between two reads of the stop-rule words: at most the report's 64 totals
+constexpr int32_t TAG_MAX_BATCH = 64;
+
+// the mapped report of gtf_tag_propagate (one per host thread, kept): 4 header words + the
+// flip totals of one batch. Coherent page-locked memory: the report kernel's system-scope
+// stores reach the host while the stream runs.
+struct TagReport {
+    int32_t* host = nullptr;
+    int32_t* dev = nullptr;
+    int32_t seq = 0;
+};
+static TagReport& tag_report() {
+    static thread_local TagReport r;
+    static thread_local bool tried = false;
+    if (!tried) {
+        tried = true;
+        void* h = nullptr;
+        if (hipHostMalloc(&h, (4 + TAG_MAX_BATCH) * sizeof(int32_t),
+                          hipHostMallocMapped | hipHostMallocCoherent | hipHostMallocPortable) == hipSuccess) {
+            void* d = nullptr;
+            if (hipHostGetDevicePointer(&d, h, 0) == hipSuccess) {
+                r.host = static_cast<int32_t*>(h);
+                r.dev = static_cast<int32_t*>(d);
+                __atomic_store_n(r.host, 0, __ATOMIC_RELAXED);
+            } else {
+                (void)hipHostFree(h);
+            }
+        }
+        (void)hipGetLastError();
+    }
+    return r;
+}
+static int32_t* tag_report_buffer() { return tag_report().host; }
+static int32_t* tag_report_dev() { return tag_report().dev; }
+static int32_t tag_next_seq() {
+    TagReport& r = tag_report();
+    r.seq = r.seq == INT32_MAX ? 1 : r.seq + 1;
+    return r.seq;
+}
+static bool tag_poll_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("GTF_TAG_POLL");   // 0: the copy-and-synchronise read-back
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+// the host waits for the report's sequence word; a stream that finished (or failed) without it
+// showing ends the wait -- then the words are re-read once after the stream's completion
+static int tag_wait_report(int32_t* rep, int32_t seq, hipStream_t st) {
+    for (uint64_t spin = 1;; spin++) {
+        if (__atomic_load_n(rep, __ATOMIC_ACQUIRE) == seq) break;
+        if ((spin & 255) == 0) {
+            const hipError_t q = hipStreamQuery(st);
+            if (q == hipSuccess) {
+                if (__atomic_load_n(rep, __ATOMIC_ACQUIRE) == seq) break;
+                (void)hipGetLastError();
+                gtf::set_error("gtf_tag_propagate: the report did not reach the host");
+                return -1;
+            }
+            if (q != hipErrorNotReady) return hip_fail("gtf_tag_propagate: waiting for the report");
+        }
+        __builtin_ia32_pause();
+    }
+    (void)hipGetLastError();   // (a not-ready query leaves its status behind)
+    return 0;
 }
 
 static int32_t* tag_readback_buffer() {
@@ -460,52 +564,68 @@ int gtf_tag_propagate(const gtf_graph* g, const double* radius, int64_t* tags, d
     w += tag_align(n);
     int64_t* other = reinterpret_cast<int64_t*>(w);
     *sweeps_out = 0;
-    // the header words and the first pass over the ring's counters zeroed in one memset
-    const int32_t ring0 = max_sweeps < TAG_RING ? max_sweeps : TAG_RING;
-    if (hipMemsetAsync(hdr, 0, (64 + ring0 * TAG_CTR) * sizeof(int32_t), st) != hipSuccess)
-        return hip_fail("gtf_tag_propagate");
-    if (int rc = tag_prepare(g, radius, keep, proc, hdr, false, st)) return rc;
+    // the header words and the first sweep's counter shards zeroed by the prepare launch; every
+    // executed sweep zeroes the next one's (TagCtl.next)
+    int32_t* hostrep = tag_report_buffer();   // mapped page-locked report (NULL: read back by copy)
+    const bool poll = hostrep && tag_poll_enabled();
+    if (int rc = tag_prepare(g, radius, keep, proc, hdr, false, st, hdr, 64 + (int)TAG_CTR)) return rc;
     int32_t s = 0, batch = 2, executed = 0;
-    // the header words, then the ring: read back into page-locked memory (one per host
-    // thread, kept), so the copy is a direct DMA instead of a staged pageable one
-    int32_t* host = tag_readback_buffer();
-    if (!host) return hip_fail("gtf_tag_propagate: page-locked read-back buffer");
-    int32_t* hring = host + 64;
+    int32_t* host = poll ? nullptr : tag_readback_buffer();   // the header words, then the ring
+    if (!poll && !host) return hip_fail("gtf_tag_propagate: page-locked read-back buffer");
     bool stopped = false;
     while (!stopped && s < max_sweeps) {
         const int32_t at = s % TAG_RING;
         int32_t nb = batch < max_sweeps - s ? batch : max_sweeps - s;
         if (nb > TAG_RING - at) nb = TAG_RING - at;   // the batch's counters stay contiguous in the ring
-        if (s >= TAG_RING &&   // (a later pass over the ring: its counters zeroed again)
-            hipMemsetAsync(ring + at * TAG_CTR, 0, nb * TAG_CTR * sizeof(int32_t), st) != hipSuccess)
-            return hip_fail("gtf_tag_propagate: zeroing the flip counters");
         for (int32_t i = 0; i < nb; i++) {
             const int32_t q = s + i;
             const TagCtl ctl{hdr, q > 0 ? ring + ((q - 1) % TAG_RING) * TAG_CTR : nullptr, hdr + 1, hdr + 2,
-                             flip_threshold};
+                             flip_threshold, ring + ((q + 1) % TAG_RING) * TAG_CTR};
             int64_t* tin = (q & 1) ? other : tags;
             int64_t* tout = (q & 1) ? tags : other;
             if (int rc = tag_sweep(g, keep, proc, tin, tout, ring + (q % TAG_RING) * TAG_CTR, TAG_SHARDS, ctl, st))
                 return rc;
         }
-        // one read-back: the header words through the batch's last counter
-        if (hipMemcpyAsync(host, hdr, (64 + (at + nb) * TAG_CTR) * sizeof(int32_t), hipMemcpyDeviceToHost,
-                           st) != hipSuccess ||
-            hipStreamSynchronize(st) != hipSuccess)
-            return hip_fail("gtf_tag_propagate: reading the flip counts");
-        executed = host[2];
+        int32_t words[3];   // processed, stop, executed
+        const int32_t* fl;  // flips of sweeps s, s + 1, ...
+        std::vector<int32_t> tot;
+        if (poll) {
+            // one small launch writes the words and the batch's flip totals into the mapped report;
+            // the host waits for its sequence word instead of a copy and a stream synchronisation
+            const int32_t seq = tag_next_seq();
+            hipLaunchKernelGGL(k_tag_report, dim3(1), dim3(64), 0, st, hdr, ring, s, nb, TAG_RING, tag_report_dev(),
+                               seq);
+            if (hipGetLastError() != hipSuccess) return hip_fail("gtf_tag_propagate: report launch");
+            if (int rc = tag_wait_report(hostrep, seq, st)) return rc;
+            for (int k = 0; k < 3; k++) words[k] = hostrep[1 + k];
+            fl = hostrep + 4;
+        } else {
+            // one read-back: the header words through the batch's last counter
+            if (hipMemcpyAsync(host, hdr, (64 + (at + nb) * TAG_CTR) * sizeof(int32_t), hipMemcpyDeviceToHost, st) !=
+                    hipSuccess ||
+                hipStreamSynchronize(st) != hipSuccess)
+                return hip_fail("gtf_tag_propagate: reading the flip counts");
+            for (int k = 0; k < 3; k++) words[k] = host[k];
+            tot.resize(nb);
+            for (int32_t i = 0; i < nb; i++) {
+                const int32_t* c = host + 64 + (at + i) * TAG_CTR;
+                int32_t f = 0;
+                for (int k = 0; k < TAG_SHARDS; k++) f += c[k * TAG_STRIDE];
+                tot[i] = f;
+            }
+            fl = tot.data();
+        }
+        executed = words[2];
         for (int32_t q = s; q < executed; q++) {
-            int32_t f = 0;
-            const int32_t* c = hring + (q % TAG_RING) * TAG_CTR;
-            for (int k = 0; k < TAG_SHARDS; k++) f += c[k * TAG_STRIDE];
+            const int32_t f = fl[q - s];
             if (flips_out) flips_out[q] = f;
             // the rule on the host too: the batch's last executed sweep may already stop it
-            const double frac = host[0] ? (double)f / (double)host[0] : 0.0;
+            const double frac = words[0] ? (double)f / (double)words[0] : 0.0;
             if (q == executed - 1 && !(frac > flip_threshold)) stopped = true;
         }
-        stopped = stopped || host[1] != 0 || executed < s + nb;
+        stopped = stopped || words[1] != 0 || executed < s + nb;
         s = executed;
-        if (batch < TAG_RING / 2) batch *= 2;
+        if (batch < TAG_MAX_BATCH) batch *= 2;
     }
     *sweeps_out = executed;
     if (g->n_nodes > 0) {

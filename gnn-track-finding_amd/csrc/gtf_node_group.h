@@ -534,7 +534,8 @@ __device__ __forceinline__ void g_ranks(NodeCtx<G>& c) {
 // which keys are present and in what order (GTF_EARLY_STAGE).
 template <int CAP>
 #ifndef GTF_STAGE_NOINV
-#define GTF_STAGE_NOINV 3   // (with GTF_KL_LEAN) 3 = 2x2-block inverses staged after the pair loop (below);
+#define GTF_STAGE_NOINV 2   // (with GTF_KL_LEAN) 3 = 2x2-block inverses staged after the pair loop (below;
+                            // one division per merge instead of three, but 3 VGPRs spill: 3.5 us slower);
                             // no inverses in LDS: 1 = in the owning lane's registers,
                             // 2 = recomputed from the staged covariances where used
 #endif

@@ -497,12 +497,9 @@ static int32_t tag_next_seq() {
     r.seq = r.seq == INT32_MAX ? 1 : r.seq + 1;
     return r.seq;
 }
-static bool tag_poll_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("GTF_TAG_POLL");   // 0: the copy-and-synchronise read-back
-        return !(e && e[0] == '0');
-    }();
-    return on;
+static bool tag_poll_enabled() {   // (read per call: a test switches it in-process)
+    const char* e = getenv("GTF_TAG_POLL");   // 0: the copy-and-synchronise read-back
+    return !(e && e[0] == '0');
 }
 // the host waits for the report's sequence word; a stream that finished (or failed) without it
 // showing ends the wait -- then the words are re-read once after the stream's completion

@@ -122,12 +122,15 @@ def test_tag_propagate_one_call():
                                ctypes.c_void_p(ws.data_ptr()), nb - 1, d.stream) != 0
 
 
+@pytest.mark.parametrize("poll", ["1", "0"])
 @pytest.mark.parametrize("schedule", [True, False])
 @pytest.mark.parametrize("max_sweeps", [64, 3, 0])
-def test_tag_propagate_stop_rule_and_cap(schedule, max_sweeps):
+def test_tag_propagate_stop_rule_and_cap(schedule, max_sweeps, poll, monkeypatch):
     """the stop rule evaluated on the device (gtf_tag_propagate's batched sweeps): the
     reference's flip vector, cut at max_sweeps, on the sender-schedule and the thread-per-node
-    kernels; the tags equal the host loop of single sweeps run that many times"""
+    kernels, with the batch report polled in mapped memory or copied back (GTF_TAG_POLL); the
+    tags equal the host loop of single sweeps run that many times"""
+    monkeypatch.setenv("GTF_TAG_POLL", poll)
     import ctypes
     import torch
     from gtf import _native as nat
@@ -161,6 +164,59 @@ def test_tag_propagate_stop_rule_and_cap(schedule, max_sweeps):
         ta, tb = tb, ta
     torch.cuda.synchronize()
     assert torch.equal(tags, ta)
+
+
+def _chain_graph(n):
+    """n nodes, edges u -> u + 1, radius falling along the chain and tag[u] = u: every sweep
+    carries the largest tag one hop down, so the stage runs n sweeps with flips n-1, ..., 1, 0
+    (flip threshold 0)"""
+    from gtf.graph import TrackGraph, NODE_FIELDS, SLOT_FIELDS, empty_arrays
+    node = empty_arrays(NODE_FIELDS, n)
+    slot = empty_arrays(SLOT_FIELDS, n - 1)
+    node["gnn"][:] = 1.0
+    node["xyzr"][:] = 1.0
+    node["xyzr"][:, 3] = np.arange(n, 0, -1, dtype=np.float64)
+    node["tag"][:] = np.arange(n)
+    node["layer"][:] = np.arange(n) % 7
+    slot["slot_src"][:] = np.arange(n - 1)
+    slot["slot_key"][:] = np.arange(n - 1)
+    slot["is_edge"][:] = 1
+    slot["act"][:] = 1
+    slot_ptr = np.concatenate([[0], np.arange(n - 1)]).astype(np.int32)
+    slot_ptr = np.concatenate([slot_ptr, [n - 1]]).astype(np.int32)
+    out_ptr = np.concatenate([np.arange(n), [n - 1]]).astype(np.int32)
+    return TrackGraph(n, n - 1, slot_ptr, out_ptr, np.arange(n - 1, dtype=np.int32), node, slot)
+
+
+@pytest.mark.parametrize("poll", ["1", "0"])
+@pytest.mark.parametrize("schedule", [True, False])
+def test_tag_propagate_long_run(schedule, poll, monkeypatch):
+    """300 sweeps in one gtf_tag_propagate call: batches of 2 .. 64 launches, the flip-counter
+    ring (128 sweeps) wrapped twice with every sweep zeroing the next one's counters"""
+    monkeypatch.setenv("GTF_TAG_POLL", poll)
+    import ctypes
+    import torch
+    from gtf import _native as nat
+    from gtf.device import DeviceGraph
+    n = 300
+    g = _chain_graph(n)
+    d = DeviceGraph(g, schedule=schedule)
+    L = d.lib
+    tags = torch.arange(n, dtype=torch.int64, device=d.device)
+    radius = torch.from_numpy(np.ascontiguousarray(g.node["xyzr"][:, 3])).to(d.device)
+    nb = L.gtf_tag_workspace_bytes(g.n_nodes, g.n_edges)
+    ws = torch.full((nb,), 0xFF, dtype=torch.uint8, device=d.device)
+    flips = (ctypes.c_int32 * 512)()
+    sweeps = ctypes.c_int32(-1)
+    nat.check(L.gtf_tag_propagate(ctypes.byref(d.cg), ctypes.c_void_p(radius.data_ptr()),
+                                  ctypes.c_void_p(tags.data_ptr()), 0.0, 512,
+                                  ctypes.cast(flips, ctypes.c_void_p), ctypes.byref(sweeps),
+                                  ctypes.c_void_p(ws.data_ptr()), nb, d.stream))
+    torch.cuda.synchronize()
+    want_tags, want_flips = O.tag_propagation(g, 0.0)
+    assert want_flips == list(range(n - 1, -1, -1))
+    assert sweeps.value == len(want_flips) and list(flips[:sweeps.value]) == want_flips
+    assert np.array_equal(tags.cpu().numpy(), want_tags)
 
 
 def test_workspace_init_contract():

@@ -593,6 +593,25 @@ __device__ __forceinline__ TauGeo stage_geo(const Stage* s, int i, double szb2, 
     return t;
 }
 
+#ifndef GTF_OP_TIMING
+#define GTF_OP_TIMING 0
+#endif
+#if GTF_OP_TIMING
+#define GTF_OP_TIMING_WAVES 65536
+__device__ uint64_t g_op_time[GTF_OP_TIMING_WAVES * 24];
+// a stamp inside an op (words 19 and 22 of the wave's row), lane 0 only
+#define GTF_SUBSTAMP(word)                                                                        \
+    do {                                                                                          \
+        const int wv_ = (int)((blockIdx.x * blockDim.x + threadIdx.x) / 64);                      \
+        if ((threadIdx.x & 63) == 0 && wv_ < GTF_OP_TIMING_WAVES)                                 \
+            g_op_time[24 * (int64_t)wv_ + (word)] = __builtin_readcyclecounter();                  \
+    } while (0)
+#else
+#define GTF_SUBSTAMP(word) \
+    do {                   \
+    } while (0)
+#endif
+
 // pairwise chi2 + greedy KL merging of one node (clustering.py:197-307). The
 // d(d-1)/2 pairs are dealt round-robin over the G lanes (row-major pair index t),
 // so the np.where tie order is the order of t. The parabolic and the joint merge
@@ -632,6 +651,7 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
         stg->ord[sb + pos] = (uint8_t)c.grp.gl;
     }
     wave_lds_sync();
+    GTF_SUBSTAMP(22);   // (diagnostics) the states staged
     const double szb2 = p.sigma0rz2 * p.sigma0rz2, srb2 = p.sigma0rz * p.sigma0rz;   // barrel sigma_z^2, sigma_r^2
     const bool ec = fabs(xa) >= p.endcap_boundary;
     const double sza = ec ? p.sigma0rz : p.sigma0rz2, sra = ec ? p.sigma0rz2 : p.sigma0rz;
@@ -698,6 +718,7 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
         fold(pair_d(i, j), t, i, j);
     }
 #endif
+    GTF_SUBSTAMP(19);   // (diagnostics) the pair loop done
     if (!c.grp.any(lnz)) {
         if (c.grp.gl == 0) raise_node(err, c.v, GTF_ERR_ALL_ZERO_DIST);
         return;
@@ -1110,12 +1131,7 @@ __device__ __forceinline__ bool ops_have_fresh(const NodeOps& ops) {
 // op of the sequence and after its stores (row of 24 words per wave; word 23 = G), read
 // back by gtf_op_timing (tools/op_timing.py); words 20 / 21 = the chip-wide real-time
 // clock at the start / end (the shader clocks of different XCDs are not aligned)
-#ifndef GTF_OP_TIMING
-#define GTF_OP_TIMING 0
-#endif
 #if GTF_OP_TIMING
-#define GTF_OP_TIMING_WAVES 65536
-__device__ uint64_t g_op_time[GTF_OP_TIMING_WAVES * 24];
 template <int G, int OP, typename Stage>
 __device__ __forceinline__ void node_op_timed(NodeCtx<G>& c, const gtf_graph& g, gtf_nodes& n, gtf_states& tse,
                                               gtf_states& uts, gtf_edges& e, const gtf_params& p, const Ws& w, double* sval,

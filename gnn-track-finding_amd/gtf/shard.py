@@ -33,6 +33,7 @@ exchange) before results are read back.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import numpy as np
 
@@ -346,11 +347,14 @@ class ShardedDeviceGraph:
             cgp.out_sched, cgp.out_lanes = vp(t_os), vp(t_ol)
             cgp.n_o4, cgp.n_o8, cgp.n_o16 = n_o_
             self.cg_phase.append(cgp)
-            # phase 1b (the second part) fused: the halo senders' lanes extrapolate their owned
-            # out-edges right after the scan (gtf_shard.phases bit 4): one launch, not two
+            # phase 1b (the second part): the halo senders' scan, then their owned slots; or
+            # fused (GTF_SHARD_FUSED_1B=1, gtf_shard.phases bit 4: the scan's lanes extrapolate
+            # their owned out-edges, one launch) -- measured slower on the box (N = 8: 18.0 vs
+            # 14.7 us; the fused kernel runs 3 waves per SIMD at 145 VGPRs)
+            ph = 5 if (self.shard_phase and os.environ.get("GTF_SHARD_FUSED_1B", "0") == "1") else 1
             self.shard_phase.append(nat.GtfShard(vp(ts), int(part_s.size), int(pl.node_lo[rank]), int(pl.node_hi[rank]),
                                                  int(pl.slot_lo[rank]), int(pl.slot_hi[rank]),
-                                                 1 if not self.shard_phase else 5, vp(tk), int(part_k.size), 0))
+                                                 ph, vp(tk), int(part_k.size), 0))
         self.shard_node = nat.GtfShard(vp(self.senders), int(self.senders.numel()), int(pl.node_lo[rank]),
                                        int(pl.node_hi[rank]), int(pl.slot_lo[rank]), int(pl.slot_hi[rank]), 2)
         self.split_sizes = {"interior_senders": int(self.shard_phase[0].n_senders),

@@ -86,8 +86,11 @@ def single_gpu():
     return g, outs
 
 
-@pytest.mark.parametrize("world", [2, 4, 8])
-def test_sharded_c4_equals_single_gpu_and_digest(world, single_gpu, tmp_path):
+@pytest.mark.parametrize("world,fused_1b", [(2, "0"), (4, "0"), (8, "0"), (8, "1")])
+def test_sharded_c4_equals_single_gpu_and_digest(world, fused_1b, single_gpu, tmp_path, monkeypatch):
+    """fused_1b: phase 1b as one sender-major launch (GTF_SHARD_FUSED_1B, gtf_shard.phases bit 4),
+    inherited by the spawned ranks"""
+    monkeypatch.setenv("GTF_SHARD_FUSED_1B", fused_1b)
     import torch.multiprocessing as mp
     from test_gpu_c4_digest import _digest, digest_errors
     g, ref = single_gpu

@@ -63,6 +63,19 @@ for G in sorted(set(rows[:, 23].tolist()), reverse=True):
                            "end_last_us": float((r[:, 21].max() - t0) / RT),
                            "phases_mean": {n: float(v) for n, v in zip(names, ph.mean(axis=0))},
                            "phases_p90": {n: float(v) for n, v in zip(names, np.percentile(ph, 90, axis=0))}}
+# inside the clustering (words 22 / 19: the states staged, the pair loop done), waves whose
+# first lane group clustered
+ic = OPS.index("cluster_uts") + 1   # row index of the stamp before the clustering op
+for G in sorted(set(rows[:, 23].tolist()), reverse=True):
+    r = rows[(rows[:, 23] == G) & (rows[:, 22] > 0) & (rows[:, 19] > 0)]
+    if r.shape[0] == 0:
+        continue
+    out["by_G"][int(G)]["cluster_split"] = {
+        "waves": int(r.shape[0]),
+        "stage_mean": float((r[:, 22] - r[:, ic]).mean()),
+        "pairs_mean": float((r[:, 19] - r[:, 22]).mean()),
+        "merge_store_mean": float((r[:, ic + 1] - r[:, 19]).mean()),
+        "rest_of_wave_mean": float(((r[:, NP - 1] - r[:, 0]) - (r[:, ic + 1] - r[:, ic])).mean())}
 # dispatch timeline: waves resident over time (16 bins)
 span = rows[:, 21].max() - t0
 edges = np.linspace(0, span, 33)

@@ -156,9 +156,9 @@ __shared__ uint16_t g_pair_lds[120];
 // every node kernel fills both tables at its start, before its block barrier
 __device__ __forceinline__ void node_tables_init() {
 #if GTF_RCP_TABLE
-    const int t = (int)threadIdx.x;
-    if (t < 65) g_rcp_lds[t] = t ? 1.0 / (double)t : 0.0;
-    if (t < 120) {
+    // (strided: blocks of fewer than 120 threads fill every entry too)
+    for (int t = (int)threadIdx.x; t < 120; t += (int)blockDim.x) {
+        if (t < 65) g_rcp_lds[t] = t ? 1.0 / (double)t : 0.0;
         int i, j;
         pair_ij(t, i, j);
         g_pair_lds[t] = (uint16_t)(i | (j << 8));
@@ -1282,6 +1282,23 @@ __device__ __forceinline__ void node_bucket(int q, int b, char* smem) {
 #else
 #define GTF_NODE_WAVES_ATTR
 #endif
+// Dispatch block b (on XCD b % 8, round-robin) -> the block of work it runs: runs of C
+// consecutive work blocks share an XCD, the runs of the 8 XCDs interleaved, so neighbouring
+// nodes' slot lines meet in one L2 while every XCD still draws from every part of the
+// launch (an XCD-contiguous remap of the whole launch, gtf::xcd_local, unbalanced the XCDs).
+// C = 1 is the identity; the last partial round of 8 C blocks stays in dispatch order.
+template <int C>
+__device__ __forceinline__ int node_block_map(int b, int n) {
+    if constexpr (C <= 1) {
+        return b;
+    } else {
+        const int full = n / (8 * C) * (8 * C);
+        if (b >= full) return b;
+        const int x = b % 8, r = b / 8;
+        return (r / C) * 8 * C + x * C + r % C;
+    }
+}
+
 template <int... OPS>
 __global__ void __launch_bounds__(NBLOCK) GTF_NODE_WAVES_ATTR k_node_multi(NodeKArgs args) {
     (void)args;   // read through node_kargs()
@@ -1294,7 +1311,10 @@ __global__ void __launch_bounds__(NBLOCK) GTF_NODE_WAVES_ATTR k_node_multi(NodeK
     const KArgPtr A = node_kargs();
     node_tables_init();
     __syncthreads();
-    int b = blockIdx.x;
+#ifndef GTF_NODE_XCD_CHUNK
+#define GTF_NODE_XCD_CHUNK 1   // > 1: runs of that many consecutive blocks on one XCD (node_block_map)
+#endif
+    int b = node_block_map<GTF_NODE_XCD_CHUNK>((int)blockIdx.x, (int)gridDim.x);
 #ifndef GTF_NODE_ORDER
 #define GTF_NODE_ORDER 0   // 1 (diagnostics): the buckets by measured wave life, longest first (16, 32, 8, 64, 4, 2)
 #endif

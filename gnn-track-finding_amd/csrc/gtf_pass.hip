@@ -327,7 +327,16 @@ __device__ __forceinline__ SendKArgPtr send_kargs() {
 #define GTF_SEND_NUM_SGPR 72
 #endif
 template <bool FUSED>
-__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(GTF_SEND_NUM_SGPR))) k_sender_sched(SendKArgs args) {
+#ifndef GTF_SEND_WAVES
+#define GTF_SEND_WAVES 0   // > 0: amdgpu_waves_per_eu lower bound of the (unfused) sender scan
+#endif
+#if GTF_SEND_WAVES > 0
+#define GTF_SEND_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(FUSED ? 1 : GTF_SEND_WAVES)))
+#else
+#define GTF_SEND_WAVES_ATTR
+#endif
+__global__ void __launch_bounds__(BLOCK) __attribute__((amdgpu_num_sgpr(GTF_SEND_NUM_SGPR))) GTF_SEND_WAVES_ATTR
+k_sender_sched(SendKArgs args) {
 #if GTF_SEND_KARGS
     (void)args;
     const SendKArgPtr A = send_kargs();

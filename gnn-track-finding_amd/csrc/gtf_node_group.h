@@ -1312,7 +1312,7 @@ __global__ void __launch_bounds__(NBLOCK) GTF_NODE_WAVES_ATTR k_node_multi(NodeK
     node_tables_init();
     __syncthreads();
 #ifndef GTF_NODE_XCD_CHUNK
-#define GTF_NODE_XCD_CHUNK 1   // > 1: runs of that many consecutive blocks on one XCD (node_block_map)
+#define GTF_NODE_XCD_CHUNK 4   // runs of this many consecutive blocks on one XCD (node_block_map; 1 = dispatch order)
 #endif
     int b = node_block_map<GTF_NODE_XCD_CHUNK>((int)blockIdx.x, (int)gridDim.x);
 #ifndef GTF_NODE_ORDER

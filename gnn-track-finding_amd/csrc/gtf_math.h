@@ -49,6 +49,22 @@ __device__ __forceinline__ int xcd_local(int b, int n) {
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
 }
 __host__ __device__ __forceinline__ int pad8(int n) { return (n + 7) & ~7; }
+// the same family by one parameter: C = 0 xcd_local (one contiguous range per XCD), C = 1
+// dispatch order, C > 1 runs of C consecutive blocks per XCD interleaved over the 8 XCDs
+// (the last partial round of 8 C blocks in dispatch order); a bijection of [0, n) each
+template <int C>
+__device__ __forceinline__ int block_map(int b, int n) {
+    if constexpr (C == 0) {
+        return xcd_local(b, n);
+    } else if constexpr (C == 1) {
+        return b;
+    } else {
+        const int full = n / (8 * C) * (8 * C);
+        if (b >= full) return b;
+        const int x = b % 8, r = b / 8;
+        return (r / C) * 8 * C + x * C + r % C;
+    }
+}
 
 // Lanes of ONE wavefront hand values to each other through LDS. A wave's LDS
 // instructions execute in issue order, so only the compiler has to be kept from

@@ -1286,17 +1286,10 @@ __device__ __forceinline__ void node_bucket(int q, int b, char* smem) {
 // consecutive work blocks share an XCD, the runs of the 8 XCDs interleaved, so neighbouring
 // nodes' slot lines meet in one L2 while every XCD still draws from every part of the
 // launch (an XCD-contiguous remap of the whole launch, gtf::xcd_local, unbalanced the XCDs).
-// C = 1 is the identity; the last partial round of 8 C blocks stays in dispatch order.
+// C = 1 is the identity (gtf::block_map).
 template <int C>
 __device__ __forceinline__ int node_block_map(int b, int n) {
-    if constexpr (C <= 1) {
-        return b;
-    } else {
-        const int full = n / (8 * C) * (8 * C);
-        if (b >= full) return b;
-        const int x = b % 8, r = b / 8;
-        return (r / C) * 8 * C + x * C + r % C;
-    }
+    return gtf::block_map<C < 1 ? 1 : C>(b, n);
 }
 
 template <int... OPS>

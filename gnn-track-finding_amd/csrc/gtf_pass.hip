@@ -125,6 +125,12 @@ __device__ __forceinline__ double highland_var_ms(double a, double b, const doub
 // the fused sender-major form (gtf_shard.phases bit 4, a shard's halo-dependent senders):
 // every scanned edge into the owned slots [lo, hi) is extrapolated by its lane right after
 // the scan, with the running value in a register instead of the workspace
+#ifndef GTF_EXTRAP_MAP
+#define GTF_EXTRAP_MAP 0   // gtf::block_map of k_extrapolate: 0 one slot range per XCD, 1 dispatch order, C > 1 runs of C
+#endif
+#ifndef GTF_SEND_MAP
+#define GTF_SEND_MAP 0     // the same for each bucket of k_sender_sched
+#endif
 #ifndef GTF_SEND_CHUNKS
 #define GTF_SEND_CHUNKS 2   // out-edge chunks per round of loads in the chunked sender scan (> 8 out-edges)
 #endif
@@ -280,7 +286,7 @@ template <int G, bool FUSED = false>
 __device__ __forceinline__ void sender_bucket(const gtf_graph& g, gtf_nodes& n, const gtf_edges& e,
                                               const gtf_params& p, const Ws& w, const int4* list, int count,
                                               int b, int nb, const Fuse* fu = nullptr) {
-    const int gi = (xcd_local(b, nb) * BLOCK + (int)threadIdx.x) / G;
+    const int gi = (gtf::block_map<GTF_SEND_MAP>(b, nb) * BLOCK + (int)threadIdx.x) / G;
     if (gi >= count) return;  // group-uniform
     const int4 en = list[gi];
     sender_scan<G, FUSED>(g, n, e, p, w, en.x, en.y, en.z, threadIdx.x & (G - 1), fu);
@@ -291,7 +297,7 @@ __device__ __forceinline__ void sender_bucket_lanes(const gtf_graph& g, gtf_node
                                                     const gtf_params& p, const Ws& w, const int4* list,
                                                     const int2* lanes, int count, int b, int nb,
                                                     const Fuse* fu = nullptr) {
-    const int t = xcd_local(b, nb) * BLOCK + (int)threadIdx.x;
+    const int t = gtf::block_map<GTF_SEND_MAP>(b, nb) * BLOCK + (int)threadIdx.x;
     const int gi = t / G;
     if (gi >= count) return;  // group-uniform
     const int4 en = list[gi];
@@ -568,7 +574,7 @@ __device__ __forceinline__ void extrap_slot(const gtf_graph& g, gtf_nodes& n, gt
 __global__ void __launch_bounds__(BLOCK) GTF_EXTRAP_ATTR k_extrapolate(gtf_graph g, gtf_nodes n, gtf_states uts,
                                                                        gtf_edges e, gtf_params p, Ws w, int slot_lo,
                                                                        int slot_hi, const int32_t* list) {
-    const int i = xcd_local(blockIdx.x, gridDim.x) * BLOCK + threadIdx.x;
+    const int i = gtf::block_map<GTF_EXTRAP_MAP>(blockIdx.x, gridDim.x) * BLOCK + threadIdx.x;
     if (slot_lo + i >= slot_hi) return;
     extrap_slot(g, n, uts, e, p, w, list ? list[i] : slot_lo + i, false, 0.0);
 }

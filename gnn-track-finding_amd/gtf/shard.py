@@ -307,7 +307,6 @@ class ShardedDeviceGraph:
         pl = self.plan
         self.senders = up(pl.senders(rank))
         if widen is None:
-            import os
             widen = int(os.environ.get("GTF_SHARD_WIDEN", "0"))
         sched, n_g, n_big, n_g2 = pl.schedule(rank, widen)
         self.sched = up(sched)

@@ -34,7 +34,7 @@ cd /tmp && export TMPDIR=/tmp
 timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python3 $R/bench.py > $OUT/bench_under_rocprof.json 2> $OUT/bench_under_rocprof.err || { tail -20 $OUT/bench_under_rocprof.err; exit 1; }
 cd $R
 python3 tools/kstats.py $OUT/prof final
-python3 tools/kstats_by_grid.py $OUT/prof $OUT/kernel_stats_by_grid.csv --match=k_sender,k_extrapolate,k_node,k_tag,k_count,k_parabolic | head -16
+python3 tools/kstats_by_grid.py $OUT/prof $OUT/kernel_stats_by_grid.csv --match=k_sender,k_extrapolate,k_node,k_tag,k_count,k_parabolic > $OUT/kstats_by_grid.txt; head -16 $OUT/kstats_by_grid.txt
 if [ -z "$NO_PMC" ]; then
   bash tools/gpu_profile.sh gpurun_out/$NAME/c4 --no-c5 --no-c3 --no-dropin --steps 20 --warmup 3 > /dev/null || { echo "c4 pmc failed"; exit 1; }
   python3 tools/pmc_summary.py gpurun_out/$NAME/c4 profiles/r01_pmc/calib gpurun_out/$NAME/c4/pmc_c4.json c4 | tail -8 || exit 1

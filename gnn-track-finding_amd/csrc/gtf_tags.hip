@@ -570,6 +570,17 @@ int gtf_tag_propagate(const gtf_graph* g, const double* radius, int64_t* tags, d
     int32_t* host = poll ? nullptr : tag_readback_buffer();   // the header words, then the ring
     if (!poll && !host) return hip_fail("gtf_tag_propagate: page-locked read-back buffer");
     bool stopped = false;
+    // the final tags into `tags` (k_tag_final: a copy when the executed count is odd), enqueued
+    // after every batch -- before the host has read whether the batch stopped the loop -- so the
+    // last one is already queued when it has: no launch on the stage's tail. An early copy is
+    // harmless: the next batch's first sweep rewrites every tag of `tags` or reads it as copied.
+    auto final_copy = [&]() -> int {
+        if (g->n_nodes <= 0) return 0;
+        hipLaunchKernelGGL(k_tag_final, dim3((g->n_nodes + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, st, tags, other,
+                           hdr + 2, g->n_nodes);
+        return hipGetLastError() == hipSuccess ? 0 : hip_fail("gtf_tag_propagate: final copy");
+    };
+    bool copied = false;
     while (!stopped && s < max_sweeps) {
         const int32_t at = s % TAG_RING;
         int32_t nb = batch < max_sweeps - s ? batch : max_sweeps - s;
@@ -593,11 +604,15 @@ int gtf_tag_propagate(const gtf_graph* g, const double* radius, int64_t* tags, d
             hipLaunchKernelGGL(k_tag_report, dim3(1), dim3(64), 0, st, hdr, ring, s, nb, TAG_RING, tag_report_dev(),
                                seq);
             if (hipGetLastError() != hipSuccess) return hip_fail("gtf_tag_propagate: report launch");
+            if (int rc = final_copy()) return rc;
+            copied = true;
             if (int rc = tag_wait_report(hostrep, seq, st)) return rc;
             for (int k = 0; k < 3; k++) words[k] = hostrep[1 + k];
             fl = hostrep + 4;
         } else {
             // one read-back: the header words through the batch's last counter
+            if (int rc = final_copy()) return rc;
+            copied = true;
             if (hipMemcpyAsync(host, hdr, (64 + (at + nb) * TAG_CTR) * sizeof(int32_t), hipMemcpyDeviceToHost, st) !=
                     hipSuccess ||
                 hipStreamSynchronize(st) != hipSuccess)
@@ -625,11 +640,7 @@ int gtf_tag_propagate(const gtf_graph* g, const double* radius, int64_t* tags, d
         if (batch < TAG_MAX_BATCH) batch *= 2;
     }
     *sweeps_out = executed;
-    if (g->n_nodes > 0) {
-        hipLaunchKernelGGL(k_tag_final, dim3((g->n_nodes + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, st, tags, other,
-                           hdr + 2, g->n_nodes);
-        if (hipGetLastError() != hipSuccess) return hip_fail("gtf_tag_propagate: final copy");
-    }
+    if (!copied) return final_copy();   // (no sweep at all)
     return 0;
 }
 

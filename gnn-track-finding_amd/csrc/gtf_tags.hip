@@ -39,6 +39,25 @@ __device__ __forceinline__ void block_count_add(int mine, T* ctr, int nsh) {
     }
 }
 
+// two counts of one block in one reduction: `a` lanes added to ctr_a (shard blockIdx % nsh_a)
+// and, when ctr_b is not NULL (block-uniform), `b` lanes to ctr_b (shard blockIdx % TAG_SHARDS)
+__device__ __forceinline__ void block_count_add2(int a, int32_t* ctr_a, int nsh_a, int b, int32_t* ctr_b) {
+    __shared__ int s_cnt2[2][BLOCK / 64];
+    const unsigned long long ba = __ballot(a), bb = __ballot(b);
+    if ((threadIdx.x & 63) == 0) {
+        s_cnt2[0][threadIdx.x >> 6] = (int)__popcll(ba);
+        s_cnt2[1][threadIdx.x >> 6] = (int)__popcll(bb);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int ta = 0, tb = 0;
+#pragma unroll
+        for (int w = 0; w < BLOCK / 64; w++) { ta += s_cnt2[0][w]; tb += s_cnt2[1][w]; }
+        if (ta) atomicAdd(ctr_a + (nsh_a > 1 ? (int)(blockIdx.x % nsh_a) * TAG_STRIDE : 0), ta);
+        if (ctr_b && tb) atomicAdd(ctr_b + (int)(blockIdx.x % TAG_SHARDS) * TAG_STRIDE, tb);
+    }
+}
+
 // the total of a sharded counter (wave-uniform: every lane gets it)
 __device__ __forceinline__ int32_t shard_total(const int32_t* ctr, int nsh) {
     const int lane = threadIdx.x & 63;
@@ -166,19 +185,20 @@ __global__ void __launch_bounds__(BLOCK) k_tag_prepare_sched(gtf_graph g, const 
 // sweeps is enqueued without a host read between them and the sweeps past the stop return
 // at once. Every block takes the same decision from the finished previous sweep's count.
 struct TagCtl {
-    const int32_t* total;   // processed count (gtf_tag_prepare)
+    const int32_t* total;   // processed count, TAG_SHARDS shards (counted by the first sweep)
     const int32_t* prev;    // flips of the previous sweep (TAG_SHARDS shards), NULL for the first
     int32_t* stop;          // set once the rule stops the loop
     int32_t* nexec;         // sweeps executed
     double thr;
     int32_t* next;          // the next sweep's counter shards, zeroed by block 0 (NULL: the caller zeroes)
+    int32_t* count_processed;   // (the first sweep) where its blocks add the processed nodes, else NULL
 };
 
 __device__ __forceinline__ bool tag_skip(const TagCtl& c) {
     if (!c.stop) return false;
     if (*c.stop) return true;
     if (c.prev) {
-        const int32_t tot = *c.total, f = shard_total(c.prev, TAG_SHARDS);
+        const int32_t tot = shard_total(c.total, TAG_SHARDS), f = shard_total(c.prev, TAG_SHARDS);
         const double frac = tot ? (double)f / (double)tot : 0.0;
         if (!(frac > c.thr)) {
             if (blockIdx.x == 0 && threadIdx.x == 0) atomicExch(c.stop, 1);
@@ -193,16 +213,18 @@ __device__ __forceinline__ bool tag_skip(const TagCtl& c) {
 // the batch's stop-rule words and per-sweep flip totals into the caller's page-locked report
 // (mapped, coherent): rep[1..3] = processed, stop, executed; rep[4 + i] = flips of sweep s + i;
 // rep[0] = seq last, after a system-scope fence, so the host that sees seq sees the rest
-__global__ void __launch_bounds__(64) k_tag_report(const int32_t* hdr, const int32_t* ring, int s, int nb, int ring_n,
-                                                   int32_t* rep, int32_t seq) {
+__global__ void __launch_bounds__(64) k_tag_report(const int32_t* hdr, const int32_t* pshards, const int32_t* ring,
+                                                   int s, int nb, int ring_n, int32_t* rep, int32_t seq) {
     const int t = (int)threadIdx.x;
+    const int32_t processed = shard_total(pshards, TAG_SHARDS);
     if (t < nb) {
         const int32_t* c = ring + (size_t)((s + t) % ring_n) * TAG_SHARDS * TAG_STRIDE;
         int f = 0;
         for (int k = 0; k < TAG_SHARDS; k++) f += c[k * TAG_STRIDE];
         rep[4 + t] = f;
     }
-    if (t < 3) rep[1 + t] = hdr[t];
+    if (t == 0) rep[1] = processed;
+    if (t == 1 || t == 2) rep[1 + t] = hdr[t];
     __threadfence_system();
     __syncthreads();
     if (t == 0) __hip_atomic_store(rep, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -221,11 +243,12 @@ __global__ void __launch_bounds__(BLOCK) k_tag_sweep(gtf_graph g, const uint8_t*
                                                      TagCtl ctl) {
     if (tag_skip(ctl)) return;
     const int u = gtf::xcd_local(blockIdx.x, gridDim.x) * BLOCK + threadIdx.x;
-    int flipped = 0;
+    int flipped = 0, pr = 0;
     if (u < g.n_nodes) {
         const int64_t t0 = tin[u];
         int64_t t = t0;
-        if (processed[u]) {
+        pr = processed[u] != 0;
+        if (pr) {
             for (int i = g.out_ptr[u]; i < g.out_ptr[u + 1]; i++)
                 if (keep[i]) {
                     const int64_t tw = tin[g.out_dst ? g.out_dst[i] : g.slot_dst[g.out_slot[i]]];
@@ -235,7 +258,7 @@ __global__ void __launch_bounds__(BLOCK) k_tag_sweep(gtf_graph g, const uint8_t*
         }
         tout[u] = t;
     }
-    block_count_add(flipped, flips, nsh);
+    block_count_add2(flipped, flips, nsh, pr, ctl.count_processed);
 }
 // With the sender schedule (gtf_graph.out_sched + out_lanes): G lanes per node over its
 // out-edges, every lane's loads in one round (its keep flag, its neighbour's tag, the
@@ -265,7 +288,7 @@ __device__ __forceinline__ int tag_group_lanes(const gtf_graph& g, const uint8_t
     }
     if (!pr) m = t0;
     if (gl == 0) tout[u] = m;
-    return gl == 0 && m != t0;
+    return (gl == 0 && m != t0) | ((gl == 0 && pr) ? 2 : 0);   // bit 0 flipped, bit 1 processed
 }
 
 template <int G>
@@ -287,9 +310,10 @@ __device__ __forceinline__ int tag_group(const gtf_graph& g, const uint8_t* keep
         const int64_t x = __shfl_xor(m, o, G);
         m = x > m ? x : m;
     }
-    if (!processed[u]) m = t0;
+    const bool pr = processed[u] != 0;
+    if (!pr) m = t0;
     if (gl == 0) tout[u] = m;
-    return gl == 0 && m != t0;
+    return (gl == 0 && m != t0) | ((gl == 0 && pr) ? 2 : 0);   // bit 0 flipped, bit 1 processed
 }
 
 struct TagBuckets {
@@ -304,7 +328,7 @@ __global__ void __launch_bounds__(BLOCK) k_tag_sweep_sched(gtf_graph g, const ui
                                                            const int64_t* tin, int64_t* tout, int32_t* flips,
                                                            int nsh, TagBuckets tb, TagCtl ctl) {
     if (tag_skip(ctl)) return;
-    int b = blockIdx.x, flipped = 0;
+    int b = blockIdx.x, flipped = 0;   // (bit 0 flipped, bit 1 processed: tag_group*)
     if (b < tb.blocks[0]) {
         flipped = tb.lanes[0] ? tag_group_lanes<4>(g, keep, processed, tin, tout, tb.list[0], tb.lanes[0], tb.count[0], b)
                               : tag_group<4>(g, keep, processed, tin, tout, tb.list[0], tb.count[0], b);
@@ -318,7 +342,7 @@ __global__ void __launch_bounds__(BLOCK) k_tag_sweep_sched(gtf_graph g, const ui
         if (u < g.n_nodes && g.out_ptr[u + 1] == g.out_ptr[u]) tout[u] = tin[u];
         return;   // (block-uniform: these blocks count no flips)
     }
-    block_count_add(flipped, flips, nsh);
+    block_count_add2(flipped & 1, flips, nsh, (flipped >> 1) & 1, ctl.count_processed);
 }
 
 // One rank's sweep of the sharded tag propagation: the owned nodes
@@ -366,6 +390,7 @@ static int hip_fail(const char* what) {
 static int tag_prepare(const gtf_graph* g, const double* radius, uint8_t* keep, uint8_t* processed,
                        int32_t* n_processed, bool zero_count, hipStream_t st, int32_t* zero = nullptr,
                        int nzero = 0) {
+    // n_processed NULL: no count here (gtf_tag_propagate's first sweep counts the processed nodes)
     if (zero_count && hipMemsetAsync(n_processed, 0, sizeof(int32_t), st) != hipSuccess)
         return hip_fail("gtf_tag_prepare");
     if (g->n_nodes <= 0 && zero && hipMemsetAsync(zero, 0, nzero * sizeof(int32_t), st) != hipSuccess)
@@ -392,7 +417,7 @@ static int tag_prepare(const gtf_graph* g, const double* radius, uint8_t* keep, 
         hipLaunchKernelGGL(k_tag_prepare, dim3((g->n_nodes + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, st, *g, radius,
                            keep, processed, zero, nzero);
     }
-    if (g->n_nodes > 0) {   // the processed count: a reduction of the processed bytes
+    if (g->n_nodes > 0 && n_processed) {   // the processed count: a reduction of the processed bytes
         int blocks = (g->n_nodes / 16 + BLOCK * 4 - 1) / (BLOCK * 4);   // ~4 steps per thread
         blocks = blocks < 1 ? 1 : (blocks > 128 ? 128 : blocks);
         hipLaunchKernelGGL(k_count_flags, dim3(blocks), dim3(BLOCK), 0, st, processed, g->n_nodes, n_processed);
@@ -441,7 +466,7 @@ static int tag_sweep(const gtf_graph* g, const uint8_t* keep, const uint8_t* pro
 int gtf_tag_sweep(const gtf_graph* g, const uint8_t* keep, const uint8_t* processed, const int64_t* tags_in,
                   int64_t* tags_out, int32_t* flips, gtf_stream_t stream) {
     if (int rc = gtf::check_abi(g, "gtf_tag_sweep")) return rc;
-    const TagCtl none{nullptr, nullptr, nullptr, nullptr, 0.0, nullptr};
+    const TagCtl none{nullptr, nullptr, nullptr, nullptr, 0.0, nullptr, nullptr};
     return tag_sweep(g, keep, processed, tags_in, tags_out, flips, 1, none, (hipStream_t)stream);
 }
 
@@ -451,7 +476,8 @@ static size_t tag_align(size_t x) { return (x + 255) & ~size_t(255); }
 // a ring of per-sweep flip counters, TAG_SHARDS words each (TAG_STRIDE apart)
 constexpr int TAG_RING = 128;
 constexpr size_t TAG_CTR = (size_t)TAG_SHARDS * TAG_STRIDE;   // int32 words per sweep
-constexpr size_t TAG_HDR = 64 * sizeof(int32_t) + TAG_RING * TAG_CTR * sizeof(int32_t);
+// the stop-rule words, the processed count's shards, then the ring of flip counters
+constexpr size_t TAG_HDR = 64 * sizeof(int32_t) + TAG_CTR * sizeof(int32_t) + TAG_RING * TAG_CTR * sizeof(int32_t);
 
 size_t gtf_tag_workspace_bytes(int32_t n_nodes, int32_t n_edges) {
     const size_t n = n_nodes > 0 ? (size_t)n_nodes : 1, e = n_edges > 0 ? (size_t)n_edges : 1;
@@ -524,7 +550,7 @@ static int tag_wait_report(int32_t* rep, int32_t seq, hipStream_t st) {
 
 static int32_t* tag_readback_buffer() {
     static thread_local int32_t* buf = nullptr;
-    if (!buf && hipHostMalloc((void**)&buf, (64 + TAG_RING * TAG_CTR) * sizeof(int32_t), hipHostMallocPortable) !=
+    if (!buf && hipHostMalloc((void**)&buf, (64 + (1 + TAG_RING) * TAG_CTR) * sizeof(int32_t), hipHostMallocPortable) !=
                     hipSuccess)
         buf = nullptr;
     return buf;
@@ -552,8 +578,9 @@ int gtf_tag_propagate(const gtf_graph* g, const double* radius, int64_t* tags, d
     hipStream_t st = (hipStream_t)stream;
     const size_t n = g->n_nodes > 0 ? (size_t)g->n_nodes : 1, e = n_edges > 0 ? (size_t)n_edges : 1;
     char* w = static_cast<char*>(workspace);
-    int32_t* hdr = reinterpret_cast<int32_t*>(w);   // [0] processed [1] stop [2] executed; the ring from word 64
-    int32_t* ring = hdr + 64;
+    int32_t* hdr = reinterpret_cast<int32_t*>(w);   // [1] stop [2] executed
+    int32_t* pshards = hdr + 64;                    // the processed count, TAG_SHARDS shards
+    int32_t* ring = pshards + TAG_CTR;
     w += tag_align(TAG_HDR);
     uint8_t* keep = reinterpret_cast<uint8_t*>(w);
     w += tag_align(e);
@@ -565,7 +592,7 @@ int gtf_tag_propagate(const gtf_graph* g, const double* radius, int64_t* tags, d
     // executed sweep zeroes the next one's (TagCtl.next)
     int32_t* hostrep = tag_report_buffer();   // mapped page-locked report (NULL: read back by copy)
     const bool poll = hostrep && tag_poll_enabled();
-    if (int rc = tag_prepare(g, radius, keep, proc, hdr, false, st, hdr, 64 + (int)TAG_CTR)) return rc;
+    if (int rc = tag_prepare(g, radius, keep, proc, nullptr, false, st, hdr, 64 + 2 * (int)TAG_CTR)) return rc;
     int32_t s = 0, batch = 2, executed = 0;
     int32_t* host = poll ? nullptr : tag_readback_buffer();   // the header words, then the ring
     if (!poll && !host) return hip_fail("gtf_tag_propagate: page-locked read-back buffer");
@@ -587,8 +614,8 @@ int gtf_tag_propagate(const gtf_graph* g, const double* radius, int64_t* tags, d
         if (nb > TAG_RING - at) nb = TAG_RING - at;   // the batch's counters stay contiguous in the ring
         for (int32_t i = 0; i < nb; i++) {
             const int32_t q = s + i;
-            const TagCtl ctl{hdr, q > 0 ? ring + ((q - 1) % TAG_RING) * TAG_CTR : nullptr, hdr + 1, hdr + 2,
-                             flip_threshold, ring + ((q + 1) % TAG_RING) * TAG_CTR};
+            const TagCtl ctl{pshards, q > 0 ? ring + ((q - 1) % TAG_RING) * TAG_CTR : nullptr, hdr + 1, hdr + 2,
+                             flip_threshold, ring + ((q + 1) % TAG_RING) * TAG_CTR, q == 0 ? pshards : nullptr};
             int64_t* tin = (q & 1) ? other : tags;
             int64_t* tout = (q & 1) ? tags : other;
             if (int rc = tag_sweep(g, keep, proc, tin, tout, ring + (q % TAG_RING) * TAG_CTR, TAG_SHARDS, ctl, st))
@@ -601,8 +628,8 @@ int gtf_tag_propagate(const gtf_graph* g, const double* radius, int64_t* tags, d
             // one small launch writes the words and the batch's flip totals into the mapped report;
             // the host waits for its sequence word instead of a copy and a stream synchronisation
             const int32_t seq = tag_next_seq();
-            hipLaunchKernelGGL(k_tag_report, dim3(1), dim3(64), 0, st, hdr, ring, s, nb, TAG_RING, tag_report_dev(),
-                               seq);
+            hipLaunchKernelGGL(k_tag_report, dim3(1), dim3(64), 0, st, hdr, pshards, ring, s, nb, TAG_RING,
+                               tag_report_dev(), seq);
             if (hipGetLastError() != hipSuccess) return hip_fail("gtf_tag_propagate: report launch");
             if (int rc = final_copy()) return rc;
             copied = true;
@@ -613,14 +640,16 @@ int gtf_tag_propagate(const gtf_graph* g, const double* radius, int64_t* tags, d
             // one read-back: the header words through the batch's last counter
             if (int rc = final_copy()) return rc;
             copied = true;
-            if (hipMemcpyAsync(host, hdr, (64 + (at + nb) * TAG_CTR) * sizeof(int32_t), hipMemcpyDeviceToHost, st) !=
+            if (hipMemcpyAsync(host, hdr, (64 + (1 + at + nb) * TAG_CTR) * sizeof(int32_t), hipMemcpyDeviceToHost, st) !=
                     hipSuccess ||
                 hipStreamSynchronize(st) != hipSuccess)
                 return hip_fail("gtf_tag_propagate: reading the flip counts");
-            for (int k = 0; k < 3; k++) words[k] = host[k];
+            words[0] = 0;
+            for (int k = 0; k < TAG_SHARDS; k++) words[0] += host[64 + k * TAG_STRIDE];
+            for (int k = 1; k < 3; k++) words[k] = host[k];
             tot.resize(nb);
             for (int32_t i = 0; i < nb; i++) {
-                const int32_t* c = host + 64 + (at + i) * TAG_CTR;
+                const int32_t* c = host + 64 + (1 + at + i) * TAG_CTR;
                 int32_t f = 0;
                 for (int k = 0; k < TAG_SHARDS; k++) f += c[k * TAG_STRIDE];
                 tot[i] = f;

@@ -141,8 +141,18 @@ struct Fuse {
     gtf_states uts;
     int32_t lo, hi;
 };
+// what the fused sender-major scan already holds of an out-edge when it extrapolates it: the
+// sender's state and coordinates, the receiver's coordinates, the activation and var_ms
+struct ExKnown {
+    int u, v;
+    uint8_t act;
+    double a, b, c, mc00, mc01, mc10, mc22, vm;
+    double ng[4], nb[4];
+};
+template <bool KNOWN = false>
 __device__ __forceinline__ void extrap_slot(const gtf_graph& g, gtf_nodes& n, gtf_states& uts, gtf_edges& e,
-                                            const gtf_params& p, const Ws& w, int k, bool have_vc, double vc_given);
+                                            const gtf_params& p, const Ws& w, int k, bool have_vc, double vc_given,
+                                            const ExKnown* kn = nullptr);
 
 // one sender u over its out-list [ob, oe) with SG lanes (lane gl), chunks of SG
 template <int SG, bool FUSED = false>
@@ -158,6 +168,14 @@ __device__ __forceinline__ void sender_scan(const gtf_graph& g, gtf_nodes& n, co
     const double* ng = ngl;
     double carry = n.merged_cov[5 * (int64_t)u + 3];
     const double carry0 = carry;
+    // (the fused form) the rest of the sender's state, in the same round: the extrapolation
+    // reads it from here instead of gathering it again per out-edge
+    double c3 = 0.0, m00 = 0.0, m01 = 0.0, m10 = 0.0, m22 = 0.0;
+    if constexpr (FUSED) {
+        c3 = n.merged_state[3 * (int64_t)u + 2];
+        m00 = n.merged_cov[5 * (int64_t)u + 0]; m01 = n.merged_cov[5 * (int64_t)u + 1];
+        m10 = n.merged_cov[5 * (int64_t)u + 2]; m22 = n.merged_cov[5 * (int64_t)u + 4];
+    }
     if constexpr (FUSED) {
         if (!hm) {   // no state to extrapolate: the owned slots still end their message passing
             for (int i = ob + gl; i < oe; i += SG) {
@@ -184,9 +202,11 @@ __device__ __forceinline__ void sender_scan(const gtf_graph& g, gtf_nodes& n, co
         }
         double nbv[NC][4];
         uint8_t ac[NC];
+        int vr[NC];   // the receivers (the fused form's extrapolation)
 #pragma unroll
         for (int j = 0; j < NC; j++) {
             const int v = g.out_dst ? vv[j] : g.slot_dst[kk[j]];
+            vr[j] = v;
 #pragma unroll
             for (int q = 0; q < 4; q++) nbv[j][q] = g.gnn[4 * (int64_t)v + q];
             ac[j] = e.act[kk[j]];
@@ -206,8 +226,11 @@ __device__ __forceinline__ void sender_scan(const gtf_graph& g, gtf_nodes& n, co
             // the running value of each active edge, stored in out-edge order (contiguous per
             // sender: coalesced stores) when the graph has slot_outidx, else at its slot
             if constexpr (FUSED) {
-                if (k >= fu->lo && k < fu->hi)
-                    extrap_slot(g, n, *(gtf_states*)&fu->uts, *(gtf_edges*)&e, p, w, k, true, c);
+                if (k >= fu->lo && k < fu->hi) {
+                    const ExKnown kn{u, vr[j], ac[j], a, b, c3, m00, m01, m10, m22, vm,
+                                     {ng[0], ng[1], ng[2], ng[3]}, {nbv[j][0], nbv[j][1], nbv[j][2], nbv[j][3]}};
+                    extrap_slot<true>(g, n, *(gtf_states*)&fu->uts, *(gtf_edges*)&e, p, w, k, true, c, &kn);
+                }
             } else {
                 if (vm != -1.0) w.vc[g.slot_outidx ? i : k] = c;
             }
@@ -233,6 +256,12 @@ __device__ __forceinline__ void sender_scan_lane(const gtf_graph& g, gtf_nodes& 
     const double ng[4] = {g.gnn[4 * (int64_t)u], g.gnn[4 * (int64_t)u + 1], g.gnn[4 * (int64_t)u + 2],
                           g.gnn[4 * (int64_t)u + 3]};
     const double carry = n.merged_cov[5 * (int64_t)u + 3];
+    double c3 = 0.0, m00 = 0.0, m01 = 0.0, m10 = 0.0, m22 = 0.0;   // (the fused form, as in sender_scan)
+    if constexpr (FUSED) {
+        c3 = n.merged_state[3 * (int64_t)u + 2];
+        m00 = n.merged_cov[5 * (int64_t)u + 0]; m01 = n.merged_cov[5 * (int64_t)u + 1];
+        m10 = n.merged_cov[5 * (int64_t)u + 2]; m22 = n.merged_cov[5 * (int64_t)u + 4];
+    }
     const int kk = k >= 0 ? k : 0;
     const double nb[4] = {g.gnn[4 * (int64_t)v], g.gnn[4 * (int64_t)v + 1], g.gnn[4 * (int64_t)v + 2],
                           g.gnn[4 * (int64_t)v + 3]};
@@ -257,7 +286,11 @@ __device__ __forceinline__ void sender_scan_lane(const gtf_graph& g, gtf_nodes& 
     if (gl == 0 && (!GTF_SEND_KEEP_CARRY || __double_as_longlong(fin) != __double_as_longlong(carry)))
         n.merged_cov[5 * (int64_t)u + 3] = fin;
     if constexpr (FUSED) {
-        if (k >= fu->lo && k < fu->hi) extrap_slot(g, n, *(gtf_states*)&fu->uts, *(gtf_edges*)&e, p, w, k, true, c);
+        if (k >= fu->lo && k < fu->hi) {
+            const ExKnown kn{u, v, act, a, b, c3, m00, m01, m10, m22, vm, {ng[0], ng[1], ng[2], ng[3]},
+                             {nb[0], nb[1], nb[2], nb[3]}};
+            extrap_slot<true>(g, n, *(gtf_states*)&fu->uts, *(gtf_edges*)&e, p, w, k, true, c, &kn);
+        }
     }
 }
 
@@ -396,55 +429,15 @@ k_sender_sched(SendKArgs args) {
 // the extrapolation of slot k (edge u -> v), k_extrapolate's per-slot body; have_vc: the
 // running merged_cov[1,1] of the edge comes from the caller (the fused sender-major form)
 // instead of the workspace
-__device__ __forceinline__ void extrap_slot(const gtf_graph& g, gtf_nodes& n, gtf_states& uts, gtf_edges& e,
-                                            const gtf_params& p, const Ws& w, int k, bool have_vc, double vc_given) {
-    // Two levels of loads instead of a chain: everything indexed by the slot, then
-    // everything indexed by its sender / receiver, issued before any early exit (the
-    // exits would otherwise serialise each load behind the previous one's branch).
-    const uint8_t is_edge = g.is_edge[k], act = e.act[k];
-    const uint8_t f_old = uts.fresh[k];   // bit 1 (live coordinates) survives a rejected extrapolation
-    const int src = g.slot_src[k], v = g.slot_dst[k];
-    // written by k_sender for active edges of merged senders: in out-edge order through
-    // slot_outidx (one gather beside the sender's), or by slot
-    const int oi = (have_vc || !g.slot_outidx) ? k : g.slot_outidx[k];
-    const double smw = e.send_mw[k];
-#if GTF_EXTRAP_PRED
-    // the sender / receiver gathers only for the slots that can extrapolate (an active edge
-    // with a sender): the same second level of loads, without the ~170 bytes per slot the
-    // keys without an edge and the deactivated edges would fetch for nothing
-    const bool go = is_edge && src >= 0 && act == 1;
-    double vc = 0.0, node_x = 0.0, node_y = 0.0, node_z = 0.0, node_r = 0.0, nbx = 0.0, nby = 0.0, nbz = 0.0,
-           nbr = 0.0, a = 0.0, b = 0.0, c = 0.0, mc00 = 0.0, mc01 = 0.0, mc10 = 0.0, mc22 = 0.0;
-    uint8_t hm = 0;
-    if (go) {
-        vc = have_vc ? vc_given : w.vc[oi >= 0 ? oi : 0];
-        const double* ng = g.gnn + 4 * (int64_t)src;  // sender ("node" in the reference)
-        const double* nb = g.gnn + 4 * (int64_t)v;    // receiver ("neighbour")
-        hm = n.has_merged[src];
-        node_x = ng[0]; node_y = ng[1]; node_z = ng[2]; node_r = ng[3];
-        nbx = nb[0]; nby = nb[1]; nbz = nb[2]; nbr = nb[3];
-        a = n.merged_state[3 * src + 0]; b = n.merged_state[3 * src + 1]; c = n.merged_state[3 * src + 2];
-        const double* mcp = n.merged_cov + 5 * (int64_t)src;
-        mc00 = mcp[0]; mc01 = mcp[1]; mc10 = mcp[2]; mc22 = mcp[4];
-    }
-    if (!go || !hm) {
-#else
-    const double vc = have_vc ? vc_given : w.vc[oi >= 0 ? oi : 0];
-    const int u = src >= 0 ? src : 0;   // orphan keys have no sender
-    const double* ng = g.gnn + 4 * (int64_t)u;  // sender ("node" in the reference)
-    const double* nb = g.gnn + 4 * (int64_t)v;  // receiver ("neighbour")
-    const uint8_t hm = n.has_merged[u];
-    const double node_x = ng[0], node_y = ng[1], node_z = ng[2], node_r = ng[3];
-    const double nbx = nb[0], nby = nb[1], nbz = nb[2], nbr = nb[3];
-    const double a = n.merged_state[3 * u + 0], b = n.merged_state[3 * u + 1], c = n.merged_state[3 * u + 2];
-    const double* mcp = n.merged_cov + 5 * (int64_t)u;
-    const double mc00 = mcp[0], mc01 = mcp[1], mc10 = mcp[2], mc22 = mcp[4];
-    if (!is_edge || src < 0 || !hm || act != 1) {
-#endif
-        if (f_old & 1) uts.fresh[k] = f_old & 2;
-        return;
-    }
-
+// extrapolate_validate's arithmetic and the slot's stores (extrapolate_merged_states.py:41-402)
+// for an active edge of a merged sender, from its loaded operands
+template <bool KNOWN>
+__device__ __forceinline__ void extrap_math(const gtf_graph& g, gtf_states& uts, gtf_edges& e, const gtf_params& p,
+                                            const Ws& w, int k, int v, uint8_t f_old, double smw, double vc,
+                                            double node_x, double node_y, double node_z, double node_r, double nbx,
+                                            double nby, double nbz, double nbr, double a, double b, double c,
+                                            double mc00, double mc01, double mc10, double mc22, double vm_known) {
+    (void)g;
     // cos/sin of atan2(y, x) as x/h, y/h (h = |(x, y)|): the same angles as the
     // reference's atan2 -> cos/sin round trips, to a couple of ulps, without fp64 libm
     // (divisors used more than once: one correctly rounded reciprocal, then xdiv() -- the
@@ -489,8 +482,11 @@ __device__ __forceinline__ void extrap_slot(const gtf_graph& g, gtf_nodes& n, gt
 
     // var_ms again from the operands k_sender used (the same bits): 8 bytes per slot
     // cross the two kernels instead of 16
-    const double ngv[4] = {node_x, node_y, node_z, node_r}, nbv[4] = {nbx, nby, nbz, nbr};
-    const double var_ms = highland_var_ms(a, b, ngv, nbv, p.endcap_boundary);
+    double var_ms = vm_known;   // (the fused scan: the value it computed from the same operands)
+    if constexpr (!KNOWN) {
+        const double ngv[4] = {node_x, node_y, node_z, node_r}, nbv[4] = {nbx, nby, nbz, nbr};
+        var_ms = highland_var_ms(a, b, ngv, nbv, p.endcap_boundary);
+    }
     const Mat3 C = {{{mc00, mc01, 0.0}, {mc10, vc, 0.0}, {0.0, 0.0, mc22}}};  // :128
     const double m[3] = {a, b, c};
     double xe[3];
@@ -568,6 +564,75 @@ __device__ __forceinline__ void extrap_slot(const gtf_graph& g, gtf_nodes& n, gt
     // marks it live instead of writing a 32-byte copy per accepted edge (gtf_uts_materialize
     // writes it when it is read back or before g.gnn changes)
     uts.fresh[k] = 3;   // the receiver's has_uts flag follows in the node kernel (OP_FRESH)
+}
+
+template <bool KNOWN>
+__device__ __forceinline__ void extrap_slot(const gtf_graph& g, gtf_nodes& n, gtf_states& uts, gtf_edges& e,
+                                            const gtf_params& p, const Ws& w, int k, bool have_vc, double vc_given,
+                                            const ExKnown* kn) {
+    if constexpr (KNOWN) {
+        // (the fused scan) only the slot's own fields are loaded; everything else is the scan's
+        const uint8_t is_edge = g.is_edge[k];
+        const uint8_t f_old = uts.fresh[k];
+        const double smw = e.send_mw[k];
+        if (!is_edge || kn->act != 1) {
+            if (f_old & 1) uts.fresh[k] = f_old & 2;
+            return;
+        }
+        extrap_math<true>(g, uts, e, p, w, k, kn->v, f_old, smw, vc_given, kn->ng[0], kn->ng[1], kn->ng[2], kn->ng[3],
+                          kn->nb[0], kn->nb[1], kn->nb[2], kn->nb[3], kn->a, kn->b, kn->c, kn->mc00, kn->mc01,
+                          kn->mc10, kn->mc22, kn->vm);
+        return;
+    }
+    // Two levels of loads instead of a chain: everything indexed by the slot, then
+    // everything indexed by its sender / receiver, issued before any early exit (the
+    // exits would otherwise serialise each load behind the previous one's branch).
+    const uint8_t is_edge = g.is_edge[k], act = e.act[k];
+    const uint8_t f_old = uts.fresh[k];   // bit 1 (live coordinates) survives a rejected extrapolation
+    const int src = g.slot_src[k], v = g.slot_dst[k];
+    // written by k_sender for active edges of merged senders: in out-edge order through
+    // slot_outidx (one gather beside the sender's), or by slot
+    const int oi = (have_vc || !g.slot_outidx) ? k : g.slot_outidx[k];
+    const double smw = e.send_mw[k];
+#if GTF_EXTRAP_PRED
+    // the sender / receiver gathers only for the slots that can extrapolate (an active edge
+    // with a sender): the same second level of loads, without the ~170 bytes per slot the
+    // keys without an edge and the deactivated edges would fetch for nothing
+    const bool go = is_edge && src >= 0 && act == 1;
+    double vc = 0.0, node_x = 0.0, node_y = 0.0, node_z = 0.0, node_r = 0.0, nbx = 0.0, nby = 0.0, nbz = 0.0,
+           nbr = 0.0, a = 0.0, b = 0.0, c = 0.0, mc00 = 0.0, mc01 = 0.0, mc10 = 0.0, mc22 = 0.0;
+    uint8_t hm = 0;
+    if (go) {
+        vc = have_vc ? vc_given : w.vc[oi >= 0 ? oi : 0];
+        const double* ng = g.gnn + 4 * (int64_t)src;  // sender ("node" in the reference)
+        const double* nb = g.gnn + 4 * (int64_t)v;    // receiver ("neighbour")
+        hm = n.has_merged[src];
+        node_x = ng[0]; node_y = ng[1]; node_z = ng[2]; node_r = ng[3];
+        nbx = nb[0]; nby = nb[1]; nbz = nb[2]; nbr = nb[3];
+        a = n.merged_state[3 * src + 0]; b = n.merged_state[3 * src + 1]; c = n.merged_state[3 * src + 2];
+        const double* mcp = n.merged_cov + 5 * (int64_t)src;
+        mc00 = mcp[0]; mc01 = mcp[1]; mc10 = mcp[2]; mc22 = mcp[4];
+    }
+    if (!go || !hm) {
+#else
+    const double vc = have_vc ? vc_given : w.vc[oi >= 0 ? oi : 0];
+    const int u = src >= 0 ? src : 0;   // orphan keys have no sender
+    const double* ng = g.gnn + 4 * (int64_t)u;  // sender ("node" in the reference)
+    const double* nb = g.gnn + 4 * (int64_t)v;  // receiver ("neighbour")
+    const uint8_t hm = n.has_merged[u];
+    const double node_x = ng[0], node_y = ng[1], node_z = ng[2], node_r = ng[3];
+    const double nbx = nb[0], nby = nb[1], nbz = nb[2], nbr = nb[3];
+    const double a = n.merged_state[3 * u + 0], b = n.merged_state[3 * u + 1], c = n.merged_state[3 * u + 2];
+    const double* mcp = n.merged_cov + 5 * (int64_t)u;
+    const double mc00 = mcp[0], mc01 = mcp[1], mc10 = mcp[2], mc22 = mcp[4];
+    if (!is_edge || src < 0 || !hm || act != 1) {
+#endif
+        if (f_old & 1) uts.fresh[k] = f_old & 2;
+        return;
+    }
+
+    extrap_math<false>(g, uts, e, p, w, k, v, f_old, smw, vc, node_x, node_y, node_z, node_r, nbx, nby, nbz, nbr, a, b,
+                       c, mc00, mc01, mc10, mc22, 0.0);
 }
 
 // slots [slot_lo, slot_hi), or (list) the slot_hi - slot_lo listed slots list[0, ...)

@@ -5,4 +5,4 @@ set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
 TAG=final5 bash tools/gpu_r05_final.sh || exit 1
-echo close4-done
+echo close5-done

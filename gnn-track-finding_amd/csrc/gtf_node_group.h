@@ -58,7 +58,6 @@ struct Grp {
     int lane4;  // 4 x the wave lane (ds_bpermute byte address of this lane)
     __device__ __forceinline__ Grp() {
         int tid = (int)threadIdx.x;
-        asm volatile("" : "+v"(tid));   // opaque: not hoisted out of the persistent kernel's item loop
         const int lane = tid & 63;
         gl = lane & (G - 1);
         gbase = lane & ~(G - 1);
@@ -141,8 +140,8 @@ struct Grp<0> {
     __device__ __forceinline__ int stage_base() const { return gbase; }
 };
 
-// Correctly rounded reciprocals 1/n (n = 1..64) in LDS: the persistent node kernel fills the
-// table once per block, and the ops' integer reciprocals (priors 1/count, mixture weights
+// Correctly rounded reciprocals 1/n (n = 1..64) in LDS: every node kernel block fills the
+// table at its start, and the ops' integer reciprocals (priors 1/count, mixture weights
 // 1/count, the side norm's divisor through qdiv) read it instead of running an fp64 division
 // (~10 VALU instructions each) -- the same bits (the table holds 1.0 / n itself)
 #ifndef GTF_RCP_TABLE
@@ -898,6 +897,25 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
     if (sc && pres) sc[c.k] = (alive >> pos & 1u) ? 2 : 1;   // diagnostics: merged (1) or left (2)
 }
 
+// LDS of one wavefront's clustering stages: the largest (64 / G) x sizeof(StageT<G>) over the
+// group sizes (G = 2: 32 stages of 216 bytes; every other G: 6,784 bytes). Every wave's stages
+// start at a multiple of this span whatever its G, so waves of one block that run different
+// group sizes can never overlap each other's stages (round-5 verdict item 1).
+template <int G>
+constexpr size_t wave_stage_bytes() { return (size_t)(64 / G) * sizeof(StageT<G>); }
+constexpr size_t max_sz(size_t a, size_t b) { return a > b ? a : b; }
+constexpr size_t WAVE_STAGE_BYTES =
+    max_sz(max_sz(max_sz(wave_stage_bytes<2>(), wave_stage_bytes<4>()), max_sz(wave_stage_bytes<8>(), wave_stage_bytes<16>())),
+           max_sz(wave_stage_bytes<32>(), wave_stage_bytes<64>()));
+static_assert(WAVE_STAGE_BYTES % 8 == 0, "stage spans keep 8-byte alignment");
+constexpr size_t node_smem_bytes() { return NBLOCK * sizeof(double) + (NBLOCK / 64) * WAVE_STAGE_BYTES; }
+// this lane's group's stage: the wave's own span, then the group's entry in it
+template <typename Stage, int G>
+__device__ __forceinline__ Stage* wave_stage(char* smem) {
+    const int t = (int)threadIdx.x;
+    return (Stage*)(smem + NBLOCK * sizeof(double) + (size_t)(t >> 6) * WAVE_STAGE_BYTES) + ((t & 63) / (G > 0 ? G : 64));
+}
+
 // ---------------------------------------------------------------------------
 // kernels: load a node's slots into lane registers, run the ops, write back
 // ---------------------------------------------------------------------------
@@ -1170,7 +1188,7 @@ __device__ __forceinline__ void node_seq_body(const gtf_graph& g, gtf_nodes& n, 
     }
 #endif
     double* sval = (double*)smem + (threadIdx.x & ~63);
-    Stage* stg = (Stage*)(smem + NBLOCK * sizeof(double)) + (Q::cluster ? (int)threadIdx.x / G : 0);
+    Stage* stg = Q::cluster ? wave_stage<Stage, G>(smem) : (Stage*)(smem + NBLOCK * sizeof(double));
 #if GTF_EARLY_STAGE
     // the clustering operands of every slot of a node that may cluster (>= 3 slots), read
     // with the slot fields and parked in the group's LDS stage at the slot lane
@@ -1219,20 +1237,7 @@ struct Buckets {
     int32_t count[6];
     int32_t blocks[6];
     Arith ar[6];             // padded tile layout (ar[q].c > 0: addresses by arithmetic)
-    int32_t wstart[7];       // persistent kernel: first wave item of each bucket, wstart[6] = all items
 };
-
-template <int G>
-constexpr size_t stage_bytes() { return (size_t)(NBLOCK / G) * sizeof(StageT<G>); }
-constexpr size_t node_smem_bytes() {
-    size_t m = stage_bytes<2>();
-    m = stage_bytes<4>() > m ? stage_bytes<4>() : m;
-    m = stage_bytes<8>() > m ? stage_bytes<8>() : m;
-    m = stage_bytes<16>() > m ? stage_bytes<16>() : m;
-    m = stage_bytes<32>() > m ? stage_bytes<32>() : m;
-    m = stage_bytes<64>() > m ? stage_bytes<64>() : m;
-    return NBLOCK * sizeof(double) + m;
-}
 
 // All arguments of k_node_multi in one by-value struct (the kernarg segment).
 struct NodeKArgs {
@@ -1270,6 +1275,22 @@ __device__ __forceinline__ void node_bucket(int q, int b, char* smem) {
                              *(gtf_states*)&A->uts, *(gtf_edges*)&A->e, *(const gtf_params*)&A->p,
                              *(const Ws*)&A->w, A->chi2_thr, A->kl_thr, A->bk.list[q], A->bk.seg[q],
                              A->bk.count[q], b, smem, *(const Arith*)&A->bk.ar[q]);
+}
+
+#include "gtf_node_tpn.h"
+// the <= 2-slot bucket one thread per node (gtf_node_tpn.h) instead of 2-lane groups
+#ifndef GTF_NODE_TPN
+#define GTF_NODE_TPN 1
+#endif
+template <int... OPS>
+constexpr bool node_tpn2() { return GTF_NODE_TPN && TpnOk<OPS...>::value; }
+
+template <int... OPS>
+__device__ __forceinline__ void node_bucket_tpn2(int b) {
+    const KArgPtr A = node_kargs();
+    tpn_body<2, OPS...>(*(const gtf_graph*)&A->g, *(gtf_nodes*)&A->n, *(gtf_states*)&A->tse, *(gtf_states*)&A->uts,
+                        *(gtf_edges*)&A->e, *(const gtf_params*)&A->p, *(const Ws*)&A->w, A->bk.list[5],
+                        A->bk.seg[5], A->bk.count[5], b);
 }
 
 // one launch over every bucket: blocks of the long-running buckets (many slots per node)
@@ -1332,146 +1353,10 @@ __global__ void __launch_bounds__(NBLOCK) GTF_NODE_WAVES_ATTR k_node_multi(NodeK
 #endif
     if (b < A->bk.blocks[4]) { node_bucket<4, OPS...>(4, b, smem); return; }
     b -= A->bk.blocks[4];
-    node_bucket<2, OPS...>(5, b, smem);
-}
-
-// ---------------------------------------------------------------------------
-// Persistent form of k_node_multi (the default): a grid of resident blocks whose WAVES each
-// loop over work items, one item = one wavefront's worth of lane groups of one bucket, in
-// the bucket order of k_node_multi (64, 32, 16, 8, 4, 2 lanes per node: the long-lived waves
-// first). Items come from WS_QUEUES work queues: queue j holds items j, j + NQ, j + 2 NQ, ...
-// (a round-robin slice of the heaviest-first order, NQ = 8 x waves per block) and is drawn by
-// the waves of one XCD (block % 8) and one wave slot of the block, one returning atomic
-// per item on the queue's own 128-byte line (a few hundred draws per counter per launch).
-// A wave draws its next item while it works on the current one and loads that item's
-// schedule entries (node, slot segment) one item ahead, so neither the draw nor the
-// dependent schedule round sits on an item's critical path. Waves never wait for each
-// other; every wave draws until its queue is empty and the one that draws the queue's last
-// ticket (items + waves of the queue) resets the counter to zero for the next launch.
-struct NodeEntry {
-    int v, lo, d;   // v < 0: this lane's group has no node in the item
-};
-
-__device__ __forceinline__ NodeEntry node_entry(const KArgPtr A, int item, int total) {
-    NodeEntry en{-1, 0, 0};
-    if (item >= total) return en;
-    int q = 0;   // the item's bucket (wave-uniform)
-#pragma unroll
-    for (int j = 1; j < 6; j++) q += item >= A->bk.wstart[j] ? 1 : 0;
-    const int wq = item - A->bk.wstart[q];
-    const int lane = (int)threadIdx.x & 63;
-    const int gi = (wq << q) + (lane >> (6 - q));   // G = 64 >> q lanes per node, 1 << q nodes per wave
-    if (gi < A->bk.count[q]) {
-        en.v = A->bk.list[q][gi];
-        const int32_t* sg = A->bk.seg[q];
-        if (sg) {
-            const int2 s2 = reinterpret_cast<const int2*>(sg)[gi];
-            en.lo = s2.x;
-            en.d = s2.y - s2.x;
-        } else {
-            en.lo = -1;   // (no sched_seg: the item reads slot_ptr)
-        }
-    }
-    return en;
-}
-
-template <int G, int... OPS>
-__device__ __forceinline__ void node_item(NodeEntry en, char* smem) {
-    const KArgPtr A = node_kargs();   // (re-read per item: no argument loads hoisted out of the item loop)
-    using Q = OpSeq<OPS...>;
-    using Stage = StageT<G>;
-    const gtf_graph& g = *(const gtf_graph*)&A->g;
-    gtf_nodes& n = *(gtf_nodes*)&A->n;
-    gtf_states& tse = *(gtf_states*)&A->tse;
-    gtf_states& uts = *(gtf_states*)&A->uts;
-    gtf_edges& e = *(gtf_edges*)&A->e;
-    const gtf_params& p = *(const gtf_params*)&A->p;
-    const Ws& w = *(const Ws*)&A->w;
-    NodeCtx<G> c;
-    if (en.v < 0) return;   // group-uniform
-    c.v = en.v;
-    if (en.lo >= 0) {
-        c.lo = en.lo;
-        c.d = en.d;
-    } else {
-        c.lo = g.slot_ptr[c.v];
-        c.d = g.slot_ptr[c.v + 1] - c.lo;
-    }
-    node_fields(c, g, tse, uts, e, Q::need);
-    double* sval = (double*)smem + (threadIdx.x & ~63);
-    Stage* stg = (Stage*)(smem + NBLOCK * sizeof(double)) + (Q::cluster ? (int)threadIdx.x / G : 0);
-    const bool has_tse = n.has_tse[c.v];
-    const bool has_uts = fresh_has_uts(c, n, Q::fresh);
-    (node_op<G, OPS, Stage>(c, g, n, tse, uts, e, p, w, sval, stg, A->chi2_thr, A->kl_thr, has_tse, has_uts), ...);
-    node_store(c, n, tse, uts, e);
-}
-
-constexpr int NODE_WPB = NBLOCK / 64;       // waves per block
-constexpr int NODE_NQ = 8 * NODE_WPB;       // work queues (one per XCD and wave slot)
-static_assert(NODE_NQ <= WS_QUEUES, "workspace queue counters");
-
-template <int... OPS>
-__global__ void __launch_bounds__(NBLOCK) GTF_NODE_WAVES_ATTR k_node_persist(NodeKArgs args) {
-    (void)args;   // read through node_kargs()
-    using Q = OpSeq<OPS...>;
-    __shared__ __attribute__((aligned(16))) char smem[Q::cluster ? node_smem_bytes() : NBLOCK * sizeof(double)];
-    const KArgPtr A = node_kargs();
-    node_tables_init();
-    __syncthreads();
-    const int lane = (int)threadIdx.x & 63;
-    const int xcd = (int)(blockIdx.x & 7);
-    const int qid = xcd * NODE_WPB + ((int)threadIdx.x >> 6);
-    const int total = A->bk.wstart[6];
-    const int q_items = total > qid ? (total - qid + NODE_NQ - 1) / NODE_NQ : 0;
-    const int q_waves = ((int)gridDim.x - xcd + 7) / 8;   // blocks on this queue's XCD slot
-    const int last = q_items + q_waves - 1;               // the queue's final ticket
-    uint32_t* ctr = A->w.queue + qid * WS_QSTRIDE;
-    // one ticket: lane 0 draws (returning atomic); the value is read later (the wave works meanwhile)
-    auto draw = [&]() -> int {
-        int t = 0;
-        if (lane == 0) t = (int)atomicAdd(ctr, 1u);
-        return t;
-    };
-    auto ticket = [&](int t) -> int {   // the item of a drawn ticket (total = none), reset on the last
-        t = __builtin_amdgcn_readfirstlane(t);
-        if (t == last && lane == 0) atomicExch(ctr, 0u);
-        return t < q_items ? qid + NODE_NQ * t : total;
-    };
-#ifndef GTF_PERSIST_PREFETCH
-#define GTF_PERSIST_PREFETCH 0   // 1: the next item's schedule entries loaded one item ahead (+3 VGPRs)
-#endif
-#if GTF_PERSIST_PREFETCH
-    int item = ticket(draw());
-    NodeEntry cur = node_entry(A, item, total);
-    int nxt = item < total ? ticket(draw()) : total;
-    while (item < total) {   // wave-uniform
-        const int tn = nxt < total ? draw() : 0;   // the ticket after next, drawn now
-        const NodeEntry nen = node_entry(A, nxt, total);   // next item's entries, loaded now
-#else
-    int item = ticket(draw());
-    while (item < total) {   // wave-uniform
-        const NodeEntry cur = node_entry(A, item, total);
-        const int tn = draw();   // the next ticket, drawn now, read after the item
-#endif
-        int q = 0;
-#pragma unroll
-        for (int j = 1; j < 6; j++) q += item >= A->bk.wstart[j] ? 1 : 0;
-        switch (q) {
-            case 0: node_item<64, OPS...>(cur, smem); break;
-            case 1: node_item<32, OPS...>(cur, smem); break;
-            case 2: node_item<16, OPS...>(cur, smem); break;
-            case 3: node_item<8, OPS...>(cur, smem); break;
-            case 4: node_item<4, OPS...>(cur, smem); break;
-            default: node_item<2, OPS...>(cur, smem); break;
-        }
-#if GTF_PERSIST_PREFETCH
-        item = nxt;
-        cur = nen;
-        nxt = nxt < total ? ticket(tn) : total;
-#else
-        item = ticket(tn);
-#endif
-    }
+    if constexpr (node_tpn2<OPS...>())
+        node_bucket_tpn2<OPS...>(b);
+    else
+        node_bucket<2, OPS...>(5, b, smem);
 }
 
 // Packed lane segments (gtf_graph.pack_ent / pack_wave): wavefront wv takes the entries

@@ -37,17 +37,12 @@ struct Ws {
     uint32_t* err;    // error word (the workspace's first bytes; gtf_diag at GTF_DIAG_OFFSET)
     double* vc;       // [S] per active edge, by SLOT: the merged_cov[1,1] its extrapolation sees
     const gtf_diag* diag;   // optional diagnostics outputs (gtf_set_diagnostics), in the workspace
-    uint32_t* queue;  // the persistent node kernel's work-queue counters (WS_QUEUES, 128 B apart)
 };
 
 __host__ inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
-// workspace header: [0, 256) error word + gtf_diag, [256, WS_HEAD) the node kernel's
-// work-queue counters -- zero between launches (gtf_workspace_init zeroes them once; every
-// launch leaves them zero: the wave that draws a queue's last ticket resets it)
-constexpr int WS_QUEUES = 64;
-constexpr int WS_QSTRIDE = 32;   // uint32 words between two counters: one 128-byte line each
-constexpr size_t WS_HEAD = 256 + (size_t)WS_QUEUES * WS_QSTRIDE * sizeof(uint32_t);
+// workspace header: [0, 256) error word + gtf_diag
+constexpr size_t WS_HEAD = 256;
 
 __host__ inline Ws carve(void* base, int32_t n_nodes, int32_t n_slots) {
     (void)n_nodes;
@@ -55,7 +50,6 @@ __host__ inline Ws carve(void* base, int32_t n_nodes, int32_t n_slots) {
     Ws w;
     w.err = (uint32_t*)p;
     w.diag = (const gtf_diag*)(p + GTF_DIAG_OFFSET);
-    w.queue = (uint32_t*)(p + 256);
     w.vc = (double*)(p + WS_HEAD);
     return w;
 }
@@ -1166,42 +1160,6 @@ int launch_ops(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* ut
     return err == hipSuccess ? 0 : fail("node kernel launch", err);
 }
 
-// the persistent node kernel (k_node_persist) with GTF_NODE_PERSIST=1 in the environment,
-// else the launch-per-item form k_node_multi (the default: measured faster);
-// the two are bit-identical
-bool node_persist_enabled() {
-    static const bool on = [] {
-        const char* v = getenv("GTF_NODE_PERSIST");
-        return v && v[0] == '1';
-    }();
-    return on;
-}
-
-// resident blocks of a persistent kernel on the current device: CUs x blocks per CU (its
-// occupancy), at most one block per 4 items, at least 8 (every work queue needs waves)
-int persist_grid(const void* kernel, int items) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    static int cus[64] = {0};
-    int& c = cus[dev & 63];
-    if (c == 0 && hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) c = 256;
-    static const void* ks[16] = {nullptr};   // occupancy per kernel, asked once
-    static int occ[16] = {0};
-    int per_cu = 0;
-    for (int i = 0; i < 16 && ks[i]; i++)
-        if (ks[i] == kernel) per_cu = occ[i];
-    if (per_cu == 0) {
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, NBLOCK, 0) != hipSuccess || per_cu < 1)
-            per_cu = 1;
-        for (int i = 0; i < 16; i++)
-            if (!ks[i]) { ks[i] = kernel; occ[i] = per_cu; break; }
-    }
-    int grid = c * per_cu;
-    const int need = (items + NODE_WPB - 1) / NODE_WPB;
-    if (grid > need) grid = need;
-    return grid < 8 ? 8 : grid;
-}
-
 // compile-time op sequence (the stage entry points)
 template <int... OPS>
 int launch_seq(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* uts, gtf_edges* e, const gtf_params* p,
@@ -1241,23 +1199,14 @@ int launch_seq(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* ut
                     bk.ar[q] = Arith{g->pad_count[j], noff[j], soff[j], g->pad_tile_nodes, g->pad_tile_slots};
                     bk.count[q] = g->pad_tiles * g->pad_count[j];
                 }
-                bk.blocks[q] = (bk.count[q] + NBLOCK / gs[q] - 1) / (NBLOCK / gs[q]);
+                // (the <= 2-slot bucket one thread per node where the sequence allows it)
+                const int per_block = (q == 5 && node_tpn2<OPS...>()) ? NBLOCK : NBLOCK / gs[q];
+                bk.blocks[q] = (bk.count[q] + per_block - 1) / per_block;
                 total += bk.blocks[q];
             }
-            // persistent form: one work item per wavefront's worth of lane groups, in bucket order
-            int items = 0;
-            for (int q = 0; q < 6; q++) {
-                bk.wstart[q] = items;
-                items += (bk.count[q] + 64 / gs[q] - 1) / (64 / gs[q]);
-            }
-            bk.wstart[6] = items;
-            const bool persist = node_persist_enabled() && g->pad_tiles == 0;
             if (g->pack_ent && g->pack_wave && g->n_pack_waves > 0)   // every <= 64-slot node, packed
                 hipLaunchKernelGGL((k_node_pack<OPS...>), dim3((g->n_pack_waves + NBLOCK / 64 - 1) / (NBLOCK / 64)),
                                    dim3(NBLOCK), 0, st, *g, *n, T, U, *e, *p, w, chi2, kl);
-            else if (persist && items > 0)
-                hipLaunchKernelGGL((k_node_persist<OPS...>), dim3(persist_grid((const void*)k_node_persist<OPS...>, items)),
-                                   dim3(NBLOCK), 0, st, NodeKArgs{*g, *n, T, U, *e, *p, w, chi2, kl, bk});
             else if (total > 0)
                 hipLaunchKernelGGL((k_node_multi<OPS...>), dim3(total), dim3(NBLOCK), 0, st,
                                    NodeKArgs{*g, *n, T, U, *e, *p, w, chi2, kl, bk});
@@ -1333,7 +1282,7 @@ size_t gtf_workspace_bytes(int32_t n_nodes, int32_t n_slots) {
 }
 
 int gtf_workspace_init(void* ws, gtf_stream_t stream) {
-    // error word + gtf_diag (no diagnostics) + the node kernel's work-queue counters
+    // error word + gtf_diag (no diagnostics)
     hipError_t e = hipMemsetAsync(ws, 0, WS_HEAD, (hipStream_t)stream);
     return e == hipSuccess ? 0 : fail("workspace init", e);
 }
@@ -1448,6 +1397,13 @@ int gtf_pass_shard(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states
     }
     if (!g->sched) {
         snprintf(g_err, sizeof(g_err), "gtf_pass_shard: needs the owned receivers' schedule in g->sched");
+        return -2;
+    }
+    // bit 4 (fused sender-major phase 1) only with bit 1, the sender schedule and no slot list:
+    // phases 4 / 6 would skip the edge phase silently, and the fused form ignores slot_list
+    if ((sh->phases & 4) && (!(sh->phases & 1) || !g->out_sched || sh->slot_list || sh->n_slot_list > 0)) {
+        snprintf(g_err, sizeof(g_err),
+                 "gtf_pass_shard: phases bit 4 needs bit 1, g->out_sched and no slot_list (phases %d)", sh->phases);
         return -2;
     }
     return run_pass(g, n, tse, uts, e, p, sh, ws, (hipStream_t)stream, events);

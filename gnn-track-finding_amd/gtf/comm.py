@@ -39,19 +39,37 @@ def unique_id(lib=None) -> bytes:
 _ID_MAGIC = b"GTFCOMM1"
 
 
+def _parent_identity() -> str:
+    """the launching parent process: its pid and its start time (field 22 of /proc/<pid>/stat,
+    clock ticks since boot), so a recycled pid of a later launcher gives another identity"""
+    ppid = os.getppid()
+    try:
+        with open("/proc/%d/stat" % ppid, "rb") as fh:
+            stat = fh.read().decode(errors="replace")
+        start = stat[stat.rindex(")") + 2:].split()[19]
+    except (OSError, ValueError, IndexError):
+        start = "?"
+    return "%d@%s" % (ppid, start)
+
+
 def job_token() -> str:
     """a token that names this launch of the job: GTF_COMM_JOB, else the launcher's run id
-    (torchrun's TORCHELASTIC_RUN_ID, Slurm's SLURM_JOB_ID.SLURM_STEP_ID), else its rendezvous
-    address MASTER_ADDR:MASTER_PORT (a port is bound by one job at a time)"""
+    (torchrun's TORCHELASTIC_RUN_ID when it is a real id -- torchrun's default static
+    rendezvous sets the literal "none" --, Slurm's SLURM_JOB_ID.SLURM_STEP_ID), else the
+    rendezvous address MASTER_ADDR:MASTER_PORT together with the identity of the launching
+    parent process (pid and start time). The address alone does not tell two runs apart
+    (consecutive runs reuse the default port 29500); the ranks of one launch on a node share
+    their parent (torchrun's agent, bench.spawn_ranks), and a later launch has another one."""
     e = os.environ
     if e.get("GTF_COMM_JOB"):
         return e["GTF_COMM_JOB"]
-    if e.get("TORCHELASTIC_RUN_ID"):
-        return "torchelastic:" + e["TORCHELASTIC_RUN_ID"]
+    rid = e.get("TORCHELASTIC_RUN_ID", "")
+    if rid and rid.lower() != "none":
+        return "torchelastic:" + rid
     if e.get("SLURM_JOB_ID"):
         return "slurm:%s.%s" % (e["SLURM_JOB_ID"], e.get("SLURM_STEP_ID", ""))
     if e.get("MASTER_PORT"):
-        return "rdzv:%s:%s" % (e.get("MASTER_ADDR", ""), e["MASTER_PORT"])
+        return "rdzv:%s:%s:parent:%s" % (e.get("MASTER_ADDR", ""), e["MASTER_PORT"], _parent_identity())
     raise ValueError("NativeComm.from_file needs a job token: pass job=... or set GTF_COMM_JOB "
                      "(or run under a launcher that sets MASTER_PORT / TORCHELASTIC_RUN_ID)")
 
@@ -81,7 +99,8 @@ def read_id_file(path: str, job: str, timeout: float = 120.0) -> bytes:
         except FileNotFoundError:
             pass
         if time.monotonic() - t0 > timeout:
-            raise TimeoutError("no RCCL unique id of job %r at %s after %.0f s" % (job, path, timeout))
+            raise TimeoutError("no RCCL unique id of job %r at %s after %.0f s (ranks launched by different "
+                               "parents need a common GTF_COMM_JOB)" % (job, path, timeout))
         time.sleep(0.01)
 
 

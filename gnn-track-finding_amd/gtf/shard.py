@@ -335,6 +335,7 @@ class ShardedDeviceGraph:
         # halo overlaps the next pass's phase 1a (step)
         self._phase_t = []
         self.cg_phase, self.shard_phase = [], []
+        self._part_slots = []
         for part_s, part_k in (lambda x: ((x[0], x[2]), (x[1], x[3])))(pl.split(rank)):
             z1 = np.zeros(1, np.int32)
             ts, tk = up(np.concatenate([part_s, z1])), up(np.concatenate([part_k, z1]))   # int32, never empty
@@ -351,15 +352,18 @@ class ShardedDeviceGraph:
             # their owned out-edges, one launch) -- measured slower on the box (N = 8: 18.0 vs
             # 14.7 us; the fused kernel runs 3 waves per SIMD at 145 VGPRs)
             ph = 5 if (self.shard_phase and os.environ.get("GTF_SHARD_FUSED_1B", "0") == "1") else 1
+            self._part_slots.append(int(part_k.size))
+            # (the fused form extrapolates the senders' owned out-edges itself: no slot list)
             self.shard_phase.append(nat.GtfShard(vp(ts), int(part_s.size), int(pl.node_lo[rank]), int(pl.node_hi[rank]),
                                                  int(pl.slot_lo[rank]), int(pl.slot_hi[rank]),
-                                                 ph, vp(tk), int(part_k.size), 0))
+                                                 ph, vp(tk) if ph != 5 else ctypes.c_void_p(0),
+                                                 int(part_k.size) if ph != 5 else 0, 0))
         self.shard_node = nat.GtfShard(vp(self.senders), int(self.senders.numel()), int(pl.node_lo[rank]),
                                        int(pl.node_hi[rank]), int(pl.slot_lo[rank]), int(pl.slot_hi[rank]), 2)
         self.split_sizes = {"interior_senders": int(self.shard_phase[0].n_senders),
                             "halo_senders": int(self.shard_phase[1].n_senders),
                             "interior_slots": int(self.shard_phase[0].n_slot_list),
-                            "halo_slots": int(self.shard_phase[1].n_slot_list)}
+                            "halo_slots": int(self._part_slots[1])}
         self.overlap = True        # step(): the halo exchange beside the next pass's phase 1a
         self._pending = False      # a pass's halo not yet exchanged
         # halo exchange buffers and lists (fixed per plan)
@@ -420,6 +424,18 @@ class ShardedDeviceGraph:
                                self.recv_buf[:sum(self.recv_sizes)])
         return io
 
+    def _tstream(self):
+        """the cached pass stream (_io) as a torch stream: the exchange's events, asynchronous
+        collectives and host copies are ordered against THIS stream, on which halo_pack /
+        halo_unpack and the phases run, whatever stream is current at a later call"""
+        ts = getattr(self, "_ts_c", None)
+        if ts is None:
+            torch = self.torch
+            h = self._io()[1].value or 0
+            dev = torch.device(self.d.device)
+            ts = self._ts_c = (torch.cuda.ExternalStream(h, device=dev) if h else torch.cuda.default_stream(dev))
+        return ts
+
     def _cparams(self, p):
         key = (p.sigma0xy, p.sigma0rz, p.sigma0rz2, p.endcap_boundary, p.chi2_cut, p.reweight_threshold,
                p.cluster_chi2, p.cluster_kl)
@@ -429,7 +445,9 @@ class ShardedDeviceGraph:
         return c[1]
 
     def pass_(self, p, events=None):
-        """the pass for the owned receivers (events: optional 5 hipEvent_t handles)"""
+        """the pass for the owned receivers (events: optional 5 hipEvent_t handles); a halo
+        an overlapped step left pending is exchanged first"""
+        self.flush()
         d = self.d
         ws, st = self._io()[:2]
         ev = (ctypes.c_void_p * 5)(*events) if events is not None else None
@@ -439,6 +457,7 @@ class ShardedDeviceGraph:
 
     def exchange(self):
         """the halo: what the other ranks' next pass reads, one all-to-all"""
+        self.flush()
         if self.comm is not None:   # pack, all-to-all and unpack inside libgtf (gtf_halo_exchange)
             d = self.d
             _, st, sbuf, rbuf = self._io()[:4]
@@ -451,7 +470,8 @@ class ShardedDeviceGraph:
             return
         _, st, sbuf, rbuf, sview, rview = self._io()
         self.halo_pack()
-        alltoall_bytes(sview, rview, self.send_sizes, self.recv_sizes, self.backend, self.group)
+        with self.torch.cuda.stream(self._tstream()):   # ordered after the pack, before the unpack
+            alltoall_bytes(sview, rview, self.send_sizes, self.recv_sizes, self.backend, self.group)
         self.halo_unpack(rbuf)
 
     def halo_pack(self):
@@ -496,21 +516,23 @@ class ShardedDeviceGraph:
                                        ctypes.byref(d.cuts), ctypes.byref(d.ce), ctypes.byref(self._cparams(p)),
                                        ctypes.byref(sh), ws, st, None))
 
-    def _exchange_begin(self):
-        """pack this rank's halo segments and start the all-to-all; returns what
+    def _exchange_begin(self, pack=True):
+        """(pack this rank's halo segments and) start the all-to-all; returns what
         _exchange_end needs. The pack is stream-ordered before anything the caller enqueues
-        next, so the next pass's phase 1a can run while the segments travel."""
+        next, so the next pass's phase 1a can run while the segments travel. step() packs at
+        the end of its own pass (pack=False here): the halo is that pass's outputs whatever
+        the caller does between two steps (e.g. bench's use_inputs)."""
         if self.world == 1 and self.comm is None:
             return None
-        self.halo_pack()
+        if pack:
+            self.halo_pack()
         _, st, sbuf, rbuf, sview, rview = self._io()
         if self.comm is not None:   # libgtf's RCCL group on a stream of its own
             torch = self.torch
             if getattr(self, "_xs", None) is None:
                 self._xs = torch.cuda.Stream(device=self.d.device)
                 self._xev = (torch.cuda.Event(), torch.cuda.Event())
-            cur = torch.cuda.current_stream(self.d.device)
-            self._xev[0].record(cur)
+            self._xev[0].record(self._tstream())   # after the pack (on the pass stream)
             self._xs.wait_event(self._xev[0])
             nat.check(self.d.lib.gtf_halo_alltoall(self.comm.ptr, sbuf, rbuf,
                                                    ctypes.cast(self._sizes_c[0], ctypes.c_void_p),
@@ -520,20 +542,25 @@ class ShardedDeviceGraph:
             return "native"
         if self.backend == "nccl":   # torch.distributed over RCCL, asynchronous
             import torch.distributed as dist
-            return dist.all_to_all_single(rview, sview, self.recv_sizes, self.send_sizes, group=self.group,
-                                          async_op=True)
+            # the collective's stream waits on the CURRENT stream: make it the pass stream
+            with self.torch.cuda.stream(self._tstream()):
+                return dist.all_to_all_single(rview, sview, self.recv_sizes, self.send_sizes, group=self.group,
+                                              async_op=True)
         return "host"   # gloo: through host memory at _exchange_end
 
     def _exchange_end(self, h):
         if h is None:
             return
         _, st, sbuf, rbuf, sview, rview = self._io()
+        ts = self._tstream()   # the unpack runs on the pass stream: that stream waits
         if h == "native":
-            self.torch.cuda.current_stream(self.d.device).wait_event(self._xev[1])
-        elif h == "host":
-            alltoall_bytes(sview, rview, self.send_sizes, self.recv_sizes, self.backend, self.group)
+            ts.wait_event(self._xev[1])
         else:
-            h.wait()
+            with self.torch.cuda.stream(ts):
+                if h == "host":
+                    alltoall_bytes(sview, rview, self.send_sizes, self.recv_sizes, self.backend, self.group)
+                else:
+                    h.wait()
         self.halo_unpack(rbuf)
 
     def step(self, p, events=None, overlap=None):
@@ -550,19 +577,21 @@ class ShardedDeviceGraph:
             self.pass_(p, events)
             self.exchange()
             return
-        h = self._exchange_begin() if self._pending else None
+        h = self._exchange_begin(pack=False) if self._pending else None
         self._pending = False
         self._phase(p, 0)
         self._exchange_end(h)
         self._phase(p, 1)
         self._phase(p, 2)
-        self._pending = self.world > 1 or self.comm is not None   # (native: RCCL even at world 1)
+        if self.world > 1 or self.comm is not None:   # (native: RCCL even at world 1)
+            self.halo_pack()        # this pass's halo, packed now; sent by the next step / flush
+            self._pending = True
 
     def flush(self):
-        """the pending halo exchange (a step's last pass), now"""
+        """the pending halo exchange (a step's last pass, already packed), now"""
         if self._pending:
             self._pending = False
-            self._exchange_end(self._exchange_begin())
+            self._exchange_end(self._exchange_begin(pack=False))
 
     def tag_propagation(self, tags, radius, threshold=0.1, max_sweeps=100000):
         """Tag propagation (tag_propagation/tag_propagation.py:97-164) on the edge-sharded

@@ -327,69 +327,8 @@ def bench_components(g, params, dev, reps=5):
     npairs = int(cols["chi2"].numel())
     dt = float(np.median(ts[1:]))
     out["a15_updated_state_distances"] = {"pairs": npairs, "wall_ms": dt * 1e3, "pairs_per_s": npairs / dt}
-    tags = np.arange(g.n_nodes, dtype=np.int64)
-    radius = np.ascontiguousarray(g.node["xyzr"][:, 3])
-    import ctypes
-    vp = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
-    rad = torch.from_numpy(np.ascontiguousarray(d._to_dev_nodes(radius))).to(dev)
-    t_init = torch.from_numpy(np.ascontiguousarray(d._to_dev_nodes(tags))).to(dev)
-    ta = torch.empty_like(t_init)
-    # the stage as a device-resident caller runs it: one gtf_tag_propagate call (prepare, the
-    # sweeps with their stop test on the device, one flip-count read per batch), wall time
-    # from the call to its return with the final tags in place
-    ts = []
-    for _ in range(reps + 1):
-        ta.copy_(t_init)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        flips = d.tag_propagation_dev(ta, rad)
-        torch.cuda.synchronize()
-        ts.append(time.perf_counter() - t0)
-    dt = float(np.median(ts[1:]))
-    # the same with host-order inputs and outputs (upload, download, reordering: the Python API)
-    ts = []
-    for _ in range(reps + 1):
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        d.tag_propagation(tags, radius)
-        torch.cuda.synchronize()
-        ts.append(time.perf_counter() - t0)
-    dt_host = float(np.median(ts[1:]))
-    # the prepare and sweep kernels alone: K calls back to back between two events
-    keep = torch.zeros(max(g.n_edges, 1), dtype=torch.uint8, device=dev)
-    proc = torch.zeros(max(g.n_nodes, 1), dtype=torch.uint8, device=dev)
-    cnt = torch.zeros(2, dtype=torch.int32, device=dev)
-    tb = torch.empty_like(ta)
+    out["a16_tag_propagation"] = bench_tags(d, g, dev, reps)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    K = 50
-    e0.record()
-    for i in range(K):
-        d.lib.gtf_tag_prepare(ctypes.byref(d.cg), vp(rad), vp(keep), vp(proc), vp(cnt), d.stream)
-    e1.record()
-    torch.cuda.synchronize()
-    prep_ms = e0.elapsed_time(e1) / K
-    e0.record()
-    for i in range(K):
-        d.lib.gtf_tag_sweep(ctypes.byref(d.cg), vp(keep), vp(proc), vp(ta if i % 2 == 0 else tb),
-                            vp(tb if i % 2 == 0 else ta), vp(cnt[1:2]), d.stream)
-    e1.record()
-    torch.cuda.synchronize()
-    sweep_ms = e0.elapsed_time(e1) / K
-    sweeps = len(flips)
-    nbytes = 4 * g.n_edges + 8 * g.n_nodes   # SURVEY §8d B_tag, per sweep
-    out["a16_tag_propagation"] = {"sweeps": sweeps, "flips": [int(x) for x in flips], "stage_wall_ms": dt * 1e3,
-                                  "stage_wall_host_order_ms": dt_host * 1e3,
-                                  "prepare_call_ms": prep_ms, "sweep_call_ms": sweep_ms,
-                                  "stage_over_kernels": dt * 1e3 / (prep_ms + sweeps * sweep_ms),
-                                  "algorithmic_bytes_per_sweep": nbytes,
-                                  "achieved_GBps": nbytes / (sweep_ms * 1e-3) / 1e9,
-                                  "frac_of_peak": nbytes / (sweep_ms * 1e-3) / 1e9 / rf.HBM_PEAK_GBS,
-                                  "note": "stage_wall_ms: one gtf_tag_propagate call on device-resident tags / radius "
-                                          "(prepare, sweeps with the stop rule evaluated on the device, one flip-count "
-                                          "read per batch of sweeps), call to return; stage_over_kernels = that wall "
-                                          "time / (prepare + sweeps x sweep) kernel time; *_call_ms: K calls back to "
-                                          "back between two events; stage_wall_host_order_ms adds the host-order "
-                                          "upload, download and reordering of DeviceGraph.tag_propagation"}
     # a2: the initial per-edge states of event conversion (helper.py:238-452 + priors,
     # mixture weights, degree; pipeline.build_event's device half) on the same event
     def tse():
@@ -500,6 +439,77 @@ def bench_c5_sharded(dev, steps, warmup, rank, world, backend, n_events=256):
             "collective": "none (events are independent)", "device_error_flags": flags}
 
 
+def bench_tags(d, g, dev, reps=5):
+    """tag propagation (a16, tag_propagation.py:99-164) on a device graph after a pass: one
+    gtf_tag_propagate call (wall), the host-order API, and the prepare / sweep kernels alone
+    (K calls between two events) against SURVEY §8(d)'s B_tag = 4 E + 8 N per sweep"""
+    import torch
+    from gtf import roofline as rf
+    tags = np.arange(g.n_nodes, dtype=np.int64)
+    radius = np.ascontiguousarray(g.node["xyzr"][:, 3])
+    import ctypes
+    vp = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+    rad = torch.from_numpy(np.ascontiguousarray(d._to_dev_nodes(radius))).to(dev)
+    t_init = torch.from_numpy(np.ascontiguousarray(d._to_dev_nodes(tags))).to(dev)
+    ta = torch.empty_like(t_init)
+    # the stage as a device-resident caller runs it: one gtf_tag_propagate call (prepare, the
+    # sweeps with their stop test on the device, one flip-count read per batch), wall time
+    # from the call to its return with the final tags in place
+    ts = []
+    for _ in range(reps + 1):
+        ta.copy_(t_init)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        flips = d.tag_propagation_dev(ta, rad)
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    dt = float(np.median(ts[1:]))
+    # the same with host-order inputs and outputs (upload, download, reordering: the Python API)
+    ts = []
+    for _ in range(reps + 1):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        d.tag_propagation(tags, radius)
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    dt_host = float(np.median(ts[1:]))
+    # the prepare and sweep kernels alone: K calls back to back between two events
+    keep = torch.zeros(max(g.n_edges, 1), dtype=torch.uint8, device=dev)
+    proc = torch.zeros(max(g.n_nodes, 1), dtype=torch.uint8, device=dev)
+    cnt = torch.zeros(2, dtype=torch.int32, device=dev)
+    tb = torch.empty_like(ta)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    K = 50
+    e0.record()
+    for i in range(K):
+        d.lib.gtf_tag_prepare(ctypes.byref(d.cg), vp(rad), vp(keep), vp(proc), vp(cnt), d.stream)
+    e1.record()
+    torch.cuda.synchronize()
+    prep_ms = e0.elapsed_time(e1) / K
+    e0.record()
+    for i in range(K):
+        d.lib.gtf_tag_sweep(ctypes.byref(d.cg), vp(keep), vp(proc), vp(ta if i % 2 == 0 else tb),
+                            vp(tb if i % 2 == 0 else ta), vp(cnt[1:2]), d.stream)
+    e1.record()
+    torch.cuda.synchronize()
+    sweep_ms = e0.elapsed_time(e1) / K
+    sweeps = len(flips)
+    nbytes = 4 * g.n_edges + 8 * g.n_nodes   # SURVEY §8d B_tag, per sweep
+    return {"sweeps": sweeps, "flips": [int(x) for x in flips], "stage_wall_ms": dt * 1e3,
+                                  "stage_wall_host_order_ms": dt_host * 1e3,
+                                  "prepare_call_ms": prep_ms, "sweep_call_ms": sweep_ms,
+                                  "stage_over_kernels": dt * 1e3 / (prep_ms + sweeps * sweep_ms),
+                                  "algorithmic_bytes_per_sweep": nbytes,
+                                  "achieved_GBps": nbytes / (sweep_ms * 1e-3) / 1e9,
+                                  "frac_of_peak": nbytes / (sweep_ms * 1e-3) / 1e9 / rf.HBM_PEAK_GBS,
+                                  "note": "stage_wall_ms: one gtf_tag_propagate call on device-resident tags / radius "
+                                          "(prepare, sweeps with the stop rule evaluated on the device, one flip-count "
+                                          "read per batch of sweeps), call to return; stage_over_kernels = that wall "
+                                          "time / (prepare + sweeps x sweep) kernel time; *_call_ms: K calls back to "
+                                          "back between two events; stage_wall_host_order_ms adds the host-order "
+                                          "upload, download and reordering of DeviceGraph.tag_propagation"}
+
+
 def bench_c3_section(dev, steps, warmup, params, layout="tiled", tile=4096):
     """configs[2] beside the C4 headline: 64 C2-like events fused into one CSR (2.0 M hits /
     5.9 M edges), K passes on staged inputs, then the same K with HIP events around the
@@ -548,6 +558,12 @@ def bench_c3_section(dev, steps, warmup, params, layout="tiled", tile=4096):
                         "byte_model": "SURVEY §8d (fused node kernel 89 B/edge + 186 B/node)"},
            "pass_roofline": {"algorithmic_bytes_per_step": pb, "frac": pb / t / 1e9 / rf.HBM_PEAK_GBS},
            "device_error_flags": d.errors()}
+    # a16 on the fused 5.9 M-edge graph after the pass: several sweeps (where C4 stops after one),
+    # the sweep kernel at a size where it can be bandwidth-bound
+    try:
+        res["a16_tag_propagation"] = bench_tags(d, g, dev, reps=3)
+    except Exception as ex:   # reported; the section stands
+        res["a16_tag_propagation"] = {"error": repr(ex)[:300]}
     del d
     torch.cuda.empty_cache()
     return res
@@ -646,6 +662,48 @@ def bench_sharded(workload, rank, world, dev, steps, warmup, params, backend="nc
         issue[True] = issue_ov
     el_pass = run(False)
     run(False, instrumented=True)   # this rank's kernels between events (the sharded roofline)
+    # the overlapped step with HIP events between its parts on the pass stream (rank 0's in
+    # the line): phase 1a, the wait for the halo and its unpack, phase 1b, the node kernels
+    pevs = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(steps)]
+    sd.overlap = True
+    sd.d.fill_inputs(snap)
+    torch.cuda.synchronize()
+    dist.barrier()
+    for i in range(steps):
+        sd.d.use_inputs(i)
+        sd.step(params, phase_events=pevs[i])
+    sd.flush()
+    torch.cuda.synchronize()
+    dist.barrier()
+    sd.d.use_inputs(None)
+
+    def pavg(a, b):
+        return float(np.mean([pevs[i][a].elapsed_time(pevs[i][b]) for i in range(1, steps)]))   # (step 0: no halo)
+    phase_ms = {"phase_1a": pavg(0, 1), "exchange_wait_and_unpack": pavg(1, 2), "phase_1b": pavg(2, 3),
+                "node_kernels_and_pack": pavg(3, 4), "step": pavg(0, 4)}
+    # the halo all-to-all alone (the collective, no pack / unpack), K times between barriers
+    from gtf.shard import alltoall_bytes
+    sview, rview = sd._io()[4:6]
+    with torch.cuda.stream(sd._tstream()):
+        for _ in range(2):
+            alltoall_bytes(sview, rview, sd.send_sizes, sd.recv_sizes, torch_backend, None)
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            alltoall_bytes(sview, rview, sd.send_sizes, sd.recv_sizes, torch_backend, None)
+        torch.cuda.synchronize()
+        a2a_s = reduce_scalar(time.perf_counter() - t0, dist.ReduceOp.MAX, dev, torch_backend)
+    if backend == "native":   # libgtf's own grouped send / receive pairs: the whole exchange
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            sd.exchange()
+        torch.cuda.synchronize()
+        a2a_native_s = reduce_scalar(time.perf_counter() - t0, dist.ReduceOp.MAX, dev, torch_backend)
+    else:
+        a2a_native_s = None
     flags = int(reduce_scalar(sd.d.errors(), dist.ReduceOp.MAX, dev, torch_backend))
     hb = int(reduce_scalar(sd.halo_bytes, dist.ReduceOp.MAX, dev, torch_backend))
     pl = sd.plan
@@ -701,6 +759,14 @@ def bench_sharded(workload, rank, world, dev, steps, warmup, params, backend="nc
             "overlap": ("the halo exchange of pass i beside pass i+1's phase 1a (the senders whose state and "
                         "out-edge activations are all the rank's own, and the slots they send to; gtf_shard.phases)"),
             "rank0_split": sd.split_sizes,
+            "rank0_phase_ms": phase_ms,
+            "rank0_phase_timing": ("HIP events on rank 0's pass stream inside the overlapped step (steps 1..K-1): "
+                                   "phase 1a, the wait for the previous halo + its unpack, phase 1b, the node kernels "
+                                   "+ this pass's halo pack"),
+            "alltoall_ms": a2a_s / steps * 1e3,
+            "alltoall_note": ("the halo all_to_all_single alone (%s, no pack / unpack), wall time per call, max "
+                              "over ranks" % torch_backend),
+            "native_exchange_ms": a2a_native_s / steps * 1e3 if a2a_native_s is not None else None,
             "owned_slots_min": int((pl.slot_hi - pl.slot_lo).min()),
             "owned_directed_edges_max": own_edges_max, "owned_nodes_max": own_nodes_max,
             "collective": ("gtf_halo_exchange: per-destination halo segments, grouped ncclSend / ncclRecv inside "
@@ -818,8 +884,10 @@ def main():
                     help="device node order (DeviceGraph layout)")
     ap.add_argument("--tile", type=int, default=4096, help="nodes per tile of --layout tiled")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo", "native"],
-                    help="collectives for N > 1: nccl = torch.distributed over RCCL, native = libgtf's own RCCL "
-                         "communicator (gtf_comm_*, the id handed over torch.distributed), gloo = rehearsal with "
+                    help="collectives for N > 1: nccl = torch.distributed over RCCL (the default), native = "
+                         "libgtf's own RCCL communicator (gtf_comm_*, the id handed over torch.distributed; NOTE: "
+                         "it has never run with more than one rank -- the test box has one GPU -- so its grouped "
+                         "send / receive pairing at world > 1 is unverified on hardware), gloo = rehearsal with "
                          "several ranks on one GPU")
     args = ap.parse_args()
     if args.gpus < 1:
@@ -1054,6 +1122,17 @@ def main():
                 replicas["kernel_ms"] = out["kernel_ms"]
                 out["roofline"] = sharded["roofline"]
                 out["kernel_ms"] = sharded["roofline"]["kernel_ms_all"]
+                # the N = 1 -> N speed-up of the single event: measured (this GPU's own one-event
+                # pass, event_replicas, against the sharded step), compute only (the sharded
+                # pass without its exchange), and DESIGN.md §6's projection from rank 0's
+                # compute-only pass on one MI355X (profiles/r05/shard/shard_pass_time.log)
+                proj = {2: 138.2 / 81.1, 4: 138.2 / 55.5, 8: 138.2 / 37.6}
+                sharded["speedup_vs_one_gpu"] = {
+                    "measured": replicas["ms_per_step"] / sharded["ms_per_step"],
+                    "compute_only_this_run": replicas["ms_per_step"] / sharded["pass_ms_no_exchange"],
+                    "projected_design": proj.get(world),
+                    "projected_source": "DESIGN.md §6: rank 0's compute-only share of the C4 pass, N = 1 138.2 us, "
+                                        "N = 2 / 4 / 8 81.1 / 55.5 / 37.6 us (profiles/r05/shard/)"}
                 out["sharded_single_event"] = sharded
                 if sharded["device_error_flags"]:
                     out["invalid"] = "sharded pass device_error_flags %d" % sharded["device_error_flags"]

@@ -563,13 +563,15 @@ class ShardedDeviceGraph:
                     h.wait()
         self.halo_unpack(rbuf)
 
-    def step(self, p, events=None, overlap=None):
+    def step(self, p, events=None, overlap=None, phase_events=None):
         """one pass of the owned receivers. overlap (default self.overlap = True): the pass
         in phases -- the previous pass's halo exchange (pending) starts, phase 1a (interior
         senders and their slots, which read nothing the exchange brings) runs while it
         travels, then the halo is unpacked and phase 1b and the node kernels follow; this
         pass's own halo stays pending until the next step (or flush / sync). Bit-equal to
-        overlap=False (the one-call pass, then the exchange)."""
+        overlap=False (the one-call pass, then the exchange). phase_events (diagnostics):
+        5 torch events recorded on the pass stream before phase 1a, after it, after the
+        exchange's wait and unpack, after phase 1b, after the node kernels and the pack."""
         if overlap is None:
             overlap = self.overlap
         if not overlap or events is not None:
@@ -577,15 +579,27 @@ class ShardedDeviceGraph:
             self.pass_(p, events)
             self.exchange()
             return
+        pe = phase_events
+        ts = self._tstream() if pe is not None else None
+        if pe is not None:
+            pe[0].record(ts)
         h = self._exchange_begin(pack=False) if self._pending else None
         self._pending = False
         self._phase(p, 0)
+        if pe is not None:
+            pe[1].record(ts)
         self._exchange_end(h)
+        if pe is not None:
+            pe[2].record(ts)
         self._phase(p, 1)
+        if pe is not None:
+            pe[3].record(ts)
         self._phase(p, 2)
         if self.world > 1 or self.comm is not None:   # (native: RCCL even at world 1)
             self.halo_pack()        # this pass's halo, packed now; sent by the next step / flush
             self._pending = True
+        if pe is not None:
+            pe[4].record(ts)
 
     def flush(self):
         """the pending halo exchange (a step's last pass, already packed), now"""

@@ -275,6 +275,9 @@ def bench_c5(dev, steps, warmup, n_events=256, n_batches=8, hot=True, dtypes=("f
         gbs = nbytes / (ms * 1e-3) / 1e9
         res[dt] = {"pairs_per_s": k.n_pairs / (ms * 1e-3), "kernel_ms": ms, "wall_ms_per_launch": wall * 1e3,
                    "launches": launches,
+                   # the order of this dtype's launches in a kernel trace (tools/kstats_c5.py splits
+                   # a rocprofv3 trace by it: the cold rotation's average apart from the hot one's)
+                   "launch_sequence": {"warmup": warmup * len(ks), "cold": launches, "hot": launches if hot else 0},
                    "roofline": {"bound": "hbm", "achieved": gbs, "peak": rf.HBM_PEAK_GBS, "unit": "GB/s",
                                 "frac": gbs / rf.HBM_PEAK_GBS, "algorithmic_bytes_per_launch": nbytes,
                                 "footprint_bytes_all_batches": foot, "footprint_bytes_per_batch": foot // len(ks),

@@ -374,7 +374,7 @@ __device__ __forceinline__ void g_priors(NodeCtx<G>& c, LaneDict& st, double* sv
 template <int G>
 __device__ __forceinline__ double uts_x(const NodeCtx<G>& c, const gtf_graph& g, const gtf_states& uts) {
     if (!c.valid) return 0.0;
-    if (c.live) return g.gnn[4 * (int64_t)g.slot_src[c.k]];
+    if (c.live) return g.slot_sxzr ? g.slot_sxzr[3 * (int64_t)c.k] : g.gnn[4 * (int64_t)g.slot_src[c.k]];
     return uts.xyzr[4 * (int64_t)c.k];
 }
 
@@ -500,9 +500,12 @@ __device__ __forceinline__ void g_mixture_weights(NodeCtx<G>& c, LaneDict& st, b
 template <int G>
 __device__ __forceinline__ void g_fresh(NodeCtx<G>& c) {
     if (c.valid && c.fresh) {
-        c.uts.mw = c.smw;
+        if (!GTF_MW_IN_EXTRAP) {   // (else k_extrapolate stored it)
+            c.uts.mw = c.smw;
+            c.uts.dirty |= D_MW;
+        }
         c.uts.prior = NAN;
-        c.uts.dirty |= D_MW | D_PRIOR;
+        c.uts.dirty |= D_PRIOR;
         c.lr = NAN;
         c.side = -1;
         c.uts_dirty_lr = true;
@@ -555,7 +558,7 @@ struct StageT {
 // the clustering operands of this lane's state, raw, at its slot lane
 template <typename Stage>
 __device__ __forceinline__ void stage_raw(Stage* stg, int li, const gtf_states& S, int64_t k, const double* gnn,
-                                          bool live, int src) {
+                                          bool live, int src, const double* sxzr) {
     stg->a[li] = S.sv[3 * k];
     stg->b[li] = S.sv[3 * k + 1];
     stg->c[li] = S.sv[3 * k + 2];
@@ -563,7 +566,15 @@ __device__ __forceinline__ void stage_raw(Stage* stg, int li, const gtf_states& 
     const double* cv = S.cov + 5 * k;
     stg->c00[li] = cv[0]; stg->c01[li] = cv[1]; stg->c10[li] = cv[2]; stg->c11[li] = cv[3]; stg->c22[li] = cv[4];
     // the state's stored sender coordinates: the sender's live GNN ones for an entry message
-    // passing wrote (gtf_states.fresh bit 1), else the snapshot
+    // passing wrote (gtf_states.fresh bit 1) -- from the slot's own copy (gtf_graph.slot_sxzr,
+    // contiguous) or gathered from the sender's gnn row --, else the snapshot
+    if (live && sxzr) {
+        const double* xp = sxzr + 3 * k;
+        stg->q[li] = xp[0];
+        stg->w[li] = xp[1];
+        stg->tg[li] = xp[2];
+        return;
+    }
     const double* xp = live ? gnn + 4 * (int64_t)src : S.xyzr + 4 * k;
     stg->q[li] = xp[0];
     stg->w[li] = xp[2];
@@ -619,7 +630,8 @@ __device__ uint64_t g_op_time[GTF_OP_TIMING_WAVES * 24];
 template <int G, typename Stage>
 __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf_states& S, LaneDict& st,
                                           Stage* stg, const double* xyzr_node, const double* gnn, bool live,
-                                          double chi2_thr, double kl_thr, const gtf_params& p, uint32_t* err) {
+                                          double chi2_thr, double kl_thr, const gtf_params& p, uint32_t* err,
+                                          const double* sxzr, bool prior_known) {
 #if GTF_ABLATE == 1
     return;  // diagnostics build (tools/ablate_build.sh): no clustering work
 #endif
@@ -636,7 +648,7 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
     const double xa = xyzr_node[0], za = xyzr_node[2], ra = xyzr_node[3];
 #endif
     if (pres) {
-        if (!c.staged) stage_raw(stg, me_l, S, c.k, gnn, live, c.src);
+        if (!c.staged) stage_raw(stg, me_l, S, c.k, gnn, live, c.src, sxzr);
         const double x = stg->q[me_l], z = stg->w[me_l], r = stg->tg[me_l];
 #if !GTF_STAGE_NOINV
         const Cov5 I = inv_cov5(stage_cov(stg, me_l));
@@ -646,7 +658,8 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
         const TauGeo t = tau_geo(x, z, r, za, ra, p.sigma0rz2, p.sigma0rz, p.sigma0rz, p.sigma0rz2, p.endcap_boundary);
         stg->q[me_l] = t.q; stg->w[me_l] = t.w; stg->tg[me_l] = t.tau;
         stg->ec[me_l] = fabs(x) >= p.endcap_boundary;
-        stg->prior[me_l] = st.prior;
+        // the key's prior: as an op of the sequence set it (or it was loaded), else the stored one
+        stg->prior[me_l] = (prior_known || (st.dirty & D_PRIOR)) ? st.prior : S.prior[c.k];
         stg->ord[sb + pos] = (uint8_t)c.grp.gl;
     }
     wave_lds_sync();
@@ -969,8 +982,6 @@ __device__ __forceinline__ bool node_fields(NodeCtx<G>& c, const gtf_graph& g, c
     c.k = c.lo + c.grp.gl;
     c.valid = c.grp.gl < c.d;
     const int k = c.k;
-    c.is_edge = c.valid ? g.is_edge[k] : 0;
-    c.rev_edge = c.valid ? g.rev_edge[k] : 0;
     c.act = c.valid ? e.act[k] : 0;
     c.act0 = c.act;
     // the graph-static classes of the slot (gtf_graph.slot_class) where they cover the group,
@@ -979,7 +990,21 @@ __device__ __forceinline__ bool node_fields(NodeCtx<G>& c, const gtf_graph& g, c
     c.cls = 0;
     c.sfl = 0;
     c.layer = NAN;
-    if (c.use_cls) {
+    // groups of <= 8 lanes: the slot's static fields in one word (gtf_graph.slot_static)
+    const bool st32 = G > 0 && G <= 8 && g.slot_static != nullptr;
+    if (st32) {
+        const uint32_t sw = c.valid ? g.slot_static[k] : 0u;
+        c.is_edge = (sw >> 16) & 1u;
+        c.rev_edge = (sw >> 17) & 1u;
+        c.sfl = (sw >> 18) & 1u;
+        c.cls = (uint64_t)(sw & 0xffu) | ((uint64_t)((sw >> 8) & 0xffu) << 32);
+        c.use_cls = true;
+    } else {
+        c.is_edge = c.valid ? g.is_edge[k] : 0;
+        c.rev_edge = c.valid ? g.rev_edge[k] : 0;
+    }
+    if (st32) {
+    } else if (c.use_cls) {
         if (c.valid) {
             c.cls = g.slot_class[k];
             c.sfl = g.slot_sflags[k];
@@ -990,7 +1015,9 @@ __device__ __forceinline__ bool node_fields(NodeCtx<G>& c, const gtf_graph& g, c
         const int src = c.valid ? g.slot_src[k] : -1;
         c.layer = src >= 0 ? g.layer[src] : NAN;
     }
-    c.src = (nd.src && c.valid) ? g.slot_src[k] : -1;
+    // the sender index: the clustering's coordinate gather of a live entry, not needed with
+    // the slots' own copy (gtf_graph.slot_sxzr)
+    c.src = (nd.src && c.valid && !g.slot_sxzr) ? g.slot_src[k] : -1;
     c.live = false;
     c.left = false;
     c.same_layer = 0;
@@ -1006,7 +1033,7 @@ __device__ __forceinline__ bool node_fields(NodeCtx<G>& c, const gtf_graph& g, c
 #if GTF_HOIST
     // the node's own scalars, in the same round of loads as the slot fields (loaded inside
     // an op, after its LDS fences, each one's latency would add to every wave's life)
-    if (nd.node_xyzr) {
+    if (nd.node_xyzr && c.d >= 3) {   // (read by the clustering only: >= 3 keys, clustering.py:207)
         const double* xn = g.xyzr + 4 * (int64_t)c.v;
         c.xa = xn[0]; c.za = xn[2]; c.ra = xn[3];
     }
@@ -1080,7 +1107,7 @@ template <int G, int OP, typename Stage>
 __device__ __forceinline__ void node_op(NodeCtx<G>& c, const gtf_graph& g, gtf_nodes& n, gtf_states& tse,
                                         gtf_states& uts, gtf_edges& e, const gtf_params& p, const Ws& w,
                                         double* sval, Stage* stg, double chi2_thr, double kl_thr, bool has_tse,
-                                        bool has_uts) {
+                                        bool has_uts, const Need& nd) {
 #if GTF_ASM_MARK
     asm volatile("; GTF_OP_MARK G=%0 OP=%1" ::"i"(G), "i"(OP));
 #endif
@@ -1101,12 +1128,34 @@ __device__ __forceinline__ void node_op(NodeCtx<G>& c, const gtf_graph& g, gtf_n
 #endif
     if constexpr (OP == OP_CLUSTER_TSE) {
         if (has_tse)
-            g_cluster(c, n, tse, c.tse, stg, g.xyzr + 4 * (int64_t)c.v, g.gnn, false, chi2_thr, kl_thr, p, w.err);
+            g_cluster(c, n, tse, c.tse, stg, g.xyzr + 4 * (int64_t)c.v, g.gnn, false, chi2_thr, kl_thr, p, w.err,
+                      g.slot_sxzr, nd.tse_prior);
     }
     if constexpr (OP == OP_CLUSTER_UTS) {
         if (has_uts)
-            g_cluster(c, n, uts, c.uts, stg, g.xyzr + 4 * (int64_t)c.v, g.gnn, c.live, chi2_thr, kl_thr, p, w.err);
+            g_cluster(c, n, uts, c.uts, stg, g.xyzr + 4 * (int64_t)c.v, g.gnn, c.live, chi2_thr, kl_thr, p, w.err,
+                      g.slot_sxzr, nd.uts_prior);
     }
+}
+
+// true when every OP_REWEIGHT_UTS of the sequence follows an OP_PRIORS_UTS with no op between
+// them that adds keys (OP_RANKS / OP_FRESH): the reweight then reads only priors the sequence
+// itself set (every active key's, helper.py:30-63), and the stored UTS priors need not be
+// loaded up front -- the clustering reads a key's stored prior where no op set it
+#ifndef GTF_LAZY_PRIOR
+#define GTF_LAZY_PRIOR 1   // 0 (A/B): the UTS priors loaded up front whenever a reweight runs
+#endif
+template <int... OPS>
+constexpr bool priors_before_reweights() {
+    if (!GTF_LAZY_PRIOR) return false;
+    constexpr int ops[] = {OPS..., -1};
+    bool fresh_priors = false;
+    for (int i = 0; ops[i] >= 0; i++) {
+        if (ops[i] == OP_PRIORS_UTS) fresh_priors = true;
+        if (ops[i] == OP_RANKS || ops[i] == OP_FRESH) fresh_priors = false;
+        if (ops[i] == OP_REWEIGHT_UTS && !fresh_priors) return false;
+    }
+    return true;
 }
 
 template <int... OPS>
@@ -1120,8 +1169,8 @@ struct OpSeq {
     static constexpr bool fresh = ((OPS == OP_FRESH) || ...);
     static constexpr bool cluster_uts = ((OPS == OP_CLUSTER_UTS) || ...);
     static constexpr Need need{uses_tse, ((OPS == OP_CLUSTER_TSE) || ...), uses_uts, reweight,
-                               reweight || cluster_uts, reweight, reweight || cluster_uts,
-                               ((OPS == OP_RANKS) || ...) || fresh, fresh,
+                               reweight && !priors_before_reweights<OPS...>(), reweight, reweight || cluster_uts,
+                               ((OPS == OP_RANKS) || ...) || fresh, fresh && !GTF_MW_IN_EXTRAP,
                                cluster_uts, cluster, ((OPS == OP_MW_TSE || OPS == OP_MW_UTS) || ...)};
 };
 
@@ -1154,8 +1203,8 @@ template <int G, int OP, typename Stage>
 __device__ __forceinline__ void node_op_timed(NodeCtx<G>& c, const gtf_graph& g, gtf_nodes& n, gtf_states& tse,
                                               gtf_states& uts, gtf_edges& e, const gtf_params& p, const Ws& w, double* sval,
                                               Stage* stg, double chi2_thr, double kl_thr, bool has_tse, bool has_uts,
-                                              uint64_t* tb, int& ti) {
-    node_op<G, OP, Stage>(c, g, n, tse, uts, e, p, w, sval, stg, chi2_thr, kl_thr, has_tse, has_uts);
+                                              const Need& nd, uint64_t* tb, int& ti) {
+    node_op<G, OP, Stage>(c, g, n, tse, uts, e, p, w, sval, stg, chi2_thr, kl_thr, has_tse, has_uts, nd);
     const uint64_t t = __builtin_readcyclecounter();
     if (tb && ti < 20) tb[ti] = t;
     ti++;
@@ -1200,7 +1249,7 @@ __device__ __forceinline__ void node_seq_body(const gtf_graph& g, gtf_nodes& n, 
         const bool maybe = c.valid;
 #endif
         if (c.staged && maybe)
-            stage_raw(stg, c.grp.gl, Q::cluster_uts ? uts : tse, c.k, g.gnn, Q::cluster_uts && c.live, c.src);
+            stage_raw(stg, c.grp.gl, Q::cluster_uts ? uts : tse, c.k, g.gnn, Q::cluster_uts && c.live, c.src, g.slot_sxzr);
     }
 #endif
     const bool has_tse = n.has_tse[c.v];
@@ -1209,10 +1258,11 @@ __device__ __forceinline__ void node_seq_body(const gtf_graph& g, gtf_nodes& n, 
     // diagnostics build: the node's loads and stores only (every field marked dirty)
     if (has_tse || has_uts) { c.uts.dirty = c.tse.dirty = D_RANK | D_MW | D_PRIOR; c.uts_dirty_lr = true; c.edge_mw_dirty = true; }
 #elif GTF_OP_TIMING
-    (node_op_timed<G, OPS, Stage>(c, g, n, tse, uts, e, p, w, sval, stg, chi2_thr, kl_thr, has_tse, has_uts, tb, ti),
+    (node_op_timed<G, OPS, Stage>(c, g, n, tse, uts, e, p, w, sval, stg, chi2_thr, kl_thr, has_tse, has_uts, Q::need,
+                                  tb, ti),
      ...);
 #else
-    (node_op<G, OPS, Stage>(c, g, n, tse, uts, e, p, w, sval, stg, chi2_thr, kl_thr, has_tse, has_uts), ...);
+    (node_op<G, OPS, Stage>(c, g, n, tse, uts, e, p, w, sval, stg, chi2_thr, kl_thr, has_tse, has_uts, Q::need), ...);
 #endif
 #if GTF_ASM_MARK
     asm volatile("; GTF_OP_MARK G=%0 OP=99" ::"i"(G));
@@ -1404,7 +1454,7 @@ __global__ void __launch_bounds__(NBLOCK) k_node_pack(gtf_graph g, gtf_nodes n, 
     Stage* stg = (Stage*)(smem + NBLOCK * sizeof(double)) + (Q::cluster ? (int)threadIdx.x / 64 : 0);
     const bool has_tse = n.has_tse[c.v];
     const bool has_uts = fresh_has_uts(c, n, Q::fresh);
-    (node_op<0, OPS, Stage>(c, g, n, tse, uts, e, p, w, sval, stg, chi2_thr, kl_thr, has_tse, has_uts), ...);
+    (node_op<0, OPS, Stage>(c, g, n, tse, uts, e, p, w, sval, stg, chi2_thr, kl_thr, has_tse, has_uts, Q::need), ...);
     node_store(c, n, tse, uts, e);
 }
 
@@ -1432,7 +1482,7 @@ __global__ void __launch_bounds__(NBLOCK) k_node_group(gtf_graph g, gtf_nodes n,
     for (int i = 0; i < ops.n; i++) {
         switch (ops.op[i]) {
 #define GTF_CASE(OPC) \
-    case OPC: node_op<G, OPC, Stage>(c, g, n, tse, uts, e, p, w, sval, stg, chi2_thr, kl_thr, has_tse, has_uts); break;
+    case OPC: node_op<G, OPC, Stage>(c, g, n, tse, uts, e, p, w, sval, stg, chi2_thr, kl_thr, has_tse, has_uts, nd); break;
             GTF_CASE(OP_FRESH)
             GTF_CASE(OP_RANKS)
             GTF_CASE(OP_PRIORS_TSE)

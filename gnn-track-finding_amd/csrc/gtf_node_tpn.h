@@ -135,7 +135,8 @@ __device__ __forceinline__ void t_reweight(TCtx<D>& c, const gtf_graph& g, const
             for (int j = 0; j < D; j++) {
                 const int64_t k = c.lo + j;
                 x0[j] = !tbit(c.valid, j) ? 0.0
-                        : (tbit(c.live, j) ? g.gnn[4 * (int64_t)g.slot_src[k]] : uts.xyzr[4 * k]);
+                        : (tbit(c.live, j) ? (g.slot_sxzr ? g.slot_sxzr[3 * k] : g.gnn[4 * (int64_t)g.slot_src[k]])
+                                           : uts.xyzr[4 * k]);
                 c.left |= (tbit(c.valid, j) && x0[j] < xr) ? (1u << j) : 0u;
             }
             c.sxm = 0;
@@ -204,9 +205,11 @@ __device__ __forceinline__ void t_fresh(TCtx<D>& c) {
 #pragma unroll
     for (int j = 0; j < D; j++)
         if (tbit(c.valid & c.fresh, j)) {
-            c.mwu[j] = c.smw[j];
+            if (!GTF_MW_IN_EXTRAP) {   // (else k_extrapolate stored it)
+                c.mwu[j] = c.smw[j];
+                c.du_mw |= 1u << j;
+            }
             c.pru[j] = NAN;
-            c.du_mw |= 1u << j;
             c.du_prior |= 1u << j;
             c.lri[j] = -1;   // lr = NaN
             c.side[j] = -1;
@@ -334,6 +337,14 @@ __device__ __forceinline__ void tpn_body(const gtf_graph& g, gtf_nodes& n, gtf_s
     using Q = OpSeq<OPS...>;
     constexpr Need nd = Q::need;
     const int gi = bid * NBLOCK + (int)threadIdx.x;
+#if GTF_OP_TIMING
+    // (diagnostics) the group kernels' per-wave stamps, word 23 = 1 for a thread-per-node wave
+    const uint64_t t_start = __builtin_readcyclecounter();
+    const uint64_t rt_start = __builtin_amdgcn_s_memrealtime();
+    const int wave = (int)((blockIdx.x * NBLOCK + threadIdx.x) / 64);
+    uint64_t* tb = ((threadIdx.x & 63) == 0 && wave < GTF_OP_TIMING_WAVES) ? g_op_time + 24 * (int64_t)wave : nullptr;
+    int ti = 2;
+#endif
     if (gi >= count) return;
     TCtx<D> c;
     c.v = list[gi];
@@ -347,6 +358,8 @@ __device__ __forceinline__ void tpn_body(const gtf_graph& g, gtf_nodes& n, gtf_s
     }
     c.valid = c.d >= D ? (1u << D) - 1u : (1u << c.d) - 1u;
     c.use_cls = g.slot_class != nullptr;
+    const bool st32 = D <= 8 && g.slot_static != nullptr;   // the static fields in one word per slot
+    c.use_cls = c.use_cls || st32;
     c.edge = c.rev = c.act = c.fresh = c.live = c.sfl = 0u;
     c.sl_ok = c.sx_ok = false;
     c.left = 0u;
@@ -365,10 +378,19 @@ __device__ __forceinline__ void tpn_body(const gtf_graph& g, gtf_nodes& n, gtf_s
         c.lri[j] = 1;
         c.side[j] = -1;
         if (!ok) continue;
-        c.edge |= g.is_edge[k] ? (1u << j) : 0u;
-        c.rev |= g.rev_edge[k] ? (1u << j) : 0u;
         c.act |= e.act[k] == 1 ? (1u << j) : 0u;
-        if (c.use_cls) {
+        if (st32) {
+            const uint32_t sw = g.slot_static[k];
+            c.edge |= ((sw >> 16) & 1u) << j;
+            c.rev |= ((sw >> 17) & 1u) << j;
+            c.sfl |= ((sw >> 18) & 1u) << j;
+            c.cls[j] = (uint64_t)(sw & 0xffu) | ((uint64_t)((sw >> 8) & 0xffu) << 32);
+        } else {
+            c.edge |= g.is_edge[k] ? (1u << j) : 0u;
+            c.rev |= g.rev_edge[k] ? (1u << j) : 0u;
+        }
+        if (st32) {
+        } else if (c.use_cls) {
             c.cls[j] = g.slot_class[k];
             c.sfl |= (g.slot_sflags[k] & 1) ? (1u << j) : 0u;
         } else if (g.slot_layer) {
@@ -399,6 +421,29 @@ __device__ __forceinline__ void tpn_body(const gtf_graph& g, gtf_nodes& n, gtf_s
         has_uts = true;
         n.has_uts[c.v] = 1;
     }
+#if GTF_OP_TIMING
+    {
+        const uint64_t t = __builtin_readcyclecounter();
+        if (tb) { tb[0] = t_start; tb[1] = t; tb[20] = rt_start; tb[23] = 1; }
+    }
+    (
+        [&] {
+            t_op<D, OPS>(c, g, n, tse, uts, e, p, w, has_tse, has_uts);
+            const uint64_t t = __builtin_readcyclecounter();
+            if (tb && ti < 20) tb[ti] = t;
+            ti++;
+        }(),
+        ...);
+#else
     (t_op<D, OPS>(c, g, n, tse, uts, e, p, w, has_tse, has_uts), ...);
+#endif
     t_store(c, n, tse, uts, e, false);
+#if GTF_OP_TIMING
+    {
+        const uint64_t t = __builtin_readcyclecounter();
+        const uint64_t rt = __builtin_amdgcn_s_memrealtime();
+        if (tb && ti < 20) tb[ti] = t;
+        if (tb) tb[21] = rt;
+    }
+#endif
 }

@@ -83,6 +83,13 @@ __device__ __forceinline__ double xdiv(double x, double d, double r) {
     return qdiv(x, d, r);
 }
 
+// a fresh UTS entry's mixture weight (extrapolate_merged_states.py:384): stored by the
+// extrapolation, which loads the sender's TSE weight anyway (1), or set by the node kernel's
+// OP_FRESH from its own load of send_mw (0, the round-5 form)
+#ifndef GTF_MW_IN_EXTRAP
+#define GTF_MW_IN_EXTRAP 1
+#endif
+
 // ---------------------------------------------------------------------------
 // var_ms: Highland multiple scattering term (extrapolate_merged_states.py:114-124)
 // ---------------------------------------------------------------------------
@@ -546,14 +553,18 @@ __device__ __forceinline__ void extrap_math(const gtf_graph& g, gtf_states& uts,
     vt = fma(J3 * (sigma_rn * sigma_rn), J3, vt);
 
     if (isnan(smw)) raise_node(w.err, v, GTF_ERR_SEND_MW_MISSING);
+#if GTF_MW_IN_EXTRAP
+    uts.mw[k] = smw;   // mixture_weight = the sender's TSE weight for this receiver (:384)
+#endif
     uts.sv[3 * (int64_t)k + 0] = xu0;
     uts.sv[3 * (int64_t)k + 1] = xu1;
     uts.sv[3 * (int64_t)k + 2] = xu2;
     uts.tau[k] = tau;
     store_cov5(uts.cov, k, Cov5{P00, P01, P10, P11, vt + var_ms});
     uts.lik[k] = lik;
-    // mixture_weight = smw (:384) and the empty prior / lr / side of a fresh entry are set
-    // by the node kernel's OP_FRESH, merged with its own stores of those fields. The entry's
+    // The empty prior / lr / side of a fresh entry are set by the node kernel's OP_FRESH,
+    // merged with its own stores of those fields (its mixture weight is stored here: this
+    // kernel loads send_mw anyway, and the node kernel then reads no send_mw of its own). The entry's
     // 'xyzr' (:377) is the sender's GNN coordinates, which stay resident in g.gnn: bit 1
     // marks it live instead of writing a 32-byte copy per accepted edge (gtf_uts_materialize
     // writes it when it is read back or before g.gnn changes)
@@ -795,7 +806,7 @@ __device__ void node_fresh(gtf_nodes& n, gtf_states& uts, const gtf_edges& e, Se
     for (int k = s.lo; k < s.hi; k++)
         if (uts.fresh[k] & 1) {
             n.has_uts[v] = 1;
-            uts.mw[k] = e.send_mw[k];
+            if (!GTF_MW_IN_EXTRAP) uts.mw[k] = e.send_mw[k];
             uts.prior[k] = NAN;
             uts.lr[k] = NAN;
             uts.side[k] = -1;

@@ -16,7 +16,7 @@ F64 = ctypes.c_double
 
 
 U32 = ctypes.c_uint32
-ABI_VERSION = 6   # GTF_ABI_VERSION of include/gtf.h
+ABI_VERSION = 7   # GTF_ABI_VERSION of include/gtf.h
 
 
 class GtfGraph(ctypes.Structure):
@@ -31,7 +31,8 @@ class GtfGraph(ctypes.Structure):
                 ("out_sched", P), ("n_o4", I32), ("n_o8", I32), ("n_o16", I32), ("n_g2", I32),
                 ("pack_ent", P), ("pack_wave", P), ("n_pack_waves", I32), ("out_lanes", P),
                 ("pad_tiles", I32), ("pad_tile_nodes", I32), ("pad_tile_slots", I32), ("pad_count", I32 * 6),
-                ("pad_reserved_", I32), ("slot_outidx", P), ("slot_class", P), ("slot_sflags", P)]
+                ("pad_reserved_", I32), ("slot_outidx", P), ("slot_class", P), ("slot_sflags", P),
+                ("slot_sxzr", P), ("slot_static", P)]
 
     def __init__(self, **fields):
         super().__init__(**fields)

@@ -134,6 +134,35 @@ def slot_classes(g: TrackGraph):
     return cls, sfl
 
 
+STATIC_MAX = 8   # segments of up to this many slots get gtf_graph.slot_static words
+
+
+def slot_static_words(g: TrackGraph, cls: np.ndarray, sfl: np.ndarray) -> np.ndarray:
+    """gtf_graph.slot_static (ABI v7): for a slot of a segment of d <= 8 slots, its class bits
+    (same layer: bits 0..7, same x: bits 8..15), is_edge (16), rev_edge (17) and side flag
+    (18) in one uint32; 0 for larger segments"""
+    deg = np.diff(g.slot_ptr.astype(np.int64))
+    small = np.repeat(deg <= STATIC_MAX, deg)
+    c = cls.astype(np.uint64)
+    w = (c & np.uint64(0xff)) | (((c >> np.uint64(32)) & np.uint64(0xff)) << np.uint64(8))
+    w = w.astype(np.uint32)
+    w |= (g.slot["is_edge"].astype(np.uint32) & 1) << 16
+    w |= (g.slot["rev_edge"].astype(np.uint32) & 1) << 17
+    w |= (sfl.astype(np.uint32) & 1) << 18
+    return np.where(small, w, np.uint32(0)).astype(np.uint32)
+
+
+def slot_sender_xzr(g: TrackGraph) -> np.ndarray:
+    """gtf_graph.slot_sxzr (ABI v7): per slot its sender's GNN_Measurement x, z, r
+    (gnn[slot_src][0, 2, 3]), NaN rows for orphan keys; [S, 3] float64"""
+    src = g.slot["slot_src"].astype(np.int64)
+    out = np.full((g.n_slots, 3), np.nan)
+    ok = src >= 0
+    if g.n_nodes and ok.any():
+        out[ok] = g.node["gnn"][src[ok]][:, [0, 2, 3]]
+    return out
+
+
 def live_coordinates(g: TrackGraph) -> np.ndarray:
     """gtf_states.fresh bit 1 for an uploaded graph: the updated_track_states entries whose
     stored 'xyzr' is bit for bit their sender's current GNN_Measurement coordinates (what
@@ -248,6 +277,17 @@ class DeviceGraph:
             cls, sfl = slot_classes(g)
             up("slot_class", cls.view(np.int64))
             up("slot_sflags", sfl)
+        # the senders' GNN x, z, r per slot (gtf_graph.slot_sxzr): a live UTS entry's stored
+        # coordinates, read contiguously by the clustering instead of gathered per state
+        # (GTF_NO_SXZR=1: gathered, for A/B)
+        self.use_sxzr = self.use_classes and os.environ.get("GTF_NO_SXZR", "0") != "1"
+        if self.use_sxzr:
+            up("slot_sxzr", slot_sender_xzr(g))
+        # the static slot fields of <= 8-slot segments in one word (gtf_graph.slot_static;
+        # GTF_NO_STATIC32=1: the separate arrays, for A/B)
+        self.use_static32 = self.use_classes and os.environ.get("GTF_NO_STATIC32", "0") != "1"
+        if self.use_static32:
+            up("slot_static", slot_static_words(g, cls, sfl).view(np.int32))
         sub = g.node["sub_id"].astype(np.int64)
         if g.n_nodes:
             sizes = np.bincount(sub - sub.min())
@@ -353,7 +393,9 @@ class DeviceGraph:
                     out_dst=p("out_dst"), slot_layer=p("slot_layer"),
                     slot_outidx=p("slot_outidx") if self.use_outidx else ctypes.c_void_p(0),
                     slot_class=p("slot_class") if self.use_classes else ctypes.c_void_p(0),
-                    slot_sflags=p("slot_sflags") if self.use_classes else ctypes.c_void_p(0))
+                    slot_sflags=p("slot_sflags") if self.use_classes else ctypes.c_void_p(0),
+                    slot_sxzr=p("slot_sxzr") if self.use_sxzr else ctypes.c_void_p(0),
+                    slot_static=p("slot_static") if self.use_static32 else ctypes.c_void_p(0))
         # with the node schedule (lane groups) and the sender schedule
         sched = dict(n_big=self.n_big, sched=p("sched"), n_g4=self.n_g_all[0], n_g8=self.n_g_all[1],
                      n_g16=self.n_g_all[2], n_g32=self.n_g_all[3], n_g64=self.n_g_all[4], sched_seg=p("sched_seg"),

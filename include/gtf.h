@@ -46,7 +46,7 @@ typedef void* gtf_stream_t; /* a hipStream_t */
 /* Version of the struct layouts below. gtf_graph carries it with its own size, and every
  * entry point taking a gtf_graph refuses a caller built against another layout
  * (status -3, gtf_last_error() names both). Bumped on every layout change. */
-#define GTF_ABI_VERSION 6u
+#define GTF_ABI_VERSION 7u
 
 /* ---- graph structure (read-only on the path) ------------------------------ */
 typedef struct gtf_graph {
@@ -143,6 +143,20 @@ typedef struct gtf_graph {
     /* optional (v5, with slot_class): bit 0 = the sender's GNN x < the receiver's GNN x (the
      * side of a live entry, helper.py:116-121). [S], or NULL. */
     const uint8_t* slot_sflags;
+    /* optional (v7): the GNN_Measurement x, z, r of each slot's sender (gnn[4 slot_src + 0, 2, 3],
+     * NaN for an orphan key), graph-static like slot_class. The coordinates of a live UTS entry
+     * (gtf_states.fresh bit 1, extrapolate_merged_states.py:377) are its sender's GNN ones; the
+     * node kernel's clustering stage (the tau geometry of the pairwise chi2, clustering.py:
+     * 49-57) and the side norm read them here, contiguously per slot, instead of gathering the
+     * sender's 32-byte gnn row per state. A caller that changes g->gnn refreshes it (or passes
+     * NULL: the kernel then gathers gnn). [S*3], or NULL. */
+    const double* slot_sxzr;
+    /* optional (v7): one 32-bit word per slot of a receiver segment of d <= 8 slots, read by the
+     * node kernel's lane groups of <= 8 lanes in place of four loads: bits 0..7 = slot_class bits
+     * 0..7 (the same-layer positions), bits 8..15 = slot_class bits 32..39 (the same-x
+     * positions), bit 16 = is_edge, bit 17 = rev_edge, bit 18 = slot_sflags bit 0; 0 for larger
+     * segments. Graph-static, built with slot_class. [S], or NULL. */
+    const uint32_t* slot_static;
 } gtf_graph;
 
 /* ---- per-node mutable state ------------------------------------------------ */

@@ -31,7 +31,7 @@ W = 65536
 L = nat.lib()
 L.gtf_op_timing.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32]
 L.gtf_op_timing.restype = ctypes.c_int
-g = synth.workload("c4", seed=0)
+g = synth.workload(os.environ.get("GTF_OPT_WL", "c4"), seed=0)
 d = DeviceGraph(g, "cuda:0", layout="tiled")
 snap = d.snapshot(DeviceGraph.PASS_INPUTS)
 p = Params()

@@ -195,6 +195,7 @@ struct NodeCtx {
     uint8_t is_edge, rev_edge, act, act0;
     double layer;                   // sender layer (without the static classes)
     uint64_t cls;                   // gtf_graph.slot_class of the slot (0 without)
+    uint64_t xcls;                  // G = 64: gtf_graph.slot_xclass of the slot (its same-x positions)
     uint8_t sfl;                    // gtf_graph.slot_sflags of the slot
     bool use_cls;                   // the static classes cover this group (group-uniform)
     bool live;                      // UTS entry's xyzr = gnn[slot_src] (gtf_states.fresh bit 1)
@@ -332,9 +333,10 @@ __device__ __forceinline__ bool lane_active(const NodeCtx<G>& c, int rank) {
 // iteration per distinct layer value (leader election with a ballot).
 template <int G>
 __device__ __forceinline__ void g_priors(NodeCtx<G>& c, LaneDict& st, double* sval) {
-    if constexpr (G > 0 && G <= 32) {
+    if constexpr (G > 0 && G <= 64) {
         if (!c.same_layer_ok && c.use_cls) {   // the graph-static classes (gtf_graph.slot_class)
-            c.same_layer = c.valid ? (c.cls & 0xffffffffull) : 0ull;
+            // (33..64-slot segments: all 64 bits of slot_class are the same-layer positions)
+            c.same_layer = c.valid ? (G == 64 ? c.cls : (c.cls & 0xffffffffull)) : 0ull;
             c.same_layer_ok = true;
         }
     }
@@ -400,9 +402,9 @@ __device__ __forceinline__ void g_reweight(NodeCtx<G>& c, double* sval, const gt
     // present key's x is its sender's live GNN x (the entries message passing wrote), the
     // classes and sides are graph-static (gtf_graph.slot_class / slot_sflags); the present
     // keys only shrink after this point (pruning), so they stay valid for the pass.
-    if constexpr (G > 0 && G <= 32) {
+    if constexpr (G > 0 && G <= 64) {
         if (!c.same_x_ok && c.use_cls && !c.grp.any(c.valid && st.rank >= 0 && !c.live)) {
-            c.same_x = c.valid ? (c.cls >> 32) : 0ull;
+            c.same_x = c.valid ? (G == 64 ? c.xcls : (c.cls >> 32)) : 0ull;
             c.left = (c.sfl & 1) != 0;
             c.same_x_ok = true;
         }
@@ -986,8 +988,9 @@ __device__ __forceinline__ bool node_fields(NodeCtx<G>& c, const gtf_graph& g, c
     c.act0 = c.act;
     // the graph-static classes of the slot (gtf_graph.slot_class) where they cover the group,
     // else the sender layer the priors build them from
-    c.use_cls = G > 0 && G <= 32 && g.slot_class != nullptr;
+    c.use_cls = G > 0 && ((G <= 32 && g.slot_class != nullptr) || (G == 64 && g.slot_xclass != nullptr));
     c.cls = 0;
+    c.xcls = 0;
     c.sfl = 0;
     c.layer = NAN;
     // groups of <= 8 lanes: the slot's static fields in one word (gtf_graph.slot_static)
@@ -1008,6 +1011,7 @@ __device__ __forceinline__ bool node_fields(NodeCtx<G>& c, const gtf_graph& g, c
         if (c.valid) {
             c.cls = g.slot_class[k];
             c.sfl = g.slot_sflags[k];
+            if (G == 64) c.xcls = g.slot_xclass[k];
         }
     } else if (g.slot_layer) {
         c.layer = c.valid ? g.slot_layer[k] : NAN;

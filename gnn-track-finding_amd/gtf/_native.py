@@ -32,7 +32,7 @@ class GtfGraph(ctypes.Structure):
                 ("pack_ent", P), ("pack_wave", P), ("n_pack_waves", I32), ("out_lanes", P),
                 ("pad_tiles", I32), ("pad_tile_nodes", I32), ("pad_tile_slots", I32), ("pad_count", I32 * 6),
                 ("pad_reserved_", I32), ("slot_outidx", P), ("slot_class", P), ("slot_sflags", P),
-                ("slot_sxzr", P), ("slot_static", P)]
+                ("slot_sxzr", P), ("slot_static", P), ("slot_xclass", P)]
 
     def __init__(self, **fields):
         super().__init__(**fields)

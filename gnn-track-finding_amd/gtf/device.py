@@ -92,17 +92,20 @@ def pack_schedule(slot_ptr):
 
 
 CLASS_MAX = 32   # segments of up to this many slots get graph-static classes (gtf_graph.slot_class)
+XCLASS_MAX = 64  # 33..64-slot segments: the layer classes in slot_class, the x ones in slot_xclass (ABI v7)
 CLASS_MIN_SLOTS = 1 << 16   # graphs this large get them by default (the host pass: ~4 ms on 15k slots)
 
 
 def slot_classes(g: TrackGraph):
-    """gtf_graph.slot_class / slot_sflags (ABI v5): for every slot of a receiver segment of
+    """gtf_graph.slot_class / slot_sflags (ABI v5) / slot_xclass (v7): for every slot of a receiver segment of
     d <= 32 slots, bits 0..31 = the segment positions whose sender has this slot's sender
     layer (compute_prior_probabilities' groups, helper.py:30-63), bits 32..63 = the positions
     whose sender's GNN x equals this slot's sender's (the side norm's distinct-x classes,
     helper.py:111-139, for entries holding their sender's live coordinates); a NaN (orphan
     key) equals only itself. sflags bit 0 = sender GNN x < receiver GNN x (the side,
-    helper.py:116-121). Larger segments get 0 (the kernel builds their classes)."""
+    helper.py:116-121). Segments of 33..64 slots (v7): all 64 bits of slot_class are the
+    layer positions and slot_xclass holds the x positions. Larger segments get 0 (the kernel
+    builds their classes)."""
     S = g.n_slots
     cls = np.zeros(S, np.uint64)
     src = g.slot["slot_src"].astype(np.int64)
@@ -117,21 +120,25 @@ def slot_classes(g: TrackGraph):
         sfl = (sx < rx).astype(np.uint8)
     sp = g.slot_ptr.astype(np.int64)
     deg = np.diff(sp)
-    for d in range(1, CLASS_MAX + 1):
+    xcls = np.zeros(S, np.uint64)
+    for d in range(1, XCLASS_MAX + 1):
         v = np.nonzero(deg == d)[0]
         if v.size == 0:
             continue
         idx = sp[v][:, None] + np.arange(d)[None, :]                 # [n, d] slots
         own = np.eye(d, dtype=bool)[None, :, :]
         bits = (np.uint64(1) << np.arange(d, dtype=np.uint64))[None, None, :]
-        word = np.zeros((v.size, d), np.uint64)
-        for shift, val in ((0, layer), (32, sx)):
+        masks = []
+        for val in (layer, sx):
             a = val[idx]
             eq = (a[:, :, None] == a[:, None, :]) | own              # [n, i, j]
-            m = np.bitwise_or.reduce(np.where(eq, bits, np.uint64(0)), axis=2)
-            word |= m << np.uint64(shift)
-        cls[idx.reshape(-1)] = word.reshape(-1)
-    return cls, sfl
+            masks.append(np.bitwise_or.reduce(np.where(eq, bits, np.uint64(0)), axis=2))
+        if d <= CLASS_MAX:   # both in one word
+            cls[idx.reshape(-1)] = (masks[0] | (masks[1] << np.uint64(32))).reshape(-1)
+        else:                # 33..64 slots: the layer positions in slot_class, the x ones in slot_xclass
+            cls[idx.reshape(-1)] = masks[0].reshape(-1)
+            xcls[idx.reshape(-1)] = masks[1].reshape(-1)
+    return cls, sfl, xcls
 
 
 STATIC_MAX = 8   # segments of up to this many slots get gtf_graph.slot_static words
@@ -274,9 +281,10 @@ class DeviceGraph:
             oidx[g.out_slot] = np.arange(g.n_edges, dtype=np.int32)
         up("slot_outidx", oidx)
         if self.use_classes:
-            cls, sfl = slot_classes(g)
+            cls, sfl, xcls = slot_classes(g)
             up("slot_class", cls.view(np.int64))
             up("slot_sflags", sfl)
+            up("slot_xclass", xcls.view(np.int64))
         # the senders' GNN x, z, r per slot (gtf_graph.slot_sxzr): a live UTS entry's stored
         # coordinates, read contiguously by the clustering instead of gathered per state
         # (GTF_NO_SXZR=1: gathered, for A/B)
@@ -395,7 +403,8 @@ class DeviceGraph:
                     slot_class=p("slot_class") if self.use_classes else ctypes.c_void_p(0),
                     slot_sflags=p("slot_sflags") if self.use_classes else ctypes.c_void_p(0),
                     slot_sxzr=p("slot_sxzr") if self.use_sxzr else ctypes.c_void_p(0),
-                    slot_static=p("slot_static") if self.use_static32 else ctypes.c_void_p(0))
+                    slot_static=p("slot_static") if self.use_static32 else ctypes.c_void_p(0),
+                    slot_xclass=p("slot_xclass") if self.use_classes else ctypes.c_void_p(0))
         # with the node schedule (lane groups) and the sender schedule
         sched = dict(n_big=self.n_big, sched=p("sched"), n_g4=self.n_g_all[0], n_g8=self.n_g_all[1],
                      n_g16=self.n_g_all[2], n_g32=self.n_g_all[3], n_g64=self.n_g_all[4], sched_seg=p("sched_seg"),

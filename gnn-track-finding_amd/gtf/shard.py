@@ -329,7 +329,8 @@ class ShardedDeviceGraph:
                                slot_class=p("slot_class") if d.use_classes else ctypes.c_void_p(0),
                                slot_sflags=p("slot_sflags") if d.use_classes else ctypes.c_void_p(0),
                                slot_sxzr=p("slot_sxzr") if d.use_sxzr else ctypes.c_void_p(0),
-                               slot_static=p("slot_static") if d.use_static32 else ctypes.c_void_p(0))
+                               slot_static=p("slot_static") if d.use_static32 else ctypes.c_void_p(0),
+                               slot_xclass=p("slot_xclass") if d.use_classes else ctypes.c_void_p(0))
         self.shard = nat.GtfShard(vp(self.senders), int(self.senders.numel()), int(pl.node_lo[rank]),
                                   int(pl.node_hi[rank]), int(pl.slot_lo[rank]), int(pl.slot_hi[rank]))
         # the pass in phases (ShardPlan.split): 1a the interior senders and their slots, 1b the

@@ -137,7 +137,8 @@ typedef struct gtf_graph {
      * probabilities' groups, helper.py:30-63; an orphan or NaN layer: {i}); bits 32..63 = the
      * positions whose sender's GNN_Measurement x equals slot k's sender's (the side norm's
      * distinct-x classes, helper.py:111-139, for entries whose stored x is the sender's live
-     * GNN x -- see gtf_states.fresh); 0 for segments of more than 32 slots. [S], or NULL
+     * GNN x -- see gtf_states.fresh); for a segment of 33..64 slots (v7) all 64 bits are the
+     * same-layer positions and slot_xclass holds the same-x ones; 0 for larger segments. [S], or NULL
      * (the kernel then builds the classes itself). */
     const uint64_t* slot_class;
     /* optional (v5, with slot_class): bit 0 = the sender's GNN x < the receiver's GNN x (the
@@ -157,6 +158,11 @@ typedef struct gtf_graph {
      * positions), bit 16 = is_edge, bit 17 = rev_edge, bit 18 = slot_sflags bit 0; 0 for larger
      * segments. Graph-static, built with slot_class. [S], or NULL. */
     const uint32_t* slot_static;
+    /* optional (v7, with slot_class): the same-x positions of the slots of 33..64-slot segments
+     * (64 bits; slot_class then holds all 64 same-layer bits there), so the 64-lane groups read
+     * their classes too instead of electing leaders per distinct value; 0 elsewhere. [S], or
+     * NULL. */
+    const uint64_t* slot_xclass;
 } gtf_graph;
 
 /* ---- per-node mutable state ------------------------------------------------ */

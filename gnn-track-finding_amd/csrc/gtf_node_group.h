@@ -1331,22 +1331,6 @@ __device__ __forceinline__ void node_bucket(int q, int b, char* smem) {
                              A->bk.count[q], b, smem, *(const Arith*)&A->bk.ar[q]);
 }
 
-#include "gtf_node_tpn.h"
-// the <= 2-slot bucket one thread per node (gtf_node_tpn.h) instead of 2-lane groups
-#ifndef GTF_NODE_TPN
-#define GTF_NODE_TPN 1
-#endif
-template <int... OPS>
-constexpr bool node_tpn2() { return GTF_NODE_TPN && TpnOk<OPS...>::value; }
-
-template <int... OPS>
-__device__ __forceinline__ void node_bucket_tpn2(int b) {
-    const KArgPtr A = node_kargs();
-    tpn_body<2, OPS...>(*(const gtf_graph*)&A->g, *(gtf_nodes*)&A->n, *(gtf_states*)&A->tse, *(gtf_states*)&A->uts,
-                        *(gtf_edges*)&A->e, *(const gtf_params*)&A->p, *(const Ws*)&A->w, A->bk.list[5],
-                        A->bk.seg[5], A->bk.count[5], b);
-}
-
 // one launch over every bucket: blocks of the long-running buckets (many slots per node)
 // are dealt first so they overlap the bulk of small nodes instead of trailing it
 #ifndef GTF_NODE_WAVES
@@ -1407,10 +1391,7 @@ __global__ void __launch_bounds__(NBLOCK) GTF_NODE_WAVES_ATTR k_node_multi(NodeK
 #endif
     if (b < A->bk.blocks[4]) { node_bucket<4, OPS...>(4, b, smem); return; }
     b -= A->bk.blocks[4];
-    if constexpr (node_tpn2<OPS...>())
-        node_bucket_tpn2<OPS...>(b);
-    else
-        node_bucket<2, OPS...>(5, b, smem);
+    node_bucket<2, OPS...>(5, b, smem);
 }
 
 // Packed lane segments (gtf_graph.pack_ent / pack_wave): wavefront wv takes the entries

@@ -87,7 +87,7 @@ __device__ __forceinline__ double xdiv(double x, double d, double r) {
 // extrapolation, which loads the sender's TSE weight anyway (1), or set by the node kernel's
 // OP_FRESH from its own load of send_mw (0, the round-5 form)
 #ifndef GTF_MW_IN_EXTRAP
-#define GTF_MW_IN_EXTRAP 1
+#define GTF_MW_IN_EXTRAP 0   // 1 measured: node kernel -1 us, k_extrapolate +3.5 us on C4 (profiles/r06/v3/)
 #endif
 
 // ---------------------------------------------------------------------------
@@ -1210,9 +1210,7 @@ int launch_seq(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* ut
                     bk.ar[q] = Arith{g->pad_count[j], noff[j], soff[j], g->pad_tile_nodes, g->pad_tile_slots};
                     bk.count[q] = g->pad_tiles * g->pad_count[j];
                 }
-                // (the <= 2-slot bucket one thread per node where the sequence allows it)
-                const int per_block = (q == 5 && node_tpn2<OPS...>()) ? NBLOCK : NBLOCK / gs[q];
-                bk.blocks[q] = (bk.count[q] + per_block - 1) / per_block;
+                bk.blocks[q] = (bk.count[q] + NBLOCK / gs[q] - 1) / (NBLOCK / gs[q]);
                 total += bk.blocks[q];
             }
             if (g->pack_ent && g->pack_wave && g->n_pack_waves > 0)   // every <= 64-slot node, packed

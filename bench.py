@@ -442,13 +442,18 @@ def bench_c5_sharded(dev, steps, warmup, rank, world, backend, n_events=256):
             "collective": "none (events are independent)", "device_error_flags": flags}
 
 
-def bench_tags(d, g, dev, reps=5):
+def bench_tags(d, g, dev, reps=5, descending=False):
     """tag propagation (a16, tag_propagation.py:99-164) on a device graph after a pass: one
     gtf_tag_propagate call (wall), the host-order API, and the prepare / sweep kernels alone
-    (K calls between two events) against SURVEY §8(d)'s B_tag = 4 E + 8 N per sweep"""
+    (K calls between two events) against SURVEY §8(d)'s B_tag = 4 E + 8 N per sweep.
+    Initial tag = node index; descending: N - 1 - index, so a node's inner neighbours (the
+    lower layers come first in the generator's hit order) carry the larger tags and the
+    maximum travels outward layer by layer -- several sweeps instead of one"""
     import torch
     from gtf import roofline as rf
     tags = np.arange(g.n_nodes, dtype=np.int64)
+    if descending:
+        tags = tags[::-1].copy()
     radius = np.ascontiguousarray(g.node["xyzr"][:, 3])
     import ctypes
     vp = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
@@ -498,7 +503,8 @@ def bench_tags(d, g, dev, reps=5):
     sweep_ms = e0.elapsed_time(e1) / K
     sweeps = len(flips)
     nbytes = 4 * g.n_edges + 8 * g.n_nodes   # SURVEY §8d B_tag, per sweep
-    return {"sweeps": sweeps, "flips": [int(x) for x in flips], "stage_wall_ms": dt * 1e3,
+    return {"initial_tags": "N - 1 - node index" if descending else "node index",
+            "sweeps": sweeps, "flips": [int(x) for x in flips], "stage_wall_ms": dt * 1e3,
                                   "stage_wall_host_order_ms": dt_host * 1e3,
                                   "prepare_call_ms": prep_ms, "sweep_call_ms": sweep_ms,
                                   "stage_over_kernels": dt * 1e3 / (prep_ms + sweeps * sweep_ms),
@@ -564,7 +570,7 @@ def bench_c3_section(dev, steps, warmup, params, layout="tiled", tile=4096):
     # a16 on the fused 5.9 M-edge graph after the pass: several sweeps (where C4 stops after one),
     # the sweep kernel at a size where it can be bandwidth-bound
     try:
-        res["a16_tag_propagation"] = bench_tags(d, g, dev, reps=3)
+        res["a16_tag_propagation"] = bench_tags(d, g, dev, reps=3, descending=True)
     except Exception as ex:   # reported; the section stands
         res["a16_tag_propagation"] = {"error": repr(ex)[:300]}
     del d

@@ -537,6 +537,9 @@ __device__ __forceinline__ void g_ranks(NodeCtx<G>& c) {
 // dict position to it: the operands can then be staged before the ops have settled
 // which keys are present and in what order (GTF_EARLY_STAGE).
 template <int CAP>
+#ifndef GTF_MERGE_SHFL
+#define GTF_MERGE_SHFL 0   // 1: the greedy merge takes the chosen key's inverse from its lane (below); measured +1.5 us (3 VGPRs spill), profiles/r06/shfl/
+#endif
 #ifndef GTF_STAGE_NOINV
 #define GTF_STAGE_NOINV 2   // (with GTF_KL_LEAN) 3 = 2x2-block inverses staged after the pair loop (below;
                             // one division per merge instead of three, but 3 VGPRs spill: 3.5 us slower);
@@ -809,11 +812,18 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
             const bool me = pres && (alive >> pos & 1u);
             double D = INFINITY;
             bool dn = false;
+#if GTF_STAGE_NOINV == 2 && GTF_MERGE_SHFL
+            Cov5 ime{0.0, 0.0, 0.0, 0.0, 0.0};   // this lane's state's inverse (the KL's), handed to the merge
+#endif
             if (me) {
                 const double js_me[3] = {stg->a[me_l], stg->b[me_l], stg->tau[me_l]};
                 const double jm[3] = {mm[0], mm[1], mm[3]};
 #if GTF_STAGE_NOINV == 3
                 D = kl_with_inv(js_me, stage_cov(stg, me_l), inv_of(me_l), jm, mc, im);
+#elif GTF_STAGE_NOINV == 2 && GTF_MERGE_SHFL
+                const Cov5 cme = stage_cov(stg, me_l);
+                ime = inv_cov5(cme);
+                D = kl_with_inv(js_me, cme, ime, jm, mc, im);
 #elif GTF_STAGE_NOINV == 2
                 const Cov5 cme = stage_cov(stg, me_l);
                 D = kl_with_inv(js_me, cme, inv_cov5(cme), jm, mc, im);
@@ -831,8 +841,19 @@ __device__ __forceinline__ void g_cluster(NodeCtx<G>& c, gtf_nodes& n, const gtf
             const double mind = c.grp.min_d(D);
             if (!(mind < kl_thr)) break;
             const int m = c.grp.min_i((me && D == mind) ? pos : 99);  // first minimum (list.index)
+#if GTF_STAGE_NOINV == 2 && GTF_MERGE_SHFL
+            // the merged key's inverse from the lane that holds it (it computed that inverse for
+            // its KL term: np.linalg.inv of one covariance is one value), by shuffles, instead of
+            // recomputed from the stage (two divisions on the loop's dependent chain)
+            const unsigned long long wb = c.grp.bits(me && pos == m);
+            const int wl = wb ? __ffsll((long long)wb) - 1 : 0;
+            const int lm = sb + wl;
+            const Cov5 ii{c.grp.shfl(ime.c00, wl), c.grp.shfl(ime.c01, wl), c.grp.shfl(ime.c10, wl),
+                          c.grp.shfl(ime.c11, wl), c.grp.shfl(ime.c22, wl)};
+#else
             const int lm = sb + stg->ord[sb + m];
             const Cov5 ii = inv_of(lm);
+#endif
             const Cov5 nmc = inv_cov5(add_cov5(ii, im));
             const double x[4] = {stg->a[lm], stg->b[lm], stg->c[lm], stg->tau[lm]};
             double nm[4];

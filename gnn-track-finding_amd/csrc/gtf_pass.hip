@@ -556,11 +556,23 @@ __device__ __forceinline__ void extrap_math(const gtf_graph& g, gtf_states& uts,
 #if GTF_MW_IN_EXTRAP
     uts.mw[k] = smw;   // mixture_weight = the sender's TSE weight for this receiver (:384)
 #endif
-    uts.sv[3 * (int64_t)k + 0] = xu0;
-    uts.sv[3 * (int64_t)k + 1] = xu1;
-    uts.sv[3 * (int64_t)k + 2] = xu2;
-    uts.tau[k] = tau;
-    store_cov5(uts.cov, k, Cov5{P00, P01, P10, P11, vt + var_ms});
+#ifndef GTF_DIAG_NOSTORE
+#define GTF_DIAG_NOSTORE 0   // diagnostics builds only (wrong results): 1 no covariance store, 2 no state / tau, 3 neither
+#endif
+    if (!(GTF_DIAG_NOSTORE & 2)) {
+        uts.sv[3 * (int64_t)k + 0] = xu0;
+        uts.sv[3 * (int64_t)k + 1] = xu1;
+        uts.sv[3 * (int64_t)k + 2] = xu2;
+        uts.tau[k] = tau;
+    } else {
+        asm volatile("" ::"v"(xu0), "v"(xu1), "v"(xu2), "v"(tau));
+    }
+    if (!(GTF_DIAG_NOSTORE & 1)) {
+        store_cov5(uts.cov, k, Cov5{P00, P01, P10, P11, vt + var_ms});
+    } else {
+        const double c22 = vt + var_ms;
+        asm volatile("" ::"v"(P00), "v"(P01), "v"(P10), "v"(P11), "v"(c22));
+    }
     uts.lik[k] = lik;
     // The empty prior / lr / side of a fresh entry are set by the node kernel's OP_FRESH,
     // merged with its own stores of those fields (its mixture weight is stored here: this

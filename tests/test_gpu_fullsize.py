@@ -125,3 +125,34 @@ def test_staged_input_copies_equal_the_resident_pass(c4):
     assert torch.equal(d._staged[1][0], d.arena)
     assert torch.equal(d._staged[0][0], snap["__arena__"]) and torch.equal(d._staged[2][0], snap["__arena__"])
     assert not torch.equal(d.arena, snap["__arena__"])
+
+
+@pytest.mark.parametrize("variant", ["no_sxzr", "no_static32", "no_classes"])
+def test_slot_tables_do_not_change_the_pass(c4, variant, monkeypatch):
+    """the graph-static slot tables (gtf_graph.slot_class / slot_xclass / slot_static /
+    slot_sxzr, ABI v5 / v7) only move where the node kernel reads things from: the C4 pass
+    without each of them (the kernel then gathers the senders' coordinates, reads the four
+    static fields, or builds every class itself) equals the default pass bit for bit"""
+    from gtf.device import DeviceGraph
+    p = Params()
+    d = DeviceGraph(c4, layout="tiled")
+    assert d.use_sxzr and d.use_static32 and d.use_classes
+    d.clear_errors()
+    d.full_pass(p)
+    h = d.download(c4.copy())
+    ref = {k: v for k, v in list(h.node.items()) + list(h.slot.items()) if k in _state_keys(c4)}
+    flags = d.errors()
+    if variant == "no_sxzr":
+        monkeypatch.setenv("GTF_NO_SXZR", "1")
+    elif variant == "no_static32":
+        monkeypatch.setenv("GTF_NO_STATIC32", "1")
+    e = DeviceGraph(c4, layout="tiled", classes=(False if variant == "no_classes" else None))
+    assert (e.use_sxzr, e.use_static32, e.use_classes) == {"no_sxzr": (False, True, True),
+                                                           "no_static32": (True, False, True),
+                                                           "no_classes": (False, False, False)}[variant]
+    e.clear_errors()
+    e.full_pass(p)
+    h = e.download(c4.copy())
+    got = {k: v for k, v in list(h.node.items()) + list(h.slot.items()) if k in _state_keys(c4)}
+    assert e.errors() == flags
+    _same(got, ref, variant)

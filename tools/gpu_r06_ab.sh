@@ -26,6 +26,7 @@ for r in $(seq 1 $ROUNDS); do
 done
 fi
 first=1
+[ -n "$NO_TESTS" ] && set --
 for spec in "$@"; do
   name=${spec%%=*}
   if [ $first = 1 ]; then first=0; continue; fi

@@ -1083,10 +1083,23 @@ __device__ __forceinline__ bool node_fields(NodeCtx<G>& c, const gtf_graph& g, c
     return true;
 }
 
+#ifndef GTF_FULL_STORES
+#define GTF_FULL_STORES 0   // 1 (A/B): the loaded fields (activation, ranks, UTS weight) stored for every valid slot, so a
+                            // wave's stores cover whole lines instead of the dirty slots only
+#endif
 template <int G>
 __device__ __forceinline__ void node_store(NodeCtx<G>& c, gtf_nodes& n, gtf_states& tse, gtf_states& uts,
-                                           gtf_edges& e) {
+                                           gtf_edges& e, const Need& nd) {
     const int k = c.k;
+    if (GTF_FULL_STORES && c.valid) {
+        e.act[k] = c.act;
+        if (nd.tse_rank) tse.rank[k] = c.tse.rank;
+        if (nd.uts_rank) uts.rank[k] = c.uts.rank;
+        if (nd.uts_mw) uts.mw[k] = c.uts.mw;
+        c.act0 = c.act;
+        c.tse.dirty &= (uint8_t)~D_RANK;
+        c.uts.dirty &= (uint8_t)~(D_RANK | (nd.uts_mw ? D_MW : 0));
+    }
 #if GTF_ABLATE == 6
     if (c.valid && c.act != c.act0) e.act[k] = c.act;   // diagnostics build: the activation store only
     return;
@@ -1292,7 +1305,7 @@ __device__ __forceinline__ void node_seq_body(const gtf_graph& g, gtf_nodes& n, 
 #if GTF_ASM_MARK
     asm volatile("; GTF_OP_MARK G=%0 OP=99" ::"i"(G));
 #endif
-    node_store(c, n, tse, uts, e);
+    node_store(c, n, tse, uts, e, Q::need);
 #if GTF_ASM_MARK
     asm volatile("; GTF_OP_MARK G=%0 OP=100" ::"i"(G));
 #endif
@@ -1461,7 +1474,7 @@ __global__ void __launch_bounds__(NBLOCK) k_node_pack(gtf_graph g, gtf_nodes n, 
     const bool has_tse = n.has_tse[c.v];
     const bool has_uts = fresh_has_uts(c, n, Q::fresh);
     (node_op<0, OPS, Stage>(c, g, n, tse, uts, e, p, w, sval, stg, chi2_thr, kl_thr, has_tse, has_uts, Q::need), ...);
-    node_store(c, n, tse, uts, e);
+    node_store(c, n, tse, uts, e, Q::need);
 }
 
 // run-time op sequence (gtf_node_ops): any order of any ops
@@ -1504,5 +1517,5 @@ __global__ void __launch_bounds__(NBLOCK) k_node_group(gtf_graph g, gtf_nodes n,
             default: break;
         }
     }
-    node_store(c, n, tse, uts, e);
+    node_store(c, n, tse, uts, e, nd);
 }

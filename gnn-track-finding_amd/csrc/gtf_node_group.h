@@ -1164,12 +1164,14 @@ __device__ __forceinline__ void node_op(NodeCtx<G>& c, const gtf_graph& g, gtf_n
     if constexpr (OP == OP_MW_TSE) { if (has_tse) g_mixture_weights(c, c.tse, g.solo[c.v], w.err); }
     if constexpr (OP == OP_MW_UTS) { if (has_uts) g_mixture_weights(c, c.uts, g.solo[c.v], w.err); }
 #endif
-    if constexpr (OP == OP_CLUSTER_TSE) {
+    // (a 2-lane group holds <= 2 keys: the clustering returns before doing anything,
+    // clustering.py:207, so it is not compiled in there)
+    if constexpr (OP == OP_CLUSTER_TSE && G != 2) {
         if (has_tse)
             g_cluster(c, n, tse, c.tse, stg, g.xyzr + 4 * (int64_t)c.v, g.gnn, false, chi2_thr, kl_thr, p, w.err,
                       g.slot_sxzr, nd.tse_prior);
     }
-    if constexpr (OP == OP_CLUSTER_UTS) {
+    if constexpr (OP == OP_CLUSTER_UTS && G != 2) {
         if (has_uts)
             g_cluster(c, n, uts, c.uts, stg, g.xyzr + 4 * (int64_t)c.v, g.gnn, c.live, chi2_thr, kl_thr, p, w.err,
                       g.slot_sxzr, nd.uts_prior);
@@ -1375,6 +1377,9 @@ __device__ __forceinline__ void node_bucket(int q, int b, char* smem) {
 #else
 #define GTF_NODE_WAVES_ATTR
 #endif
+#ifndef GTF_NODE_XCD_CHUNK
+#define GTF_NODE_XCD_CHUNK 4   // runs of this many consecutive blocks on one XCD (node_block_map; 1 = dispatch order)
+#endif
 // Dispatch block b (on XCD b % 8, round-robin) -> the block of work it runs: runs of C
 // consecutive work blocks share an XCD, the runs of the 8 XCDs interleaved, so neighbouring
 // nodes' slot lines meet in one L2 while every XCD still draws from every part of the
@@ -1397,9 +1402,6 @@ __global__ void __launch_bounds__(NBLOCK) GTF_NODE_WAVES_ATTR k_node_multi(NodeK
     const KArgPtr A = node_kargs();
     node_tables_init();
     __syncthreads();
-#ifndef GTF_NODE_XCD_CHUNK
-#define GTF_NODE_XCD_CHUNK 4   // runs of this many consecutive blocks on one XCD (node_block_map; 1 = dispatch order)
-#endif
     int b = node_block_map<GTF_NODE_XCD_CHUNK>((int)blockIdx.x, (int)gridDim.x);
 #ifndef GTF_NODE_ORDER
 #define GTF_NODE_ORDER 0   // 1 (diagnostics): the buckets by measured wave life, longest first (16, 32, 8, 64, 4, 2)
@@ -1426,6 +1428,23 @@ __global__ void __launch_bounds__(NBLOCK) GTF_NODE_WAVES_ATTR k_node_multi(NodeK
     if (b < A->bk.blocks[4]) { node_bucket<4, OPS...>(4, b, smem); return; }
     b -= A->bk.blocks[4];
     node_bucket<2, OPS...>(5, b, smem);
+}
+
+// GTF_SPLIT_G2 (A/B): the <= 2-slot bucket in a launch of its own after the others, at
+// GTF_G2_WAVES waves per SIMD (no clustering there, so far fewer registers, and no stage LDS)
+#ifndef GTF_SPLIT_G2
+#define GTF_SPLIT_G2 0
+#endif
+#ifndef GTF_G2_WAVES
+#define GTF_G2_WAVES 8
+#endif
+template <int... OPS>
+__global__ void __launch_bounds__(NBLOCK) __attribute__((amdgpu_waves_per_eu(GTF_G2_WAVES))) k_node_g2(NodeKArgs args) {
+    (void)args;   // read through node_kargs()
+    __shared__ __attribute__((aligned(16))) char smem[NBLOCK * sizeof(double)];
+    node_tables_init();
+    __syncthreads();
+    node_bucket<2, OPS...>(5, node_block_map<GTF_NODE_XCD_CHUNK>((int)blockIdx.x, (int)gridDim.x), smem);
 }
 
 // Packed lane segments (gtf_graph.pack_ent / pack_wave): wavefront wv takes the entries

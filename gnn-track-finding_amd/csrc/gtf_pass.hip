@@ -1228,7 +1228,16 @@ int launch_seq(const gtf_graph* g, gtf_nodes* n, gtf_states* tse, gtf_states* ut
             if (g->pack_ent && g->pack_wave && g->n_pack_waves > 0)   // every <= 64-slot node, packed
                 hipLaunchKernelGGL((k_node_pack<OPS...>), dim3((g->n_pack_waves + NBLOCK / 64 - 1) / (NBLOCK / 64)),
                                    dim3(NBLOCK), 0, st, *g, *n, T, U, *e, *p, w, chi2, kl);
-            else if (total > 0)
+            else if (GTF_SPLIT_G2 && bk.blocks[5] > 0) {   // (A/B) the <= 2-slot bucket in a launch of its own
+                const int b5 = bk.blocks[5];
+                bk.blocks[5] = 0;
+                if (total - b5 > 0)
+                    hipLaunchKernelGGL((k_node_multi<OPS...>), dim3(total - b5), dim3(NBLOCK), 0, st,
+                                       NodeKArgs{*g, *n, T, U, *e, *p, w, chi2, kl, bk});
+                bk.blocks[5] = b5;
+                hipLaunchKernelGGL((k_node_g2<OPS...>), dim3(b5), dim3(NBLOCK), 0, st,
+                                   NodeKArgs{*g, *n, T, U, *e, *p, w, chi2, kl, bk});
+            } else if (total > 0)
                 hipLaunchKernelGGL((k_node_multi<OPS...>), dim3(total), dim3(NBLOCK), 0, st,
                                    NodeKArgs{*g, *n, T, U, *e, *p, w, chi2, kl, bk});
         }

@@ -501,8 +501,36 @@ def bench_tags(d, g, dev, reps=5, descending=False):
     e1.record()
     torch.cuda.synchronize()
     sweep_ms = e0.elapsed_time(e1) / K
+    # the sweep kernel the stage itself runs, per sweep: the marginal time of the product call
+    # between S1 and S2 forced sweeps (flip threshold -1: the stop rule never fires), compact
+    # kept lists with int32 tags (the default) and the keep-mask sweeps (GTF_TAG_CSR=0)
+    S1, S2 = 8, 264
+    marg = {}
+    prev = os.environ.get("GTF_TAG_CSR")
+    try:
+        for name, val in (("csr_int32", "1"), ("keep_mask", "0")):
+            os.environ["GTF_TAG_CSR"] = val
+            w = {}
+            for S in (S1, S2):
+                ts = []
+                for _ in range(reps + 1):
+                    ta.copy_(t_init)
+                    torch.cuda.synchronize()
+                    t0 = time.perf_counter()
+                    d.tag_propagation_dev(ta, rad, threshold=-1.0, max_sweeps=S)
+                    torch.cuda.synchronize()
+                    ts.append(time.perf_counter() - t0)
+                w[S] = float(np.median(ts[1:]))
+            marg[name] = (w[S2] - w[S1]) / (S2 - S1) * 1e3
+    finally:
+        if prev is None:
+            os.environ.pop("GTF_TAG_CSR", None)
+        else:
+            os.environ["GTF_TAG_CSR"] = prev
     sweeps = len(flips)
     nbytes = 4 * g.n_edges + 8 * g.n_nodes   # SURVEY §8d B_tag, per sweep
+    stage_sweep = {k: {"sweep_ms": v, "achieved_GBps": nbytes / (v * 1e-3) / 1e9,
+                       "frac_of_peak": nbytes / (v * 1e-3) / 1e9 / rf.HBM_PEAK_GBS} for k, v in marg.items()}
     return {"initial_tags": "N - 1 - node index" if descending else "node index",
             "sweeps": sweeps, "flips": [int(x) for x in flips], "stage_wall_ms": dt * 1e3,
                                   "stage_wall_host_order_ms": dt_host * 1e3,
@@ -511,6 +539,14 @@ def bench_tags(d, g, dev, reps=5, descending=False):
                                   "algorithmic_bytes_per_sweep": nbytes,
                                   "achieved_GBps": nbytes / (sweep_ms * 1e-3) / 1e9,
                                   "frac_of_peak": nbytes / (sweep_ms * 1e-3) / 1e9 / rf.HBM_PEAK_GBS,
+            "stage_sweep": stage_sweep,
+            "stage_sweep_note": "per-sweep time of the sweeps gtf_tag_propagate itself runs: (wall(%d) - "
+                                "wall(%d)) / %d of the call with flip threshold -1 (every sweep runs); "
+                                "csr_int32 = the stage's default sweep (compact kept lists, int32 tags "
+                                "while every tag fits), keep_mask = GTF_TAG_CSR=0 (the sender-schedule "
+                                "sweep of gtf_tag_sweep, int64 tags and the keep mask); the *_call_ms / "
+                                "achieved_GBps / frac_of_peak fields above time gtf_tag_sweep alone"
+                                % (S2, S1, S2 - S1),
                                   "note": "stage_wall_ms: one gtf_tag_propagate call on device-resident tags / radius "
                                           "(prepare, sweeps with the stop rule evaluated on the device, one flip-count "
                                           "read per batch of sweeps), call to return; stage_over_kernels = that wall "

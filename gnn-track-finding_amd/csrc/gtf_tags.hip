@@ -105,20 +105,30 @@ __device__ __forceinline__ void zero_words(int32_t* zero, int nzero) {
         for (int i = (int)threadIdx.x; i < nzero; i += BLOCK) zero[i] = 0;
 }
 
+// the kept inward neighbours as a compact list per node (gtf_tag_propagate's sweeps): kcnt[u]
+// of them, their node indices at kidx[out_ptr[u] ...] (the front of u's own out-edge range)
+struct TagCsr {
+    int32_t* kcnt;   // [N] or NULL: no lists
+    int32_t* kidx;   // [E]
+};
+
 __global__ void __launch_bounds__(BLOCK) k_tag_prepare(gtf_graph g, const double* radius, uint8_t* keep,
-                                                       uint8_t* processed, int32_t* zero, int nzero) {
+                                                       uint8_t* processed, int32_t* zero, int nzero, TagCsr csr) {
     zero_words(zero, nzero);
     const int u = gtf::xcd_local(blockIdx.x, gridDim.x) * BLOCK + threadIdx.x;
     if (u < g.n_nodes) {
         const double ru = radius[u];
-        int any = 0;
-        for (int i = g.out_ptr[u]; i < g.out_ptr[u + 1]; i++) {
+        int any = 0, nk = 0;
+        const int o0 = g.out_ptr[u];
+        for (int i = o0; i < g.out_ptr[u + 1]; i++) {
             const int w = g.out_dst ? g.out_dst[i] : g.slot_dst[g.out_slot[i]];
             const uint8_t k = !(radius[w] > ru);
             keep[i] = k;
             any |= k;
+            if (k && csr.kcnt) csr.kidx[o0 + nk++] = w;
         }
         processed[u] = (uint8_t)any;
+        if (csr.kcnt) csr.kcnt[u] = nk;
     }
 }
 
@@ -126,33 +136,47 @@ __global__ void __launch_bounds__(BLOCK) k_tag_prepare(gtf_graph g, const double
 // reads its out-edge's neighbour radius in one round beside the node's own, a group ballot
 // gives processed[u]; nodes without an out-edge are not processed (the launch's last blocks)
 template <int G>
+__device__ __forceinline__ unsigned long long group_bits(bool pred) {   // this lane's G-lane group's ballot
+    const unsigned long long m = __ballot(pred);
+    if constexpr (G == 64) return m;
+    else return (m >> ((int)threadIdx.x & 63 & ~(G - 1))) & ((1ull << G) - 1ull);
+}
+
+template <int G>
 __device__ __forceinline__ void prep_group(const gtf_graph& g, const double* radius, uint8_t* keep, uint8_t* processed,
-                                          const int4* list, const int2* lanes, int count, int b) {
+                                          const int4* list, const int2* lanes, int count, int b, const TagCsr& csr) {
     const int t = b * BLOCK + (int)threadIdx.x;
     const int gi = t / G, gl = t & (G - 1);
     if (gi >= count) return;   // group-uniform
     const int4 en = list[gi];
     const int u = en.x;
     const double ru = radius[u];
-    bool any = false;
+    int nk = 0;   // kept out-edges (group-uniform)
     if (lanes) {   // one out-edge per lane (<= G of them)
         const int2 kv = lanes[t];
         const bool edge = kv.x >= 0;
         const double rw = radius[edge ? kv.y : u];
         const bool k = edge && !(rw > ru);
         if (edge) keep[en.y + gl] = (uint8_t)k;
-        any = k;
-    } else {       // chunks of G out-edges
-        for (int i = en.y + gl; i < en.z; i += G) {
-            const int w = g.out_dst ? g.out_dst[i] : g.slot_dst[g.out_slot[i]];
-            const bool k = !(radius[w] > ru);
-            keep[i] = (uint8_t)k;
-            any = any || k;
+        const unsigned long long km = group_bits<G>(k);
+        if (csr.kcnt && k) csr.kidx[en.y + __popcll(km & ((1ull << gl) - 1ull))] = kv.y;   // (in out-list order)
+        nk = __popcll(km);
+    } else {       // chunks of G out-edges (a group-uniform trip count: the ballots see every lane)
+        for (int c0 = en.y; c0 < en.z; c0 += G) {
+            const int i = c0 + gl;
+            const bool in = i < en.z;
+            const int w = in ? (g.out_dst ? g.out_dst[i] : g.slot_dst[g.out_slot[i]]) : u;
+            const bool k = in && !(radius[w] > ru);
+            if (in) keep[i] = (uint8_t)k;
+            const unsigned long long km = group_bits<G>(k);
+            if (csr.kcnt && k) csr.kidx[en.y + nk + __popcll(km & ((1ull << gl) - 1ull))] = w;
+            nk += __popcll(km);
         }
     }
-    const unsigned long long m = __ballot(any);
-    const bool grp_any = G == 64 ? m != 0ull : ((m >> (t & 63 & ~(G - 1))) & ((1ull << G) - 1ull)) != 0ull;
-    if (gl == 0) processed[u] = (uint8_t)grp_any;
+    if (gl == 0) {
+        processed[u] = (uint8_t)(nk > 0);
+        if (csr.kcnt) csr.kcnt[u] = nk;
+    }
 }
 
 struct PrepBuckets {
@@ -164,18 +188,21 @@ struct PrepBuckets {
 
 __global__ void __launch_bounds__(BLOCK) k_tag_prepare_sched(gtf_graph g, const double* radius, uint8_t* keep,
                                                              uint8_t* processed, PrepBuckets pb, int32_t* zero,
-                                                             int nzero) {
+                                                             int nzero, TagCsr csr) {
     zero_words(zero, nzero);
     int b = blockIdx.x;
     if (b < pb.blocks[0]) {
-        prep_group<4>(g, radius, keep, processed, pb.list[0], pb.lanes[0], pb.count[0], b);
+        prep_group<4>(g, radius, keep, processed, pb.list[0], pb.lanes[0], pb.count[0], b, csr);
     } else if ((b -= pb.blocks[0]) < pb.blocks[1]) {
-        prep_group<8>(g, radius, keep, processed, pb.list[1], pb.lanes[1], pb.count[1], b);
+        prep_group<8>(g, radius, keep, processed, pb.list[1], pb.lanes[1], pb.count[1], b, csr);
     } else if ((b -= pb.blocks[1]) < pb.blocks[2]) {
-        prep_group<16>(g, radius, keep, processed, pb.list[2], nullptr, pb.count[2], b);
+        prep_group<16>(g, radius, keep, processed, pb.list[2], nullptr, pb.count[2], b, csr);
     } else {
         const int u = (b - pb.blocks[2]) * BLOCK + (int)threadIdx.x;
-        if (u < g.n_nodes && g.out_ptr[u + 1] == g.out_ptr[u]) processed[u] = 0;
+        if (u < g.n_nodes && g.out_ptr[u + 1] == g.out_ptr[u]) {
+            processed[u] = 0;
+            if (csr.kcnt) csr.kcnt[u] = 0;
+        }
     }
 }
 
@@ -345,6 +372,76 @@ __global__ void __launch_bounds__(BLOCK) k_tag_sweep_sched(gtf_graph g, const ui
     block_count_add2(flipped & 1, flips, nsh, (flipped >> 1) & 1, ctl.count_processed);
 }
 
+// gtf_tag_propagate's sweep over the compact kept lists (TagCsr), one thread per node: the
+// node's count and list offset and its own tag in one round, its kept neighbours' indices in
+// the next, their tags in the third -- instead of the sender schedule's 16-byte entry plus an
+// 8-byte lane record per out-edge (24+ bytes per sender on C3's small out-degrees) and the keep
+// mask. The tags travel as int32 when every value fits: the first sweep reads the caller's
+// int64 tags, writes its output in both widths and raises `ovf` if any output does not fit;
+// the later sweeps run on the int32 pair unless `ovf` is set (then on the int64 pair, as the
+// scheduled sweep does). The maximum of values that fit fits, so one check suffices.
+template <typename T>
+__device__ __forceinline__ T tag_max_csr(const T* tin, const int32_t* kidx, int base, int c, T t) {
+    int j = 0;
+    for (; j + 4 <= c; j += 4) {   // four gathers in flight
+        const int a0 = kidx[base + j], a1 = kidx[base + j + 1], a2 = kidx[base + j + 2], a3 = kidx[base + j + 3];
+        const T v0 = tin[a0], v1 = tin[a1], v2 = tin[a2], v3 = tin[a3];
+        t = v0 > t ? v0 : t;
+        t = v1 > t ? v1 : t;
+        t = v2 > t ? v2 : t;
+        t = v3 > t ? v3 : t;
+    }
+    for (; j < c; j++) {
+        const T v = tin[kidx[base + j]];
+        t = v > t ? v : t;
+    }
+    return t;
+}
+
+__global__ void __launch_bounds__(BLOCK) k_tag_sweep_csr(gtf_graph g, TagCsr csr, const int64_t* tin64, int64_t* tout64,
+                                                         const int32_t* tin32, int32_t* tout32, int first,
+                                                         int32_t* ovf, int32_t* flips, int nsh, TagCtl ctl) {
+    if (tag_skip(ctl)) return;
+    const int u = gtf::xcd_local(blockIdx.x, gridDim.x) * BLOCK + threadIdx.x;
+    int flipped = 0, pr = 0;
+    if (u < g.n_nodes) {
+        const int c = csr.kcnt[u];
+        const int base = g.out_ptr[u];
+        pr = c > 0;
+        if (first || *ovf) {   // block-uniform
+            const int64_t t0 = tin64[u];
+            const int64_t t = c > 0 ? tag_max_csr<int64_t>(tin64, csr.kidx, base, c, t0) : t0;
+            tout64[u] = t;
+            if (first) {
+                tout32[u] = (int32_t)t;
+                if (t != (int64_t)(int32_t)t) atomicOr(ovf, 1);   // (only where a value does not fit)
+            }
+            flipped = t != t0;
+        } else {
+            const int32_t t0 = tin32[u];
+            const int32_t t = c > 0 ? tag_max_csr<int32_t>(tin32, csr.kidx, base, c, t0) : t0;
+            tout32[u] = t;
+            flipped = t != t0;
+        }
+    }
+    block_count_add2(flipped, flips, nsh, pr, ctl.count_processed);
+}
+
+// the final tags into the caller's int64 array after a run of CSR sweeps: from the int32 pair
+// (sweep q wrote buffer (q + 1) % 2, so nexec sweeps end in buffer nexec % 2), or -- when a
+// value did not fit -- from the int64 pair as k_tag_final does
+__global__ void __launch_bounds__(BLOCK) k_tag_final_csr(int64_t* tags, const int64_t* other, const int32_t* t32,
+                                                         const int32_t* nexec, const int32_t* ovf, int n) {
+    const int u = blockIdx.x * BLOCK + threadIdx.x;
+    const int ne = *nexec;
+    if (u >= n || ne == 0) return;
+    if (*ovf) {
+        if (ne & 1) tags[u] = other[u];
+    } else {
+        tags[u] = (int64_t)t32[(size_t)(ne & 1) * (size_t)n + u];
+    }
+}
+
 // One rank's sweep of the sharded tag propagation: the owned nodes
 // [lo, hi) as k_tag_sweep computes them; every other node's word is INT64_MIN and this
 // rank's flip count goes to word n_nodes + rank (the other ranks' words stay 0), so an
@@ -389,7 +486,7 @@ static int hip_fail(const char* what) {
 // nzero words at `zero`, n_processed among them)
 static int tag_prepare(const gtf_graph* g, const double* radius, uint8_t* keep, uint8_t* processed,
                        int32_t* n_processed, bool zero_count, hipStream_t st, int32_t* zero = nullptr,
-                       int nzero = 0) {
+                       int nzero = 0, TagCsr csr = TagCsr{nullptr, nullptr}) {
     // n_processed NULL: no count here (gtf_tag_propagate's first sweep counts the processed nodes)
     if (zero_count && hipMemsetAsync(n_processed, 0, sizeof(int32_t), st) != hipSuccess)
         return hip_fail("gtf_tag_prepare");
@@ -412,10 +509,10 @@ static int tag_prepare(const gtf_graph* g, const double* radius, uint8_t* keep, 
         }
         total += (g->n_nodes + BLOCK - 1) / BLOCK;   // nodes without an out-edge
         hipLaunchKernelGGL(k_tag_prepare_sched, dim3(total), dim3(BLOCK), 0, st, *g, radius, keep, processed, pb,
-                           zero, nzero);
+                           zero, nzero, csr);
     } else if (g->n_nodes > 0) {
         hipLaunchKernelGGL(k_tag_prepare, dim3((g->n_nodes + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, st, *g, radius,
-                           keep, processed, zero, nzero);
+                           keep, processed, zero, nzero, csr);
     }
     if (g->n_nodes > 0 && n_processed) {   // the processed count: a reduction of the processed bytes
         int blocks = (g->n_nodes / 16 + BLOCK * 4 - 1) / (BLOCK * 4);   // ~4 steps per thread
@@ -481,7 +578,10 @@ constexpr size_t TAG_HDR = 64 * sizeof(int32_t) + TAG_CTR * sizeof(int32_t) + TA
 
 size_t gtf_tag_workspace_bytes(int32_t n_nodes, int32_t n_edges) {
     const size_t n = n_nodes > 0 ? (size_t)n_nodes : 1, e = n_edges > 0 ? (size_t)n_edges : 1;
-    return tag_align(TAG_HDR) + tag_align(e) + tag_align(n) + tag_align(sizeof(int64_t) * n);
+    // header, keep mask, processed flags, the int64 ping-pong copy; then the compact kept lists
+    // (count per node, neighbour indices per out-edge) and the int32 tag pair
+    return tag_align(TAG_HDR) + tag_align(e) + tag_align(n) + tag_align(sizeof(int64_t) * n) +
+           tag_align(sizeof(int32_t) * n) + tag_align(sizeof(int32_t) * e) + tag_align(sizeof(int32_t) * 2 * n);
 }
 
 // batches of sweeps between two reads of the stop-rule words: at most the report's 64 totals
@@ -548,6 +648,11 @@ static int tag_wait_report(int32_t* rep, int32_t seq, hipStream_t st) {
     return 0;
 }
 
+static bool tag_csr_enabled() {   // (read per call: a test switches it in-process)
+    const char* e = getenv("GTF_TAG_CSR");   // 0: the scheduled sweep over the keep mask
+    return !(e && e[0] == '0');
+}
+
 static int32_t* tag_readback_buffer() {
     static thread_local int32_t* buf = nullptr;
     if (!buf && hipHostMalloc((void**)&buf, (64 + (1 + TAG_RING) * TAG_CTR) * sizeof(int32_t), hipHostMallocPortable) !=
@@ -587,12 +692,23 @@ int gtf_tag_propagate(const gtf_graph* g, const double* radius, int64_t* tags, d
     uint8_t* proc = reinterpret_cast<uint8_t*>(w);
     w += tag_align(n);
     int64_t* other = reinterpret_cast<int64_t*>(w);
+    w += tag_align(sizeof(int64_t) * n);
+    int32_t* kcnt = reinterpret_cast<int32_t*>(w);
+    w += tag_align(sizeof(int32_t) * n);
+    int32_t* kidx = reinterpret_cast<int32_t*>(w);
+    w += tag_align(sizeof(int32_t) * e);
+    int32_t* t32 = reinterpret_cast<int32_t*>(w);   // [2n]: the int32 ping-pong pair
+    // the sweeps over compact kept lists with int32 tags (k_tag_sweep_csr; GTF_TAG_CSR=0: the
+    // scheduled sweep of gtf_tag_sweep)
+    const bool csr = tag_csr_enabled();
+    const TagCsr lists{csr ? kcnt : nullptr, kidx};
+    int32_t* ovf = hdr + 3;   // (zeroed with the header by the prepare launch)
     *sweeps_out = 0;
     // the header words and the first sweep's counter shards zeroed by the prepare launch; every
     // executed sweep zeroes the next one's (TagCtl.next)
     int32_t* hostrep = tag_report_buffer();   // mapped page-locked report (NULL: read back by copy)
     const bool poll = hostrep && tag_poll_enabled();
-    if (int rc = tag_prepare(g, radius, keep, proc, nullptr, false, st, hdr, 64 + 2 * (int)TAG_CTR)) return rc;
+    if (int rc = tag_prepare(g, radius, keep, proc, nullptr, false, st, hdr, 64 + 2 * (int)TAG_CTR, lists)) return rc;
     int32_t s = 0, batch = 2, executed = 0;
     int32_t* host = poll ? nullptr : tag_readback_buffer();   // the header words, then the ring
     if (!poll && !host) return hip_fail("gtf_tag_propagate: page-locked read-back buffer");
@@ -603,8 +719,12 @@ int gtf_tag_propagate(const gtf_graph* g, const double* radius, int64_t* tags, d
     // harmless: the next batch's first sweep rewrites every tag of `tags` or reads it as copied.
     auto final_copy = [&]() -> int {
         if (g->n_nodes <= 0) return 0;
-        hipLaunchKernelGGL(k_tag_final, dim3((g->n_nodes + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, st, tags, other,
-                           hdr + 2, g->n_nodes);
+        if (csr)
+            hipLaunchKernelGGL(k_tag_final_csr, dim3((g->n_nodes + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, st, tags, other,
+                               t32, hdr + 2, ovf, g->n_nodes);
+        else
+            hipLaunchKernelGGL(k_tag_final, dim3((g->n_nodes + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, st, tags, other,
+                               hdr + 2, g->n_nodes);
         return hipGetLastError() == hipSuccess ? 0 : hip_fail("gtf_tag_propagate: final copy");
     };
     bool copied = false;
@@ -618,8 +738,19 @@ int gtf_tag_propagate(const gtf_graph* g, const double* radius, int64_t* tags, d
                              flip_threshold, ring + ((q + 1) % TAG_RING) * TAG_CTR, q == 0 ? pshards : nullptr};
             int64_t* tin = (q & 1) ? other : tags;
             int64_t* tout = (q & 1) ? tags : other;
-            if (int rc = tag_sweep(g, keep, proc, tin, tout, ring + (q % TAG_RING) * TAG_CTR, TAG_SHARDS, ctl, st))
+            if (csr) {
+                if (g->n_nodes > 0) {
+                    int32_t* b0 = t32 + (size_t)(q & 1) * n;         // sweep q reads buffer q % 2 ...
+                    int32_t* b1 = t32 + (size_t)((q + 1) & 1) * n;   // ... and writes the other
+                    hipLaunchKernelGGL(k_tag_sweep_csr, dim3((g->n_nodes + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, st,
+                                       *g, lists, tin, tout, b0, b1, q == 0 ? 1 : 0, ovf,
+                                       ring + (q % TAG_RING) * TAG_CTR, TAG_SHARDS, ctl);
+                    if (hipGetLastError() != hipSuccess) return hip_fail("gtf_tag_propagate: sweep launch");
+                }
+            } else if (int rc = tag_sweep(g, keep, proc, tin, tout, ring + (q % TAG_RING) * TAG_CTR, TAG_SHARDS, ctl,
+                                          st)) {
                 return rc;
+            }
         }
         int32_t words[3];   // processed, stop, executed
         const int32_t* fl;  // flips of sweeps s, s + 1, ...

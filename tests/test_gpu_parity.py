@@ -122,15 +122,18 @@ def test_tag_propagate_one_call():
                                ctypes.c_void_p(ws.data_ptr()), nb - 1, d.stream) != 0
 
 
+@pytest.mark.parametrize("csr", ["1", "0"])
 @pytest.mark.parametrize("poll", ["1", "0"])
 @pytest.mark.parametrize("schedule", [True, False])
 @pytest.mark.parametrize("max_sweeps", [64, 3, 0])
-def test_tag_propagate_stop_rule_and_cap(schedule, max_sweeps, poll, monkeypatch):
+def test_tag_propagate_stop_rule_and_cap(schedule, max_sweeps, poll, csr, monkeypatch):
     """the stop rule evaluated on the device (gtf_tag_propagate's batched sweeps): the
     reference's flip vector, cut at max_sweeps, on the sender-schedule and the thread-per-node
-    kernels, with the batch report polled in mapped memory or copied back (GTF_TAG_POLL); the
-    tags equal the host loop of single sweeps run that many times"""
+    prepare kernels, over the compact kept lists with int32 tags or the keep mask (GTF_TAG_CSR),
+    with the batch report polled in mapped memory or copied back (GTF_TAG_POLL); the tags equal
+    the host loop of single sweeps run that many times"""
     monkeypatch.setenv("GTF_TAG_POLL", poll)
+    monkeypatch.setenv("GTF_TAG_CSR", csr)
     import ctypes
     import torch
     from gtf import _native as nat
@@ -188,12 +191,14 @@ def _chain_graph(n):
     return TrackGraph(n, n - 1, slot_ptr, out_ptr, np.arange(n - 1, dtype=np.int32), node, slot)
 
 
+@pytest.mark.parametrize("csr", ["1", "0"])
 @pytest.mark.parametrize("poll", ["1", "0"])
 @pytest.mark.parametrize("schedule", [True, False])
-def test_tag_propagate_long_run(schedule, poll, monkeypatch):
+def test_tag_propagate_long_run(schedule, poll, csr, monkeypatch):
     """300 sweeps in one gtf_tag_propagate call: batches of 2 .. 64 launches, the flip-counter
     ring (128 sweeps) wrapped twice with every sweep zeroing the next one's counters"""
     monkeypatch.setenv("GTF_TAG_POLL", poll)
+    monkeypatch.setenv("GTF_TAG_CSR", csr)
     import ctypes
     import torch
     from gtf import _native as nat
@@ -217,6 +222,51 @@ def test_tag_propagate_long_run(schedule, poll, monkeypatch):
     assert want_flips == list(range(n - 1, -1, -1))
     assert sweeps.value == len(want_flips) and list(flips[:sweeps.value]) == want_flips
     assert np.array_equal(tags.cpu().numpy(), want_tags)
+
+
+@pytest.mark.parametrize("shape", ["all_wide", "one_wide", "negative"])
+def test_tag_propagate_tags_beyond_int32(shape, monkeypatch):
+    """tags that do not fit 32 bits (the int64 of the reference's tag arrays): the compact-list
+    sweeps carry int32 tags only while every value fits, so a shift by 2^40 of every tag, one
+    wide tag alone (its kept predecessors take it from the first sweep on) and tags shifted
+    below -2^31 give the keep-mask sweeps' (GTF_TAG_CSR=0) flips and tags word for word, and
+    the shifted ones the reference's flips and shifted tags"""
+    import ctypes
+    import torch
+    from gtf import _native as nat
+    g, _, extra, _ = load("tags_vol7")
+    d = _dev(g)
+    L = d.lib
+    t0 = np.ascontiguousarray(g.node["tag"], dtype=np.int64)
+    if shape == "all_wide":
+        t0 = t0 + (1 << 40)
+    elif shape == "negative":
+        t0 = t0 - (1 << 40)
+    else:
+        t0 = t0.copy()
+        t0[int(np.argmax(t0))] = 1 << 40
+    radius = torch.from_numpy(np.ascontiguousarray(g.node["xyzr"][:, 3], dtype=np.float64)).to(d.device)
+    nb = L.gtf_tag_workspace_bytes(g.n_nodes, g.n_edges)
+    res = {}
+    for csr in ("1", "0"):
+        monkeypatch.setenv("GTF_TAG_CSR", csr)
+        tags = torch.from_numpy(t0).to(d.device)
+        ws = torch.full((nb,), 0xFF, dtype=torch.uint8, device=d.device)
+        flips = (ctypes.c_int32 * 64)()
+        sweeps = ctypes.c_int32(-1)
+        nat.check(L.gtf_tag_propagate(ctypes.byref(d.cg), ctypes.c_void_p(radius.data_ptr()),
+                                      ctypes.c_void_p(tags.data_ptr()), 0.1, 64,
+                                      ctypes.cast(flips, ctypes.c_void_p), ctypes.byref(sweeps),
+                                      ctypes.c_void_p(ws.data_ptr()), nb, d.stream))
+        torch.cuda.synchronize()
+        res[csr] = (list(flips[:sweeps.value]), tags.cpu().numpy())
+    assert res["1"][0] == res["0"][0]
+    assert np.array_equal(res["1"][1], res["0"][1])
+    if shape != "one_wide":   # (a shift changes no comparison)
+        assert res["1"][0] == list(extra["flips"])
+        off = (1 << 40) if shape == "all_wide" else -(1 << 40)
+        kept = extra["tags"] >= 0
+        assert np.array_equal(res["1"][1][kept], extra["tags"][kept] + off)
 
 
 def test_workspace_init_contract():

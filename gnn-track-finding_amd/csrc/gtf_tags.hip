@@ -106,11 +106,24 @@ __device__ __forceinline__ void zero_words(int32_t* zero, int nzero) {
 }
 
 // the kept inward neighbours as a compact list per node (gtf_tag_propagate's sweeps): kcnt[u]
-// of them, their node indices at kidx[out_ptr[u] ...] (the front of u's own out-edge range)
+// of them, their node indices at kidx[out_ptr[u] ...] (the front of u's own out-edge range).
+// With `kword` (graphs of < 2^23 edges) the node's list is one 4-byte word, out_ptr[u] << 9 |
+// min(count, 511), and kcnt[u] is written only where the count saturates: the sweep reads one
+// word per node instead of the count and the offset.
+constexpr uint32_t KW_BITS = 9, KW_SAT = (1u << KW_BITS) - 1u;
 struct TagCsr {
-    int32_t* kcnt;   // [N] or NULL: no lists
-    int32_t* kidx;   // [E]
+    int32_t* kcnt;    // [N] or NULL: no lists
+    int32_t* kidx;    // [E]
+    uint32_t* kword;  // [N] or NULL: kcnt for every node
 };
+__device__ __forceinline__ void csr_node(const TagCsr& csr, int u, int base, int nk) {
+    if (csr.kword) {
+        csr.kword[u] = ((uint32_t)base << KW_BITS) | (nk < (int)KW_SAT ? (uint32_t)nk : KW_SAT);
+        if (nk >= (int)KW_SAT) csr.kcnt[u] = nk;
+    } else {
+        csr.kcnt[u] = nk;
+    }
+}
 
 __global__ void __launch_bounds__(BLOCK) k_tag_prepare(gtf_graph g, const double* radius, uint8_t* keep,
                                                        uint8_t* processed, int32_t* zero, int nzero, TagCsr csr) {
@@ -123,12 +136,12 @@ __global__ void __launch_bounds__(BLOCK) k_tag_prepare(gtf_graph g, const double
         for (int i = o0; i < g.out_ptr[u + 1]; i++) {
             const int w = g.out_dst ? g.out_dst[i] : g.slot_dst[g.out_slot[i]];
             const uint8_t k = !(radius[w] > ru);
-            keep[i] = k;
+            if (keep) keep[i] = k;
             any |= k;
             if (k && csr.kcnt) csr.kidx[o0 + nk++] = w;
         }
-        processed[u] = (uint8_t)any;
-        if (csr.kcnt) csr.kcnt[u] = nk;
+        if (processed) processed[u] = (uint8_t)any;
+        if (csr.kcnt) csr_node(csr, u, o0, nk);
     }
 }
 
@@ -157,7 +170,7 @@ __device__ __forceinline__ void prep_group(const gtf_graph& g, const double* rad
         const bool edge = kv.x >= 0;
         const double rw = radius[edge ? kv.y : u];
         const bool k = edge && !(rw > ru);
-        if (edge) keep[en.y + gl] = (uint8_t)k;
+        if (edge && keep) keep[en.y + gl] = (uint8_t)k;
         const unsigned long long km = group_bits<G>(k);
         if (csr.kcnt && k) csr.kidx[en.y + __popcll(km & ((1ull << gl) - 1ull))] = kv.y;   // (in out-list order)
         nk = __popcll(km);
@@ -167,15 +180,73 @@ __device__ __forceinline__ void prep_group(const gtf_graph& g, const double* rad
             const bool in = i < en.z;
             const int w = in ? (g.out_dst ? g.out_dst[i] : g.slot_dst[g.out_slot[i]]) : u;
             const bool k = in && !(radius[w] > ru);
-            if (in) keep[i] = (uint8_t)k;
+            if (in && keep) keep[i] = (uint8_t)k;
             const unsigned long long km = group_bits<G>(k);
             if (csr.kcnt && k) csr.kidx[en.y + nk + __popcll(km & ((1ull << gl) - 1ull))] = w;
             nk += __popcll(km);
         }
     }
     if (gl == 0) {
-        processed[u] = (uint8_t)(nk > 0);
-        if (csr.kcnt) csr.kcnt[u] = nk;
+        if (processed) processed[u] = (uint8_t)(nk > 0);
+        if (csr.kcnt) csr_node(csr, u, en.y, nk);
+    }
+}
+
+// gtf_tag_propagate's prepare in the compact-list form (no keep mask, no processed flags: its
+// sweeps read neither), NPT nodes per thread BLOCK apart with their loads interleaved as in
+// sweep_csr_nodes: the out-list bounds and own radius of each, its first four out-neighbours,
+// their radii (longer lists in steps of four); the kept ones written to the front of the node's
+// out-range, in out-list order.
+template <int NPT>
+__global__ void __launch_bounds__(BLOCK) k_tag_prepare_csr(gtf_graph g, const double* radius, TagCsr csr,
+                                                           int32_t* zero, int nzero) {
+    zero_words(zero, nzero);
+    const int u0 = gtf::xcd_local(blockIdx.x, gridDim.x) * BLOCK * NPT + (int)threadIdx.x;
+    int o0[NPT], o1[NPT];
+    double ru[NPT];
+#pragma unroll
+    for (int j = 0; j < NPT; j++) {
+        const int u = u0 + j * BLOCK;
+        o0[j] = o1[j] = 0;
+        ru[j] = 0.0;
+        if (u < g.n_nodes) {
+            o0[j] = g.out_ptr[u];
+            o1[j] = g.out_ptr[u + 1];
+            ru[j] = radius[u];
+        }
+    }
+    constexpr int R = 4;   // out-neighbours per node in the second round (then chunks of R)
+    auto dst = [&](int i) { return g.out_dst ? g.out_dst[i] : g.slot_dst[g.out_slot[i]]; };
+    int w[NPT][R];
+#pragma unroll
+    for (int j = 0; j < NPT; j++)
+#pragma unroll
+        for (int r = 0; r < R; r++) w[j][r] = o0[j] + r < o1[j] ? dst(o0[j] + r) : 0;
+    double rw[NPT][R];
+#pragma unroll
+    for (int j = 0; j < NPT; j++)
+#pragma unroll
+        for (int r = 0; r < R; r++) rw[j][r] = o0[j] + r < o1[j] ? radius[w[j][r]] : 0.0;
+#pragma unroll
+    for (int j = 0; j < NPT; j++) {
+        const int u = u0 + j * BLOCK;
+        if (u >= g.n_nodes) continue;
+        int nk = 0;
+#pragma unroll
+        for (int r = 0; r < R; r++)
+            if (o0[j] + r < o1[j] && !(rw[j][r] > ru[j])) csr.kidx[o0[j] + nk++] = w[j][r];
+        for (int i = o0[j] + R; i < o1[j]; i += R) {   // longer lists: R independent loads per step
+            int x[R];
+            double rx[R];
+#pragma unroll
+            for (int r = 0; r < R; r++) x[r] = i + r < o1[j] ? dst(i + r) : 0;
+#pragma unroll
+            for (int r = 0; r < R; r++) rx[r] = i + r < o1[j] ? radius[x[r]] : 0.0;
+#pragma unroll
+            for (int r = 0; r < R; r++)
+                if (i + r < o1[j] && !(rx[r] > ru[j])) csr.kidx[o0[j] + nk++] = x[r];
+        }
+        csr_node(csr, u, o0[j], nk);
     }
 }
 
@@ -200,8 +271,8 @@ __global__ void __launch_bounds__(BLOCK) k_tag_prepare_sched(gtf_graph g, const 
     } else {
         const int u = (b - pb.blocks[2]) * BLOCK + (int)threadIdx.x;
         if (u < g.n_nodes && g.out_ptr[u + 1] == g.out_ptr[u]) {
-            processed[u] = 0;
-            if (csr.kcnt) csr.kcnt[u] = 0;
+            if (processed) processed[u] = 0;
+            if (csr.kcnt) csr_node(csr, u, g.out_ptr[u], 0);
         }
     }
 }
@@ -380,6 +451,105 @@ __global__ void __launch_bounds__(BLOCK) k_tag_sweep_sched(gtf_graph g, const ui
 // int64 tags, writes its output in both widths and raises `ovf` if any output does not fit;
 // the later sweeps run on the int32 pair unless `ovf` is set (then on the int64 pair, as the
 // scheduled sweep does). The maximum of values that fit fits, so one check suffices.
+// NPT nodes per thread (BLOCK apart, so every round of loads stays coalesced), their loads
+// interleaved: the words and own tags of all of them, then the first four kept indices of each,
+// then those neighbours' tags -- three dependent rounds for NPT nodes instead of for one.
+// Longer lists finish in steps of four independent loads.
+// `t32` (the first sweep only): the int32 copy of the output, with `ovf` raised where a value
+// does not fit.
+template <int NPT, int R, typename T>
+__device__ __forceinline__ void sweep_csr_nodes(const gtf_graph& g, const TagCsr& csr, const T* tin, T* tout,
+                                                int32_t* t32, int32_t* ovf, int u0, int& nflip, int& nproc) {
+    int c[NPT], b[NPT];
+    T t[NPT];
+#pragma unroll
+    for (int j = 0; j < NPT; j++) {
+        const int u = u0 + j * BLOCK;
+        c[j] = 0;
+        b[j] = 0;
+        t[j] = 0;
+        if (u < g.n_nodes) {
+            if (csr.kword) {   // (uniform)
+                const uint32_t w = csr.kword[u];
+                b[j] = (int)(w >> KW_BITS);
+                c[j] = (int)(w & KW_SAT);
+            } else {
+                c[j] = csr.kcnt[u];
+                b[j] = g.out_ptr[u];
+            }
+            t[j] = tin[u];
+        }
+    }
+    int a[NPT][R];   // R kept indices per node in the second round (then chunks of R)
+#pragma unroll
+    for (int j = 0; j < NPT; j++) {
+        if (csr.kword && c[j] == (int)KW_SAT) c[j] = csr.kcnt[u0 + j * BLOCK];   // (a saturated count)
+#pragma unroll
+        for (int r = 0; r < R; r++) a[j][r] = c[j] > r ? csr.kidx[b[j] + r] : 0;
+    }
+    T m[NPT];
+#pragma unroll
+    for (int j = 0; j < NPT; j++) {
+        m[j] = t[j];
+#pragma unroll
+        for (int r = 0; r < R; r++)
+            if (c[j] > r) {
+                const T v = tin[a[j][r]];
+                m[j] = v > m[j] ? v : m[j];
+            }
+    }
+#pragma unroll
+    for (int j = 0; j < NPT; j++)
+        for (int k = R; k < c[j]; k += R) {   // longer lists: R independent loads per step
+            int x[R];
+#pragma unroll
+            for (int r = 0; r < R; r++) x[r] = k + r < c[j] ? csr.kidx[b[j] + k + r] : -1;
+#pragma unroll
+            for (int r = 0; r < R; r++)
+                if (x[r] >= 0) {
+                    const T v = tin[x[r]];
+                    m[j] = v > m[j] ? v : m[j];
+                }
+        }
+#pragma unroll
+    for (int j = 0; j < NPT; j++) {
+        const int u = u0 + j * BLOCK;
+        const bool in = u < g.n_nodes;
+        if (in) {
+            tout[u] = m[j];
+            if (t32) {
+                t32[u] = (int32_t)m[j];
+                if ((int64_t)m[j] != (int64_t)(int32_t)m[j]) atomicOr(ovf, 1);   // (only where a value does not fit)
+            }
+        }
+        // wave-level counts by ballot (every lane of the wave holds them): a cross-lane sum would
+        // add a dependent chain of LDS permutes to the end of every wave, exposed on a launch of
+        // one round of waves like C4's
+        nflip += (int)__popcll(__ballot(in && m[j] != t[j]));
+        nproc += (int)__popcll(__ballot(in && c[j] > 0));
+    }
+}
+
+// the block's totals of two wave-level counts into sharded counters (block_count_add2 with counts)
+__device__ __forceinline__ void block_sum_add2(int a, int32_t* ctr_a, int nsh_a, int b, int32_t* ctr_b) {
+    __shared__ int s_sum2[2][BLOCK / 64];
+    if ((threadIdx.x & 63) == 0) {
+        s_sum2[0][threadIdx.x >> 6] = a;
+        s_sum2[1][threadIdx.x >> 6] = b;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int ta = 0, tb = 0;
+#pragma unroll
+        for (int w = 0; w < BLOCK / 64; w++) { ta += s_sum2[0][w]; tb += s_sum2[1][w]; }
+        if (ta) atomicAdd(ctr_a + (nsh_a > 1 ? (int)(blockIdx.x % nsh_a) * TAG_STRIDE : 0), ta);
+        if (ctr_b && tb) atomicAdd(ctr_b + (int)(blockIdx.x % TAG_SHARDS) * TAG_STRIDE, tb);
+    }
+}
+
+// one node per thread (the launches of under ~262 k nodes, C4's): the count and offset, then the
+// list in steps of four independent loads -- measured 6.2 against 9.4 us per C4 sweep for
+// sweep_csr_nodes<1, 4> (round 6)
 template <typename T>
 __device__ __forceinline__ T tag_max_csr(const T* tin, const int32_t* kidx, int base, int c, T t) {
     int j = 0;
@@ -398,17 +568,25 @@ __device__ __forceinline__ T tag_max_csr(const T* tin, const int32_t* kidx, int 
     return t;
 }
 
-__global__ void __launch_bounds__(BLOCK) k_tag_sweep_csr(gtf_graph g, TagCsr csr, const int64_t* tin64, int64_t* tout64,
-                                                         const int32_t* tin32, int32_t* tout32, int first,
-                                                         int32_t* ovf, int32_t* flips, int nsh, TagCtl ctl) {
+__global__ void __launch_bounds__(BLOCK) k_tag_sweep_csr1(gtf_graph g, TagCsr csr, const int64_t* tin64, int64_t* tout64,
+                                                          const int32_t* tin32, int32_t* tout32, int first,
+                                                          int32_t* ovf, int32_t* flips, int nsh, TagCtl ctl) {
     if (tag_skip(ctl)) return;
     const int u = gtf::xcd_local(blockIdx.x, gridDim.x) * BLOCK + threadIdx.x;
     int flipped = 0, pr = 0;
     if (u < g.n_nodes) {
-        const int c = csr.kcnt[u];
-        const int base = g.out_ptr[u];
+        int c, base;
+        if (csr.kword) {   // (uniform)
+            const uint32_t w = csr.kword[u];
+            base = (int)(w >> KW_BITS);
+            c = (int)(w & KW_SAT);
+            if (c == (int)KW_SAT) c = csr.kcnt[u];
+        } else {
+            c = csr.kcnt[u];
+            base = g.out_ptr[u];
+        }
         pr = c > 0;
-        if (first || *ovf) {   // block-uniform
+        if (first || *ovf) {   // (uniform)
             const int64_t t0 = tin64[u];
             const int64_t t = c > 0 ? tag_max_csr<int64_t>(tin64, csr.kidx, base, c, t0) : t0;
             tout64[u] = t;
@@ -425,6 +603,20 @@ __global__ void __launch_bounds__(BLOCK) k_tag_sweep_csr(gtf_graph g, TagCsr csr
         }
     }
     block_count_add2(flipped, flips, nsh, pr, ctl.count_processed);
+}
+
+template <int NPT, int R>
+__global__ void __launch_bounds__(BLOCK) k_tag_sweep_csr(gtf_graph g, TagCsr csr, const int64_t* tin64, int64_t* tout64,
+                                                         const int32_t* tin32, int32_t* tout32, int first,
+                                                         int32_t* ovf, int32_t* flips, int nsh, TagCtl ctl) {
+    if (tag_skip(ctl)) return;
+    const int u0 = gtf::xcd_local(blockIdx.x, gridDim.x) * BLOCK * NPT + (int)threadIdx.x;
+    int nflip = 0, nproc = 0;
+    if (first || *ovf)   // (uniform)
+        sweep_csr_nodes<NPT, R, int64_t>(g, csr, tin64, tout64, first ? tout32 : nullptr, ovf, u0, nflip, nproc);
+    else
+        sweep_csr_nodes<NPT, R, int32_t>(g, csr, tin32, tout32, nullptr, nullptr, u0, nflip, nproc);
+    block_sum_add2(nflip, flips, nsh, nproc, ctl.count_processed);
 }
 
 // the final tags into the caller's int64 array after a run of CSR sweeps: from the int32 pair
@@ -481,18 +673,35 @@ static int hip_fail(const char* what) {
     return -1;
 }
 
-// zero_count: n_processed zeroed here (else the caller has)
+// nodes per thread of the compact-list prepare (GTF_TAG_PREP_NPT 1 / 2 / 4; 0: the lane-group or
+// thread-per-node prepare with the keep mask skipped). Measured (round 6): on C3 (2.0 M nodes)
+// one node per thread 40 us against 48-49 us for the lane groups or two per thread; on C4
+// (180 k nodes) the lane groups' wider launch is ahead.
+static int tag_prep_npt(int n) {
+    const char* e = getenv("GTF_TAG_PREP_NPT");
+    if (e && e[0]) {
+        const int v = atoi(e);
+        if (v == 0 || v == 1 || v == 2 || v == 4) return v;
+    }
+    return n >= 2 * BLOCK * 512 ? 1 : 0;
+}
+
 // zero_count: n_processed zeroed here (else the caller has, or the prepare launch zeroes the
 // nzero words at `zero`, n_processed among them)
 static int tag_prepare(const gtf_graph* g, const double* radius, uint8_t* keep, uint8_t* processed,
                        int32_t* n_processed, bool zero_count, hipStream_t st, int32_t* zero = nullptr,
-                       int nzero = 0, TagCsr csr = TagCsr{nullptr, nullptr}) {
+                       int nzero = 0, TagCsr csr = TagCsr{nullptr, nullptr, nullptr}) {
     // n_processed NULL: no count here (gtf_tag_propagate's first sweep counts the processed nodes)
     if (zero_count && hipMemsetAsync(n_processed, 0, sizeof(int32_t), st) != hipSuccess)
         return hip_fail("gtf_tag_prepare");
     if (g->n_nodes <= 0 && zero && hipMemsetAsync(zero, 0, nzero * sizeof(int32_t), st) != hipSuccess)
         return hip_fail("gtf_tag_prepare");
-    if (g->n_nodes > 0 && g->out_sched) {   // lane groups over the sender schedule
+    if (g->n_nodes > 0 && !keep && csr.kcnt && tag_prep_npt(g->n_nodes) > 0) {   // the compact lists alone
+        const int npt = tag_prep_npt(g->n_nodes);
+        auto kern = npt == 4 ? k_tag_prepare_csr<4> : npt == 2 ? k_tag_prepare_csr<2> : k_tag_prepare_csr<1>;
+        hipLaunchKernelGGL(kern, dim3((g->n_nodes + BLOCK * npt - 1) / (BLOCK * npt)), dim3(BLOCK), 0, st, *g,
+                           radius, csr, zero, nzero);
+    } else if (g->n_nodes > 0 && g->out_sched) {   // lane groups over the sender schedule
         PrepBuckets pb;
         const int cnt[3] = {g->n_o4, g->n_o8, g->n_o16}, gs[3] = {4, 8, 16};
         const int4* l = reinterpret_cast<const int4*>(g->out_sched);
@@ -579,9 +788,9 @@ constexpr size_t TAG_HDR = 64 * sizeof(int32_t) + TAG_CTR * sizeof(int32_t) + TA
 size_t gtf_tag_workspace_bytes(int32_t n_nodes, int32_t n_edges) {
     const size_t n = n_nodes > 0 ? (size_t)n_nodes : 1, e = n_edges > 0 ? (size_t)n_edges : 1;
     // header, keep mask, processed flags, the int64 ping-pong copy; then the compact kept lists
-    // (count per node, neighbour indices per out-edge) and the int32 tag pair
+    // (count and packed word per node, neighbour indices per out-edge) and the int32 tag pair
     return tag_align(TAG_HDR) + tag_align(e) + tag_align(n) + tag_align(sizeof(int64_t) * n) +
-           tag_align(sizeof(int32_t) * n) + tag_align(sizeof(int32_t) * e) + tag_align(sizeof(int32_t) * 2 * n);
+           2 * tag_align(sizeof(int32_t) * n) + tag_align(sizeof(int32_t) * e) + tag_align(sizeof(int32_t) * 2 * n);
 }
 
 // batches of sweeps between two reads of the stop-rule words: at most the report's 64 totals
@@ -652,6 +861,24 @@ static bool tag_csr_enabled() {   // (read per call: a test switches it in-proce
     const char* e = getenv("GTF_TAG_CSR");   // 0: the scheduled sweep over the keep mask
     return !(e && e[0] == '0');
 }
+// nodes per thread of the compact-list sweep: 2 where that keeps >= 2 blocks per CU (256 CUs);
+// 4 measured no faster on C3 (round 6)
+static int tag_nodes_per_thread(int n) {
+    const char* e = getenv("GTF_TAG_NPT");
+    if (e && e[0]) {   // 1 / 2 / 4 (A/B)
+        const int v = atoi(e);
+        if (v == 1 || v == 2 || v == 4) return v;
+    }
+    return n >= 2 * BLOCK * 512 ? 2 : 1;
+}
+static int tag_sweep_r() {   // kept indices per node in the second round of a 2- / 4-node sweep
+    const char* e = getenv("GTF_TAG_R");   // (GTF_TAG_R 2 / 4; C3: 2 at least as fast)
+    return e && e[0] == '4' ? 4 : 2;
+}
+static bool tag_kword_enabled() {
+    const char* e = getenv("GTF_TAG_KWORD");   // 0: the count and the offset per node
+    return !(e && e[0] == '0');
+}
 
 static int32_t* tag_readback_buffer() {
     static thread_local int32_t* buf = nullptr;
@@ -698,17 +925,24 @@ int gtf_tag_propagate(const gtf_graph* g, const double* radius, int64_t* tags, d
     int32_t* kidx = reinterpret_cast<int32_t*>(w);
     w += tag_align(sizeof(int32_t) * e);
     int32_t* t32 = reinterpret_cast<int32_t*>(w);   // [2n]: the int32 ping-pong pair
+    w += tag_align(sizeof(int32_t) * 2 * n);
+    uint32_t* kword = reinterpret_cast<uint32_t*>(w);
     // the sweeps over compact kept lists with int32 tags (k_tag_sweep_csr; GTF_TAG_CSR=0: the
-    // scheduled sweep of gtf_tag_sweep)
+    // scheduled sweep of gtf_tag_sweep over the keep mask and processed flags, which only it
+    // reads); one packed word per node where every list offset fits its 23 bits
     const bool csr = tag_csr_enabled();
-    const TagCsr lists{csr ? kcnt : nullptr, kidx};
+    const bool packed = csr && (size_t)n_edges < ((size_t)1 << (32 - KW_BITS)) && tag_kword_enabled();
+    const TagCsr lists{csr ? kcnt : nullptr, kidx, packed ? kword : nullptr};
+    const int npt = tag_nodes_per_thread(g->n_nodes);
     int32_t* ovf = hdr + 3;   // (zeroed with the header by the prepare launch)
     *sweeps_out = 0;
     // the header words and the first sweep's counter shards zeroed by the prepare launch; every
     // executed sweep zeroes the next one's (TagCtl.next)
     int32_t* hostrep = tag_report_buffer();   // mapped page-locked report (NULL: read back by copy)
     const bool poll = hostrep && tag_poll_enabled();
-    if (int rc = tag_prepare(g, radius, keep, proc, nullptr, false, st, hdr, 64 + 2 * (int)TAG_CTR, lists)) return rc;
+    if (int rc = tag_prepare(g, radius, csr ? nullptr : keep, csr ? nullptr : proc, nullptr, false, st, hdr,
+                             64 + 2 * (int)TAG_CTR, lists))
+        return rc;
     int32_t s = 0, batch = 2, executed = 0;
     int32_t* host = poll ? nullptr : tag_readback_buffer();   // the header words, then the ring
     if (!poll && !host) return hip_fail("gtf_tag_propagate: page-locked read-back buffer");
@@ -742,8 +976,11 @@ int gtf_tag_propagate(const gtf_graph* g, const double* radius, int64_t* tags, d
                 if (g->n_nodes > 0) {
                     int32_t* b0 = t32 + (size_t)(q & 1) * n;         // sweep q reads buffer q % 2 ...
                     int32_t* b1 = t32 + (size_t)((q + 1) & 1) * n;   // ... and writes the other
-                    hipLaunchKernelGGL(k_tag_sweep_csr, dim3((g->n_nodes + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, st,
-                                       *g, lists, tin, tout, b0, b1, q == 0 ? 1 : 0, ovf,
+                    auto kern = npt == 1   ? k_tag_sweep_csr1
+                                : npt == 4 ? (tag_sweep_r() == 4 ? k_tag_sweep_csr<4, 4> : k_tag_sweep_csr<4, 2>)
+                                           : (tag_sweep_r() == 4 ? k_tag_sweep_csr<2, 4> : k_tag_sweep_csr<2, 2>);
+                    hipLaunchKernelGGL(kern, dim3((g->n_nodes + BLOCK * npt - 1) / (BLOCK * npt)), dim3(BLOCK), 0,
+                                       st, *g, lists, tin, tout, b0, b1, q == 0 ? 1 : 0, ovf,
                                        ring + (q % TAG_RING) * TAG_CTR, TAG_SHARDS, ctl);
                     if (hipGetLastError() != hipSuccess) return hip_fail("gtf_tag_propagate: sweep launch");
                 }

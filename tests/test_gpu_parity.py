@@ -122,7 +122,23 @@ def test_tag_propagate_one_call():
                                ctypes.c_void_p(ws.data_ptr()), nb - 1, d.stream) != 0
 
 
-@pytest.mark.parametrize("csr", ["1", "0"])
+# GTF_TAG_CSR, GTF_TAG_KWORD, GTF_TAG_NPT, GTF_TAG_PREP_NPT, GTF_TAG_R ("": the default)
+_CSR_MODES = {"packed": ("1", "1", "", "", ""), "packed_n2": ("1", "1", "2", "2", "2"),
+              "packed_n2_r4": ("1", "1", "2", "0", "4"), "packed_n4": ("1", "1", "4", "4", "4"),
+              "counts_thread_prep": ("1", "0", "1", "1", ""), "counts_group_prep": ("1", "0", "2", "0", ""),
+              "mask": ("0", "1", "", "", "")}
+
+
+def _csr_env(monkeypatch, mode):
+    """gtf_tag_propagate's sweep form: compact kept lists with one packed word per node (1, 2 or
+    4 nodes per thread in the prepare and the sweeps, 2 or 4 kept indices per node in a sweep's
+    second round), with a count and an offset per node built by the one-node-per-thread or the
+    lane-group prepare, or the keep-mask sweeps (GTF_TAG_CSR=0)"""
+    for k, v in zip(("GTF_TAG_CSR", "GTF_TAG_KWORD", "GTF_TAG_NPT", "GTF_TAG_PREP_NPT", "GTF_TAG_R"), _CSR_MODES[mode]):
+        monkeypatch.setenv(k, v)
+
+
+@pytest.mark.parametrize("csr", list(_CSR_MODES))
 @pytest.mark.parametrize("poll", ["1", "0"])
 @pytest.mark.parametrize("schedule", [True, False])
 @pytest.mark.parametrize("max_sweeps", [64, 3, 0])
@@ -133,7 +149,7 @@ def test_tag_propagate_stop_rule_and_cap(schedule, max_sweeps, poll, csr, monkey
     with the batch report polled in mapped memory or copied back (GTF_TAG_POLL); the tags equal
     the host loop of single sweeps run that many times"""
     monkeypatch.setenv("GTF_TAG_POLL", poll)
-    monkeypatch.setenv("GTF_TAG_CSR", csr)
+    _csr_env(monkeypatch, csr)
     import ctypes
     import torch
     from gtf import _native as nat
@@ -191,14 +207,14 @@ def _chain_graph(n):
     return TrackGraph(n, n - 1, slot_ptr, out_ptr, np.arange(n - 1, dtype=np.int32), node, slot)
 
 
-@pytest.mark.parametrize("csr", ["1", "0"])
+@pytest.mark.parametrize("csr", list(_CSR_MODES))
 @pytest.mark.parametrize("poll", ["1", "0"])
 @pytest.mark.parametrize("schedule", [True, False])
 def test_tag_propagate_long_run(schedule, poll, csr, monkeypatch):
     """300 sweeps in one gtf_tag_propagate call: batches of 2 .. 64 launches, the flip-counter
     ring (128 sweeps) wrapped twice with every sweep zeroing the next one's counters"""
     monkeypatch.setenv("GTF_TAG_POLL", poll)
-    monkeypatch.setenv("GTF_TAG_CSR", csr)
+    _csr_env(monkeypatch, csr)
     import ctypes
     import torch
     from gtf import _native as nat
@@ -248,8 +264,8 @@ def test_tag_propagate_tags_beyond_int32(shape, monkeypatch):
     radius = torch.from_numpy(np.ascontiguousarray(g.node["xyzr"][:, 3], dtype=np.float64)).to(d.device)
     nb = L.gtf_tag_workspace_bytes(g.n_nodes, g.n_edges)
     res = {}
-    for csr in ("1", "0"):
-        monkeypatch.setenv("GTF_TAG_CSR", csr)
+    for csr, mode in (("1", "packed"), ("0", "mask")):
+        _csr_env(monkeypatch, mode)
         tags = torch.from_numpy(t0).to(d.device)
         ws = torch.full((nb,), 0xFF, dtype=torch.uint8, device=d.device)
         flips = (ctypes.c_int32 * 64)()
@@ -267,6 +283,59 @@ def test_tag_propagate_tags_beyond_int32(shape, monkeypatch):
         off = (1 << 40) if shape == "all_wide" else -(1 << 40)
         kept = extra["tags"] >= 0
         assert np.array_equal(res["1"][1][kept], extra["tags"][kept] + off)
+
+
+_ORACLE_CACHE = {}
+
+
+def _star_graph(k, r0):
+    """node 0 sends to nodes 1..k (one slot each), receiver radius 1..k against node 0's r0:
+    the receivers at or inside r0 are kept; receiver v also sends to v + 1 (a chain behind the
+    star, so the maximum travels several sweeps)"""
+    from gtf.graph import TrackGraph, NODE_FIELDS, SLOT_FIELDS, empty_arrays
+    n = k + 1
+    src = np.concatenate([np.zeros(k, np.int64), np.arange(1, k)])        # star, then chain v -> v + 1
+    dst = np.concatenate([np.arange(1, k + 1), np.arange(2, k + 1)])
+    order = np.lexsort((src, dst))   # slots grouped by receiver
+    src, dst = src[order], dst[order]
+    ns = src.size
+    node = empty_arrays(NODE_FIELDS, n)
+    slot = empty_arrays(SLOT_FIELDS, ns)
+    node["gnn"][:] = 1.0
+    node["xyzr"][:] = 1.0
+    node["xyzr"][1:, 3] = np.arange(k, 0, -1, dtype=np.float64)   # v -> v + 1 kept: radius falls
+    node["xyzr"][0, 3] = r0
+    node["tag"][:] = np.random.default_rng(5).permutation(n)
+    node["layer"][:] = np.arange(n) % 7
+    slot["slot_src"][:] = src
+    slot["slot_key"][:] = np.arange(ns)
+    slot["is_edge"][:] = 1
+    slot["act"][:] = 1
+    slot_ptr = np.searchsorted(dst, np.arange(n + 1)).astype(np.int32)
+    eo = np.lexsort((dst, src))      # out-edges grouped by sender
+    out_ptr = np.searchsorted(src[eo], np.arange(n + 1)).astype(np.int32)
+    return TrackGraph(n, ns, slot_ptr, out_ptr, eo.astype(np.int32), node, slot)
+
+
+@pytest.mark.parametrize("csr", list(_CSR_MODES))
+@pytest.mark.parametrize("schedule", [True, False])
+def test_tag_propagate_saturated_kept_count(schedule, csr, monkeypatch):
+    """a node with 1,200 out-edges, 700 of them kept: past the packed word's 511 (the count then
+    read from its own word), on the lane-group and thread-per-node prepare kernels; the tags and
+    flips equal the oracle's"""
+    _csr_env(monkeypatch, csr)
+    import torch
+    from gtf.device import DeviceGraph
+    g = _star_graph(1200, 700.5)
+    d = DeviceGraph(g, schedule=schedule)
+    tags = torch.from_numpy(np.ascontiguousarray(g.node["tag"], dtype=np.int64)).to(d.device)
+    radius = torch.from_numpy(np.ascontiguousarray(g.node["xyzr"][:, 3])).to(d.device)
+    flips = d.tag_propagation_dev(tags, radius, threshold=0.0, max_sweeps=5000)
+    if "star" not in _ORACLE_CACHE:   # (920 sweeps of the Python oracle: once per module)
+        _ORACLE_CACHE["star"] = O.tag_propagation(g, 0.0)
+    want_tags, want_flips = _ORACLE_CACHE["star"]
+    assert flips == list(want_flips) and len(flips) > 2
+    assert np.array_equal(tags.cpu().numpy(), want_tags)
 
 
 def test_workspace_init_contract():

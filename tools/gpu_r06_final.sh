@@ -29,7 +29,8 @@ print('c5', c5.get('f64',{}).get('kernel_ms'), c5.get('f64',{}).get('roofline',{
 a16=(d.get('other_path_stages') or {}).get('a16_tag_propagation',{})
 print('a16', {k:a16.get(k) for k in ('stage_wall_ms','prepare_call_ms','sweep_call_ms','sweeps','flips','stage_over_kernels')})
 a16c3=c3.get('a16_tag_propagation') or {}
-print('a16 c3', {k:a16c3.get(k) for k in ('stage_wall_ms','sweep_call_ms','sweeps','flips','frac_of_peak')})
+print('a16 c3', {k:a16c3.get(k) for k in ('stage_wall_ms','sweep_call_ms','sweeps','flips','frac_of_peak','stage_sweep')})
+print('a16 c4 stage_sweep', a16.get('stage_sweep'))
 print('cpu', d.get('cpu_baseline',{}).get('value'), d.get('cpu_baseline',{}).get('seconds'))
 PY
 cd /tmp && export TMPDIR=/tmp

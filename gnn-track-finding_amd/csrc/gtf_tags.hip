@@ -261,7 +261,9 @@ __global__ void __launch_bounds__(BLOCK) k_tag_prepare_sched(gtf_graph g, const 
                                                              uint8_t* processed, PrepBuckets pb, int32_t* zero,
                                                              int nzero, TagCsr csr) {
     zero_words(zero, nzero);
-    int b = blockIdx.x;
+    // (XCD-contiguous block ranges: a run of one bucket's senders -- neighbours of each other --
+    // shares one XCD's L2 for the radius gathers)
+    int b = gtf::xcd_local(blockIdx.x, gridDim.x);
     if (b < pb.blocks[0]) {
         prep_group<4>(g, radius, keep, processed, pb.list[0], pb.lanes[0], pb.count[0], b, csr);
     } else if ((b -= pb.blocks[0]) < pb.blocks[1]) {
@@ -426,7 +428,7 @@ __global__ void __launch_bounds__(BLOCK) k_tag_sweep_sched(gtf_graph g, const ui
                                                            const int64_t* tin, int64_t* tout, int32_t* flips,
                                                            int nsh, TagBuckets tb, TagCtl ctl) {
     if (tag_skip(ctl)) return;
-    int b = blockIdx.x, flipped = 0;   // (bit 0 flipped, bit 1 processed: tag_group*)
+    int b = gtf::xcd_local(blockIdx.x, gridDim.x), flipped = 0;   // (bit 0 flipped, bit 1 processed: tag_group*)
     if (b < tb.blocks[0]) {
         flipped = tb.lanes[0] ? tag_group_lanes<4>(g, keep, processed, tin, tout, tb.list[0], tb.lanes[0], tb.count[0], b)
                               : tag_group<4>(g, keep, processed, tin, tout, tb.list[0], tb.count[0], b);
@@ -875,6 +877,14 @@ static int tag_sweep_r() {   // kept indices per node in the second round of a 2
     const char* e = getenv("GTF_TAG_R");   // (GTF_TAG_R 2 / 4; C3: 2 at least as fast)
     return e && e[0] == '4' ? 4 : 2;
 }
+// sweeps in the first batch (then doubling): 4 -- a sweep enqueued past the stop returns at once
+// (~1 us), a batch boundary costs a report and a host round trip (~10-15 us), and the stage
+// runs 1 sweep (+1 that sees the stop) on ascending tags, 7-10 on the descending ones
+static int32_t tag_first_batch() {
+    const char* e = getenv("GTF_TAG_BATCH0");   // (A/B: 1, 2, 4, 8 ...)
+    const int v = e && e[0] ? atoi(e) : 4;
+    return v < 1 ? 1 : (v > TAG_MAX_BATCH ? TAG_MAX_BATCH : v);
+}
 static bool tag_kword_enabled() {
     const char* e = getenv("GTF_TAG_KWORD");   // 0: the count and the offset per node
     return !(e && e[0] == '0');
@@ -889,11 +899,11 @@ static int32_t* tag_readback_buffer() {
 }
 
 // The whole stage behind one call: prepare, then the sweeps (the loop of
-// tag_propagation.py:130-164, first sweep unconditional) in batches of 2, 4, 8, ... launches
-// whose stop test runs on the device (TagCtl), the tag arrays ping-ponging between `tags` and
-// the workspace; the host reads the batch's flip counters once per batch (one stream
-// synchronisation) and stops as soon as the rule has. The final tags land in `tags` by a
-// device copy when the executed count is odd.
+// tag_propagation.py:130-164, first sweep unconditional) in batches of 4, 8, 16, ... launches
+// whose stop test runs on the device (TagCtl), over the compact kept lists with the tags
+// ping-ponging between two int32 arrays (or `tags` and the workspace's int64 copy); the host
+// reads the batch's flip counters once per batch and stops as soon as the rule has. The final
+// tags land in `tags` by a device copy.
 int gtf_tag_propagate(const gtf_graph* g, const double* radius, int64_t* tags, double flip_threshold,
                       int32_t max_sweeps, int32_t* flips_out, int32_t* sweeps_out, void* workspace,
                       size_t workspace_bytes, gtf_stream_t stream) {
@@ -943,7 +953,7 @@ int gtf_tag_propagate(const gtf_graph* g, const double* radius, int64_t* tags, d
     if (int rc = tag_prepare(g, radius, csr ? nullptr : keep, csr ? nullptr : proc, nullptr, false, st, hdr,
                              64 + 2 * (int)TAG_CTR, lists))
         return rc;
-    int32_t s = 0, batch = 2, executed = 0;
+    int32_t s = 0, batch = tag_first_batch(), executed = 0;
     int32_t* host = poll ? nullptr : tag_readback_buffer();   // the header words, then the ring
     if (!poll && !host) return hip_fail("gtf_tag_propagate: page-locked read-back buffer");
     bool stopped = false;

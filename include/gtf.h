@@ -416,11 +416,14 @@ int gtf_tag_sweep(const gtf_graph* g, const uint8_t* keep, const uint8_t* proces
  * max_sweeps; the first sweep always runs). tags: device int64 [n_nodes], the initial tags
  * in, the final tags out; flips_out: host int32 [max_sweeps] (or NULL), the flip count of
  * every sweep; *sweeps_out: the number of sweeps. workspace: device, at least
- * gtf_tag_workspace_bytes(n_nodes, n_edges) bytes. The sweeps go out in batches of 2, 4, 8,
- * ... 64 launches with the stop rule evaluated on the device; the host waits once per batch,
- * for a small report (the stop-rule words and the batch's flip totals) the device writes into
- * mapped page-locked memory the host polls (environment GTF_TAG_POLL=0: a device-to-host copy
- * and a stream synchronisation instead). */
+ * gtf_tag_workspace_bytes(n_nodes, n_edges) bytes. The prepare launch builds a compact list
+ * of every node's kept out-neighbours in the workspace, and the sweeps read those lists with
+ * the tags carried as int32 while every tag fits (int64 from the first value that does not;
+ * environment GTF_TAG_CSR=0: the keep-mask sweeps of gtf_tag_sweep). The sweeps go out in
+ * batches of 4, 8, 16, ... 64 launches with the stop rule evaluated on the device; the host
+ * waits once per batch, for a small report (the stop-rule words and the batch's flip totals)
+ * the device writes into mapped page-locked memory the host polls (environment
+ * GTF_TAG_POLL=0: a device-to-host copy and a stream synchronisation instead). */
 size_t gtf_tag_workspace_bytes(int32_t n_nodes, int32_t n_edges);
 int gtf_tag_propagate(const gtf_graph* g, const double* radius, int64_t* tags, double flip_threshold,
                       int32_t max_sweeps, int32_t* flips_out, int32_t* sweeps_out, void* workspace,

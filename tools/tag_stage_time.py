@@ -2,7 +2,7 @@
 on C4 / C3 after one pass, over the compact kept lists with int32 tags (GTF_TAG_CSR=1; csr1 one
 packed word per node at the defaults; csr1r4: four kept indices per node in the sweep's second
 round (GTF_TAG_R), csr1n1 / csr1n2: one / two nodes per sweep thread (GTF_TAG_NPT), csr1p1 / csr1gp: the one-node-
-per-thread / lane-group prepare (GTF_TAG_PREP_NPT)) against the keep-mask sweeps
+per-thread / lane-group prepare (GTF_TAG_PREP_NPT), csr1b2: a first batch of 2 sweeps (GTF_TAG_BATCH0)) against the keep-mask sweeps
 (GTF_TAG_CSR=0), both initial tag orders; wall time median of K calls,
 and the tags / flips of the two forms compared word for word (diagnostics).
 usage: python tools/tag_stage_time.py c3|c4 [K [mode,mode...]]"""
@@ -38,8 +38,8 @@ def main():
         t_init = torch.from_numpy(np.ascontiguousarray(d._to_dev_nodes(t))).to(d.device)
         outs = {}
         modes = (("1", {}), ("1r4", {"GTF_TAG_R": "4"}), ("1n1", {"GTF_TAG_NPT": "1"}), ("1n2", {"GTF_TAG_NPT": "2"}),
-                 ("1p1", {"GTF_TAG_PREP_NPT": "1"}), ("1gp", {"GTF_TAG_PREP_NPT": "0"}), ("0", {"GTF_TAG_CSR": "0"}))
-        keys = ("GTF_TAG_CSR", "GTF_TAG_KWORD", "GTF_TAG_NPT", "GTF_TAG_PREP_NPT", "GTF_TAG_R")
+                 ("1p1", {"GTF_TAG_PREP_NPT": "1"}), ("1gp", {"GTF_TAG_PREP_NPT": "0"}), ("1b2", {"GTF_TAG_BATCH0": "2"}), ("0", {"GTF_TAG_CSR": "0"}))
+        keys = ("GTF_TAG_CSR", "GTF_TAG_KWORD", "GTF_TAG_NPT", "GTF_TAG_PREP_NPT", "GTF_TAG_R", "GTF_TAG_BATCH0")
         for csr, env in modes:
             if only and csr not in only:
                 continue

@@ -122,20 +122,27 @@ def test_tag_propagate_one_call():
                                ctypes.c_void_p(ws.data_ptr()), nb - 1, d.stream) != 0
 
 
-# GTF_TAG_CSR, GTF_TAG_KWORD, GTF_TAG_NPT, GTF_TAG_PREP_NPT, GTF_TAG_R ("": the default)
-_CSR_MODES = {"packed": ("1", "1", "", "", ""), "packed_n2": ("1", "1", "2", "2", "2"),
-              "packed_n2_r4": ("1", "1", "2", "0", "4"), "packed_n4": ("1", "1", "4", "4", "4"),
-              "counts_thread_prep": ("1", "0", "1", "1", ""), "counts_group_prep": ("1", "0", "2", "0", ""),
-              "mask": ("0", "1", "", "", "")}
+# gtf_tag_propagate's forms (environment; unset: the default)
+_CSR_MODES = {
+    "default": {},
+    "packed_n1": {"GTF_TAG_NPT": "1"},
+    "packed_n2": {"GTF_TAG_NPT": "2", "GTF_TAG_PREP_NPT": "2", "GTF_TAG_R": "2"},
+    "packed_n2_r4": {"GTF_TAG_NPT": "2", "GTF_TAG_PREP_NPT": "0", "GTF_TAG_R": "4"},
+    "packed_n4": {"GTF_TAG_NPT": "4", "GTF_TAG_PREP_NPT": "4", "GTF_TAG_R": "4"},
+    "counts_thread_prep": {"GTF_TAG_KWORD": "0", "GTF_TAG_NPT": "1", "GTF_TAG_PREP_NPT": "1"},
+    "counts_group_prep": {"GTF_TAG_KWORD": "0", "GTF_TAG_NPT": "2", "GTF_TAG_PREP_NPT": "0"},
+    "mask": {"GTF_TAG_CSR": "0"},
+}
+_TAG_ENV = ("GTF_TAG_CSR", "GTF_TAG_KWORD", "GTF_TAG_NPT", "GTF_TAG_PREP_NPT", "GTF_TAG_R")
 
 
 def _csr_env(monkeypatch, mode):
     """gtf_tag_propagate's sweep form: compact kept lists with one packed word per node (1, 2 or
     4 nodes per thread in the prepare and the sweeps, 2 or 4 kept indices per node in a sweep's
-    second round), with a count and an offset per node built by the one-node-per-thread or the
+    second round) or a count and an offset per node, built by the one-node-per-thread or the
     lane-group prepare, or the keep-mask sweeps (GTF_TAG_CSR=0)"""
-    for k, v in zip(("GTF_TAG_CSR", "GTF_TAG_KWORD", "GTF_TAG_NPT", "GTF_TAG_PREP_NPT", "GTF_TAG_R"), _CSR_MODES[mode]):
-        monkeypatch.setenv(k, v)
+    for k in _TAG_ENV:
+        monkeypatch.setenv(k, _CSR_MODES[mode].get(k, ""))
 
 
 @pytest.mark.parametrize("csr", list(_CSR_MODES))
@@ -264,7 +271,7 @@ def test_tag_propagate_tags_beyond_int32(shape, monkeypatch):
     radius = torch.from_numpy(np.ascontiguousarray(g.node["xyzr"][:, 3], dtype=np.float64)).to(d.device)
     nb = L.gtf_tag_workspace_bytes(g.n_nodes, g.n_edges)
     res = {}
-    for csr, mode in (("1", "packed"), ("0", "mask")):
+    for csr, mode in (("1", "default"), ("0", "mask")):
         _csr_env(monkeypatch, mode)
         tags = torch.from_numpy(t0).to(d.device)
         ws = torch.full((nb,), 0xFF, dtype=torch.uint8, device=d.device)

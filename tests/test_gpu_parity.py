@@ -271,7 +271,8 @@ def test_tag_propagate_tags_beyond_int32(shape, monkeypatch):
     radius = torch.from_numpy(np.ascontiguousarray(g.node["xyzr"][:, 3], dtype=np.float64)).to(d.device)
     nb = L.gtf_tag_workspace_bytes(g.n_nodes, g.n_edges)
     res = {}
-    for csr, mode in (("1", "default"), ("0", "mask")):
+    for csr, mode in (("1", "default"), ("n2", "packed_n2"), ("n4", "packed_n4"), ("ct", "counts_thread_prep"),
+                      ("0", "mask")):
         _csr_env(monkeypatch, mode)
         tags = torch.from_numpy(t0).to(d.device)
         ws = torch.full((nb,), 0xFF, dtype=torch.uint8, device=d.device)
@@ -283,8 +284,9 @@ def test_tag_propagate_tags_beyond_int32(shape, monkeypatch):
                                       ctypes.c_void_p(ws.data_ptr()), nb, d.stream))
         torch.cuda.synchronize()
         res[csr] = (list(flips[:sweeps.value]), tags.cpu().numpy())
-    assert res["1"][0] == res["0"][0]
-    assert np.array_equal(res["1"][1], res["0"][1])
+    for m in ("1", "n2", "n4", "ct"):   # (every compact-list form, its int64 fallback included)
+        assert res[m][0] == res["0"][0]
+        assert np.array_equal(res[m][1], res["0"][1])
     if shape != "one_wide":   # (a shift changes no comparison)
         assert res["1"][0] == list(extra["flips"])
         off = (1 << 40) if shape == "all_wide" else -(1 << 40)

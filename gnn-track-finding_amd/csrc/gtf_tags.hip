@@ -192,16 +192,40 @@ __device__ __forceinline__ void prep_group(const gtf_graph& g, const double* rad
     }
 }
 
+// exclusive prefix of v over the block's threads in thread order (every thread of the block calls it)
+__device__ __forceinline__ int block_excl_scan(int v) {
+    __shared__ int s_tot[BLOCK / 64];
+    const int lane = (int)threadIdx.x & 63, wid = (int)threadIdx.x >> 6;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) s_tot[wid] = x;
+    __syncthreads();
+    int add = 0;
+#pragma unroll
+    for (int w = 0; w < BLOCK / 64; w++) add += w < wid ? s_tot[w] : 0;
+    __syncthreads();   // (s_tot is reused by the next call)
+    return add + x - v;
+}
+
 // gtf_tag_propagate's prepare in the compact-list form (no keep mask, no processed flags: its
 // sweeps read neither), NPT nodes per thread BLOCK apart with their loads interleaved as in
 // sweep_csr_nodes: the out-list bounds and own radius of each, its first four out-neighbours,
-// their radii (longer lists in steps of four); the kept ones written to the front of the node's
-// out-range, in out-list order.
+// their radii (longer lists in steps of four); the kept ones in out-list order. Where they go:
+// - pack = 0: the front of the node's own out-range (kidx[out_ptr[u] ...]);
+// - pack = 1 (packed words only: the word carries the offset): back to back in node order from
+//   the start of the out-range of the node's run of BLOCK nodes (a block scan of the counts; a
+//   run's kept lists never outgrow its out-edges), so the lists a sweep wave reads are dense --
+//   half the kidx lines of the out-range fronts on C3, where about half the out-edges are kept.
 template <int NPT>
 __global__ void __launch_bounds__(BLOCK) k_tag_prepare_csr(gtf_graph g, const double* radius, TagCsr csr,
-                                                           int32_t* zero, int nzero) {
+                                                           int32_t* zero, int nzero, int pack) {
     zero_words(zero, nzero);
-    const int u0 = gtf::xcd_local(blockIdx.x, gridDim.x) * BLOCK * NPT + (int)threadIdx.x;
+    const int blk = gtf::xcd_local(blockIdx.x, gridDim.x);
+    const int u0 = blk * BLOCK * NPT + (int)threadIdx.x;
     int o0[NPT], o1[NPT];
     double ru[NPT];
 #pragma unroll
@@ -227,14 +251,9 @@ __global__ void __launch_bounds__(BLOCK) k_tag_prepare_csr(gtf_graph g, const do
     for (int j = 0; j < NPT; j++)
 #pragma unroll
         for (int r = 0; r < R; r++) rw[j][r] = o0[j] + r < o1[j] ? radius[w[j][r]] : 0.0;
-#pragma unroll
-    for (int j = 0; j < NPT; j++) {
-        const int u = u0 + j * BLOCK;
-        if (u >= g.n_nodes) continue;
+    // the kept out-neighbours past the first R of node j: counted, or (write) stored from kidx[at]
+    auto rest = [&](int j, bool write, int at) {
         int nk = 0;
-#pragma unroll
-        for (int r = 0; r < R; r++)
-            if (o0[j] + r < o1[j] && !(rw[j][r] > ru[j])) csr.kidx[o0[j] + nk++] = w[j][r];
         for (int i = o0[j] + R; i < o1[j]; i += R) {   // longer lists: R independent loads per step
             int x[R];
             double rx[R];
@@ -244,9 +263,42 @@ __global__ void __launch_bounds__(BLOCK) k_tag_prepare_csr(gtf_graph g, const do
             for (int r = 0; r < R; r++) rx[r] = i + r < o1[j] ? radius[x[r]] : 0.0;
 #pragma unroll
             for (int r = 0; r < R; r++)
-                if (i + r < o1[j] && !(rx[r] > ru[j])) csr.kidx[o0[j] + nk++] = x[r];
+                if (i + r < o1[j] && !(rx[r] > ru[j])) {
+                    if (write) csr.kidx[at + nk] = x[r];
+                    nk++;
+                }
         }
-        csr_node(csr, u, o0[j], nk);
+        return nk;
+    };
+    int base[NPT];
+#pragma unroll
+    for (int j = 0; j < NPT; j++) base[j] = o0[j];
+    if (pack) {   // (uniform) the counts first, then every node's place in its run
+        int nk[NPT];
+#pragma unroll
+        for (int j = 0; j < NPT; j++) {
+            nk[j] = 0;
+#pragma unroll
+            for (int r = 0; r < R; r++) nk[j] += o0[j] + r < o1[j] && !(rw[j][r] > ru[j]);
+            if (o1[j] - o0[j] > R) nk[j] += rest(j, false, 0);
+        }
+#pragma unroll
+        for (int j = 0; j < NPT; j++) {
+            const int first = blk * BLOCK * NPT + j * BLOCK;   // the run's first node
+            const int run0 = first < g.n_nodes ? g.out_ptr[first] : 0;
+            base[j] = run0 + block_excl_scan(nk[j]);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < NPT; j++) {
+        const int u = u0 + j * BLOCK;
+        if (u >= g.n_nodes) continue;
+        int nk = 0;
+#pragma unroll
+        for (int r = 0; r < R; r++)
+            if (o0[j] + r < o1[j] && !(rw[j][r] > ru[j])) csr.kidx[base[j] + nk++] = w[j][r];
+        if (o1[j] - o0[j] > R) nk += rest(j, true, base[j] + nk);
+        csr_node(csr, u, base[j], nk);
     }
 }
 
@@ -688,6 +740,11 @@ static int tag_prep_npt(int n) {
     return n >= 2 * BLOCK * 512 ? 1 : 0;
 }
 
+static bool tag_pack_enabled() {   // (read per call: a test switches it in-process)
+    const char* e = getenv("GTF_TAG_PACK");   // 0: each kept list at the front of its node's out-range
+    return !(e && e[0] == '0');
+}
+
 // zero_count: n_processed zeroed here (else the caller has, or the prepare launch zeroes the
 // nzero words at `zero`, n_processed among them)
 static int tag_prepare(const gtf_graph* g, const double* radius, uint8_t* keep, uint8_t* processed,
@@ -702,7 +759,7 @@ static int tag_prepare(const gtf_graph* g, const double* radius, uint8_t* keep, 
         const int npt = tag_prep_npt(g->n_nodes);
         auto kern = npt == 4 ? k_tag_prepare_csr<4> : npt == 2 ? k_tag_prepare_csr<2> : k_tag_prepare_csr<1>;
         hipLaunchKernelGGL(kern, dim3((g->n_nodes + BLOCK * npt - 1) / (BLOCK * npt)), dim3(BLOCK), 0, st, *g,
-                           radius, csr, zero, nzero);
+                           radius, csr, zero, nzero, csr.kword && tag_pack_enabled() ? 1 : 0);
     } else if (g->n_nodes > 0 && g->out_sched) {   // lane groups over the sender schedule
         PrepBuckets pb;
         const int cnt[3] = {g->n_o4, g->n_o8, g->n_o16}, gs[3] = {4, 8, 16};

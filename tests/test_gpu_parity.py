@@ -129,18 +129,21 @@ _CSR_MODES = {
     "packed_n2": {"GTF_TAG_NPT": "2", "GTF_TAG_PREP_NPT": "2", "GTF_TAG_R": "2"},
     "packed_n2_r4": {"GTF_TAG_NPT": "2", "GTF_TAG_PREP_NPT": "0", "GTF_TAG_R": "4"},
     "packed_n4": {"GTF_TAG_NPT": "4", "GTF_TAG_PREP_NPT": "4", "GTF_TAG_R": "4"},
+    "packed_prep1": {"GTF_TAG_PREP_NPT": "1"},
+    "unpacked_n2": {"GTF_TAG_NPT": "2", "GTF_TAG_PREP_NPT": "2", "GTF_TAG_PACK": "0"},
     "counts_thread_prep": {"GTF_TAG_KWORD": "0", "GTF_TAG_NPT": "1", "GTF_TAG_PREP_NPT": "1"},
     "counts_group_prep": {"GTF_TAG_KWORD": "0", "GTF_TAG_NPT": "2", "GTF_TAG_PREP_NPT": "0"},
     "mask": {"GTF_TAG_CSR": "0"},
 }
-_TAG_ENV = ("GTF_TAG_CSR", "GTF_TAG_KWORD", "GTF_TAG_NPT", "GTF_TAG_PREP_NPT", "GTF_TAG_R")
+_TAG_ENV = ("GTF_TAG_CSR", "GTF_TAG_KWORD", "GTF_TAG_NPT", "GTF_TAG_PREP_NPT", "GTF_TAG_R", "GTF_TAG_PACK")
 
 
 def _csr_env(monkeypatch, mode):
     """gtf_tag_propagate's sweep form: compact kept lists with one packed word per node (1, 2 or
     4 nodes per thread in the prepare and the sweeps, 2 or 4 kept indices per node in a sweep's
-    second round) or a count and an offset per node, built by the one-node-per-thread or the
-    lane-group prepare, or the keep-mask sweeps (GTF_TAG_CSR=0)"""
+    second round; the thread prepare's lists back to back per run of 256 nodes, or at the front
+    of each node's out-range with GTF_TAG_PACK=0) or a count and an offset per node, built by the
+    one-node-per-thread or the lane-group prepare, or the keep-mask sweeps (GTF_TAG_CSR=0)"""
     for k in _TAG_ENV:
         monkeypatch.setenv(k, _CSR_MODES[mode].get(k, ""))
 
@@ -271,8 +274,8 @@ def test_tag_propagate_tags_beyond_int32(shape, monkeypatch):
     radius = torch.from_numpy(np.ascontiguousarray(g.node["xyzr"][:, 3], dtype=np.float64)).to(d.device)
     nb = L.gtf_tag_workspace_bytes(g.n_nodes, g.n_edges)
     res = {}
-    for csr, mode in (("1", "default"), ("n2", "packed_n2"), ("n4", "packed_n4"), ("ct", "counts_thread_prep"),
-                      ("0", "mask")):
+    for csr, mode in (("1", "default"), ("n2", "packed_n2"), ("n4", "packed_n4"), ("p1", "packed_prep1"),
+                      ("u2", "unpacked_n2"), ("ct", "counts_thread_prep"), ("0", "mask")):
         _csr_env(monkeypatch, mode)
         tags = torch.from_numpy(t0).to(d.device)
         ws = torch.full((nb,), 0xFF, dtype=torch.uint8, device=d.device)
@@ -284,7 +287,7 @@ def test_tag_propagate_tags_beyond_int32(shape, monkeypatch):
                                       ctypes.c_void_p(ws.data_ptr()), nb, d.stream))
         torch.cuda.synchronize()
         res[csr] = (list(flips[:sweeps.value]), tags.cpu().numpy())
-    for m in ("1", "n2", "n4", "ct"):   # (every compact-list form, its int64 fallback included)
+    for m in ("1", "n2", "n4", "p1", "u2", "ct"):   # (every compact-list form, its int64 fallback included)
         assert res[m][0] == res["0"][0]
         assert np.array_equal(res[m][1], res["0"][1])
     if shape != "one_wide":   # (a shift changes no comparison)

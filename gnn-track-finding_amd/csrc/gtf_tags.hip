@@ -673,6 +673,113 @@ __global__ void __launch_bounds__(BLOCK) k_tag_sweep_csr(gtf_graph g, TagCsr csr
     block_sum_add2(nflip, flips, nsh, nproc, ctl.count_processed);
 }
 
+// The wave-cooperative sweep over block-packed lists (k_tag_prepare_csr with pack: a 64-node
+// group's kept lists are back to back, from its first node's offset on). A wave takes NG groups
+// of 64 consecutive nodes: the packed words and own tags (one node per lane), then the group's
+// whole list range in coalesced loads (lane l: entries l, l + 64, ...), each entry's neighbour tag
+// gathered by the lane that loaded it and staged in LDS, and every lane's maximum over its own
+// entries from there. Against sweep_csr_nodes (each lane loading its own node's entries, R at a
+// time, predicated on its count), the index loads are whole-wave and dense and every gather lane
+// is a kept edge: about half the vector memory instructions per node. A group whose lists hold
+// more than COOP_CAP entries takes the per-lane loop (wave-uniform).
+constexpr int COOP_CAP = 256;
+template <int NG, typename T>
+__device__ __forceinline__ void sweep_coop_nodes(const gtf_graph& g, const TagCsr& csr, const T* tin, T* tout,
+                                                 int32_t* t32, int32_t* ovf, int n0, T* buf, int& nflip, int& nproc) {
+    const int lane = (int)threadIdx.x & 63;
+    int c[NG], b[NG];
+    T t[NG];
+#pragma unroll
+    for (int j = 0; j < NG; j++) {
+        const int u = n0 + j * 64 + lane;
+        c[j] = 0;
+        b[j] = 0;
+        t[j] = 0;
+        if (u < g.n_nodes) {
+            const uint32_t w = csr.kword[u];
+            b[j] = (int)(w >> KW_BITS);
+            c[j] = (int)(w & KW_SAT);
+            t[j] = tin[u];
+        }
+    }
+    int w0[NG], tot[NG];
+    bool fits = true;
+#pragma unroll
+    for (int j = 0; j < NG; j++) {
+        const int g0 = n0 + j * 64;   // (wave-uniform)
+        if (c[j] == (int)KW_SAT) c[j] = csr.kcnt[g0 + lane];   // (a saturated count)
+        const int last = g.n_nodes - 1 - g0 < 63 ? g.n_nodes - 1 - g0 : 63;   // the group's last node's lane
+        w0[j] = __builtin_amdgcn_readfirstlane(b[j]);
+        tot[j] = last >= 0 ? __shfl(b[j] + c[j], last) - w0[j] : 0;
+        fits = fits && tot[j] <= COOP_CAP;
+    }
+    T m[NG];
+    if (fits) {   // (uniform)
+        constexpr int NI = COOP_CAP / 64;
+        int x[NG][NI];
+#pragma unroll
+        for (int j = 0; j < NG; j++)
+#pragma unroll
+            for (int i = 0; i < NI; i++)
+                x[j][i] = i * 64 < tot[j] && i * 64 + lane < tot[j] ? csr.kidx[w0[j] + i * 64 + lane] : -1;
+        T v[NG][NI];
+#pragma unroll
+        for (int j = 0; j < NG; j++)
+#pragma unroll
+            for (int i = 0; i < NI; i++) v[j][i] = x[j][i] >= 0 ? tin[x[j][i]] : (T)0;
+#pragma unroll
+        for (int j = 0; j < NG; j++)
+#pragma unroll
+            for (int i = 0; i < NI; i++)
+                if (i * 64 < tot[j]) buf[j * COOP_CAP + i * 64 + lane] = v[j][i];
+        gtf::wave_lds_sync();
+#pragma unroll
+        for (int j = 0; j < NG; j++) {
+            m[j] = t[j];
+            const T* s = buf + j * COOP_CAP + (b[j] - w0[j]);
+            for (int k = 0; k < c[j]; k++) {
+                const T y = s[k];
+                m[j] = y > m[j] ? y : m[j];
+            }
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < NG; j++) m[j] = c[j] > 0 ? tag_max_csr<T>(tin, csr.kidx, b[j], c[j], t[j]) : t[j];
+    }
+#pragma unroll
+    for (int j = 0; j < NG; j++) {
+        const int u = n0 + j * 64 + lane;
+        const bool in = u < g.n_nodes;
+        if (in) {
+            tout[u] = m[j];
+            if (t32) {
+                t32[u] = (int32_t)m[j];
+                if ((int64_t)m[j] != (int64_t)(int32_t)m[j]) atomicOr(ovf, 1);   // (only where a value does not fit)
+            }
+        }
+        nflip += (int)__popcll(__ballot(in && m[j] != t[j]));
+        nproc += (int)__popcll(__ballot(in && c[j] > 0));
+    }
+}
+
+template <int NG>
+__global__ void __launch_bounds__(BLOCK) k_tag_sweep_coop(gtf_graph g, TagCsr csr, const int64_t* tin64, int64_t* tout64,
+                                                          const int32_t* tin32, int32_t* tout32, int first,
+                                                          int32_t* ovf, int32_t* flips, int nsh, TagCtl ctl) {
+    if (tag_skip(ctl)) return;
+    __shared__ int64_t s_buf[BLOCK / 64][NG * COOP_CAP];   // (the int32 sweeps use half of it)
+    const int wv = (int)threadIdx.x >> 6;
+    const int n0 = (gtf::xcd_local(blockIdx.x, gridDim.x) * (BLOCK / 64) + wv) * 64 * NG;
+    int nflip = 0, nproc = 0;
+    if (first || *ovf)   // (uniform)
+        sweep_coop_nodes<NG, int64_t>(g, csr, tin64, tout64, first ? tout32 : nullptr, ovf, n0, s_buf[wv], nflip,
+                                      nproc);
+    else
+        sweep_coop_nodes<NG, int32_t>(g, csr, tin32, tout32, nullptr, nullptr, n0,
+                                      reinterpret_cast<int32_t*>(s_buf[wv]), nflip, nproc);
+    block_sum_add2(nflip, flips, nsh, nproc, ctl.count_processed);
+}
+
 // the final tags into the caller's int64 array after a run of CSR sweeps: from the int32 pair
 // (sweep q wrote buffer (q + 1) % 2, so nexec sweeps end in buffer nexec % 2), or -- when a
 // value did not fit -- from the int64 pair as k_tag_final does
@@ -942,6 +1049,14 @@ static int32_t tag_first_batch() {
     const int v = e && e[0] ? atoi(e) : 4;
     return v < 1 ? 1 : (v > TAG_MAX_BATCH ? TAG_MAX_BATCH : v);
 }
+static int tag_coop_groups() {   // the wave-cooperative sweep on packed lists: 64-node groups per wave (0: off)
+    const char* e = getenv("GTF_TAG_COOP");
+    if (e && e[0]) {
+        const int v = atoi(e);
+        return v == 1 || v == 2 || v == 4 ? v : 0;
+    }
+    return 2;
+}
 static bool tag_kword_enabled() {
     const char* e = getenv("GTF_TAG_KWORD");   // 0: the count and the offset per node
     return !(e && e[0] == '0');
@@ -1001,6 +1116,9 @@ int gtf_tag_propagate(const gtf_graph* g, const double* radius, int64_t* tags, d
     const bool packed = csr && (size_t)n_edges < ((size_t)1 << (32 - KW_BITS)) && tag_kword_enabled();
     const TagCsr lists{csr ? kcnt : nullptr, kidx, packed ? kword : nullptr};
     const int npt = tag_nodes_per_thread(g->n_nodes);
+    // the wave-cooperative sweep where the thread prepare packs the lists (graphs the 2- / 4-node
+    // sweeps take)
+    const int coop = packed && npt > 1 && tag_prep_npt(g->n_nodes) > 0 && tag_pack_enabled() ? tag_coop_groups() : 0;
     int32_t* ovf = hdr + 3;   // (zeroed with the header by the prepare launch)
     *sweeps_out = 0;
     // the header words and the first sweep's counter shards zeroed by the prepare launch; every
@@ -1046,7 +1164,12 @@ int gtf_tag_propagate(const gtf_graph* g, const double* radius, int64_t* tags, d
                     auto kern = npt == 1   ? k_tag_sweep_csr1
                                 : npt == 4 ? (tag_sweep_r() == 4 ? k_tag_sweep_csr<4, 4> : k_tag_sweep_csr<4, 2>)
                                            : (tag_sweep_r() == 4 ? k_tag_sweep_csr<2, 4> : k_tag_sweep_csr<2, 2>);
-                    hipLaunchKernelGGL(kern, dim3((g->n_nodes + BLOCK * npt - 1) / (BLOCK * npt)), dim3(BLOCK), 0,
+                    int per_block = BLOCK * npt;
+                    if (coop) {
+                        kern = coop == 1 ? k_tag_sweep_coop<1> : coop == 4 ? k_tag_sweep_coop<4> : k_tag_sweep_coop<2>;
+                        per_block = BLOCK * coop;
+                    }
+                    hipLaunchKernelGGL(kern, dim3((g->n_nodes + per_block - 1) / per_block), dim3(BLOCK), 0,
                                        st, *g, lists, tin, tout, b0, b1, q == 0 ? 1 : 0, ovf,
                                        ring + (q % TAG_RING) * TAG_CTR, TAG_SHARDS, ctl);
                     if (hipGetLastError() != hipSuccess) return hip_fail("gtf_tag_propagate: sweep launch");

@@ -128,21 +128,26 @@ _CSR_MODES = {
     "packed_n1": {"GTF_TAG_NPT": "1"},
     "packed_n2": {"GTF_TAG_NPT": "2", "GTF_TAG_PREP_NPT": "2", "GTF_TAG_R": "2"},
     "packed_n2_r4": {"GTF_TAG_NPT": "2", "GTF_TAG_PREP_NPT": "0", "GTF_TAG_R": "4"},
-    "packed_n4": {"GTF_TAG_NPT": "4", "GTF_TAG_PREP_NPT": "4", "GTF_TAG_R": "4"},
+    "packed_n4": {"GTF_TAG_NPT": "4", "GTF_TAG_PREP_NPT": "4", "GTF_TAG_R": "4", "GTF_TAG_COOP": "0"},
+    "packed_n2_lanes": {"GTF_TAG_NPT": "2", "GTF_TAG_PREP_NPT": "2", "GTF_TAG_COOP": "0"},
+    "coop1": {"GTF_TAG_NPT": "2", "GTF_TAG_PREP_NPT": "1", "GTF_TAG_COOP": "1"},
+    "coop4": {"GTF_TAG_NPT": "2", "GTF_TAG_PREP_NPT": "1", "GTF_TAG_COOP": "4"},
     "packed_prep1": {"GTF_TAG_PREP_NPT": "1"},
     "unpacked_n2": {"GTF_TAG_NPT": "2", "GTF_TAG_PREP_NPT": "2", "GTF_TAG_PACK": "0"},
     "counts_thread_prep": {"GTF_TAG_KWORD": "0", "GTF_TAG_NPT": "1", "GTF_TAG_PREP_NPT": "1"},
     "counts_group_prep": {"GTF_TAG_KWORD": "0", "GTF_TAG_NPT": "2", "GTF_TAG_PREP_NPT": "0"},
     "mask": {"GTF_TAG_CSR": "0"},
 }
-_TAG_ENV = ("GTF_TAG_CSR", "GTF_TAG_KWORD", "GTF_TAG_NPT", "GTF_TAG_PREP_NPT", "GTF_TAG_R", "GTF_TAG_PACK")
+_TAG_ENV = ("GTF_TAG_CSR", "GTF_TAG_KWORD", "GTF_TAG_NPT", "GTF_TAG_PREP_NPT", "GTF_TAG_R", "GTF_TAG_PACK", "GTF_TAG_COOP")
 
 
 def _csr_env(monkeypatch, mode):
     """gtf_tag_propagate's sweep form: compact kept lists with one packed word per node (1, 2 or
     4 nodes per thread in the prepare and the sweeps, 2 or 4 kept indices per node in a sweep's
     second round; the thread prepare's lists back to back per run of 256 nodes, or at the front
-    of each node's out-range with GTF_TAG_PACK=0) or a count and an offset per node, built by the
+    of each node's out-range with GTF_TAG_PACK=0; on packed lists the 2-node sweep is the
+    wave-cooperative one, 1 / 2 / 4 groups of 64 nodes per wave, or GTF_TAG_COOP=0 the per-lane
+    one) or a count and an offset per node, built by the
     one-node-per-thread or the lane-group prepare, or the keep-mask sweeps (GTF_TAG_CSR=0)"""
     for k in _TAG_ENV:
         monkeypatch.setenv(k, _CSR_MODES[mode].get(k, ""))
@@ -275,7 +280,8 @@ def test_tag_propagate_tags_beyond_int32(shape, monkeypatch):
     nb = L.gtf_tag_workspace_bytes(g.n_nodes, g.n_edges)
     res = {}
     for csr, mode in (("1", "default"), ("n2", "packed_n2"), ("n4", "packed_n4"), ("p1", "packed_prep1"),
-                      ("u2", "unpacked_n2"), ("ct", "counts_thread_prep"), ("0", "mask")):
+                      ("u2", "unpacked_n2"), ("l2", "packed_n2_lanes"), ("c1", "coop1"), ("c4", "coop4"),
+                      ("ct", "counts_thread_prep"), ("0", "mask")):
         _csr_env(monkeypatch, mode)
         tags = torch.from_numpy(t0).to(d.device)
         ws = torch.full((nb,), 0xFF, dtype=torch.uint8, device=d.device)
@@ -287,7 +293,7 @@ def test_tag_propagate_tags_beyond_int32(shape, monkeypatch):
                                       ctypes.c_void_p(ws.data_ptr()), nb, d.stream))
         torch.cuda.synchronize()
         res[csr] = (list(flips[:sweeps.value]), tags.cpu().numpy())
-    for m in ("1", "n2", "n4", "p1", "u2", "ct"):   # (every compact-list form, its int64 fallback included)
+    for m in ("1", "n2", "n4", "p1", "u2", "l2", "c1", "c4", "ct"):   # (every compact-list form, its int64 fallback included)
         assert res[m][0] == res["0"][0]
         assert np.array_equal(res[m][1], res["0"][1])
     if shape != "one_wide":   # (a shift changes no comparison)
@@ -331,21 +337,23 @@ def _star_graph(k, r0):
 
 @pytest.mark.parametrize("csr", list(_CSR_MODES))
 @pytest.mark.parametrize("schedule", [True, False])
-def test_tag_propagate_saturated_kept_count(schedule, csr, monkeypatch):
+@pytest.mark.parametrize("kept", [700, 300])
+def test_tag_propagate_saturated_kept_count(schedule, csr, kept, monkeypatch):
     """a node with 1,200 out-edges, 700 of them kept: past the packed word's 511 (the count then
-    read from its own word), on the lane-group and thread-per-node prepare kernels; the tags and
-    flips equal the oracle's"""
+    read from its own word), or 300: more than the cooperative sweep stages for one 64-node group
+    (its per-lane loop); on the lane-group and thread-per-node prepare kernels; the tags and flips
+    equal the oracle's"""
     _csr_env(monkeypatch, csr)
     import torch
     from gtf.device import DeviceGraph
-    g = _star_graph(1200, 700.5)
+    g = _star_graph(1200, kept + 0.5)
     d = DeviceGraph(g, schedule=schedule)
     tags = torch.from_numpy(np.ascontiguousarray(g.node["tag"], dtype=np.int64)).to(d.device)
     radius = torch.from_numpy(np.ascontiguousarray(g.node["xyzr"][:, 3])).to(d.device)
     flips = d.tag_propagation_dev(tags, radius, threshold=0.0, max_sweeps=5000)
-    if "star" not in _ORACLE_CACHE:   # (920 sweeps of the Python oracle: once per module)
-        _ORACLE_CACHE["star"] = O.tag_propagation(g, 0.0)
-    want_tags, want_flips = _ORACLE_CACHE["star"]
+    if kept not in _ORACLE_CACHE:   # (~1,000 sweeps of the Python oracle: once per module and size)
+        _ORACLE_CACHE[kept] = O.tag_propagation(g, 0.0)
+    want_tags, want_flips = _ORACLE_CACHE[kept]
     assert flips == list(want_flips) and len(flips) > 2
     assert np.array_equal(tags.cpu().numpy(), want_tags)
 

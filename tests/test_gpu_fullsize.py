@@ -156,3 +156,36 @@ def test_slot_tables_do_not_change_the_pass(c4, variant, monkeypatch):
     got = {k: v for k, v in list(h.node.items()) + list(h.slot.items()) if k in _state_keys(c4)}
     assert e.errors() == flags
     _same(got, ref, variant)
+
+
+@pytest.mark.parametrize("order", ["ascending", "descending"])
+def test_c3_tag_stage_forms_agree(order, monkeypatch):
+    """gtf_tag_propagate on configs[2] (C3: 64 C2-like events fused, 2.0 M nodes / 5.9 M edges,
+    after one pass) -- the size where the stage's defaults are the packed kept lists and the
+    wave-cooperative sweep (two 64-node groups per wave) -- against the per-lane sweep on the
+    same packed lists (GTF_TAG_COOP=0), the lists at the out-range fronts (GTF_TAG_PACK=0) and
+    the keep-mask sweeps of gtf_tag_sweep (GTF_TAG_CSR=0): the same flips, sweep count and tags
+    word for word, from ascending (one sweep) and descending (several) initial tags"""
+    import torch
+    from gtf.device import DeviceGraph
+    g = synth.workload("c3", seed=0)
+    d = DeviceGraph(g, layout="tiled")
+    d.full_pass(Params())
+    rad = torch.from_numpy(np.ascontiguousarray(d._to_dev_nodes(g.node["xyzr"][:, 3]))).to(d.device)
+    t = np.arange(g.n_nodes, dtype=np.int64)
+    if order == "descending":
+        t = t[::-1].copy()
+    t0 = torch.from_numpy(np.ascontiguousarray(d._to_dev_nodes(t))).to(d.device)
+    res = {}
+    for name, env in (("default", {}), ("lanes", {"GTF_TAG_COOP": "0"}), ("unpacked", {"GTF_TAG_PACK": "0"}),
+                      ("mask", {"GTF_TAG_CSR": "0"})):
+        for k in ("GTF_TAG_CSR", "GTF_TAG_PACK", "GTF_TAG_COOP"):
+            monkeypatch.setenv(k, env.get(k, ""))
+        ta = t0.clone()
+        flips = d.tag_propagation_dev(ta, rad)
+        torch.cuda.synchronize()
+        res[name] = (list(flips), ta.cpu())
+    assert len(res["default"][0]) >= (2 if order == "descending" else 1)
+    for name in ("lanes", "unpacked", "mask"):
+        assert res[name][0] == res["default"][0], name
+        assert torch.equal(res[name][1], res["default"][1]), name

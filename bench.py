@@ -825,9 +825,9 @@ def bench_sharded(workload, rank, world, dev, steps, warmup, params, backend="nc
 # the fused node kernel: priors, side norm, reweights, update and KL clustering of every
 # receiver in one launch (gtf_pass.hip run_pass)
 NODE_KERNEL = "k_node_multi<update+cluster> (KL-distance kernel)"
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r06", "final4", "c4", "pmc_c4.json")
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r06", "final5", "c4", "pmc_c4.json")
 # per-launch SQ instruction counters of the pass kernels (tools/gpu_sqmix.sh, same event)
-SQ_SUMMARY = os.path.join(ROOT, "profiles", "r06", "final4", "sqmix", "sqmix.json")
+SQ_SUMMARY = os.path.join(ROOT, "profiles", "r06", "final5", "sqmix", "sqmix.json")
 SQ_NAMES = {"k_sender+k_extrapolate": ("k_sender_sched", "k_extrapolate"),
             NODE_KERNEL: ("k_node_multi<11, 1, 3, 4, 3, 4, 5, 6, 2, 3, 4, 12, 10, 5, 8, 3>",
                           "k_node_multi<11, 1, 3, 4, 3, 4, 5, 6, 2, 3, 4, 10, 5, 8, 3>")}

@@ -270,9 +270,52 @@ __global__ void __launch_bounds__(BLOCK) k_tag_prepare_csr(gtf_graph g, const do
         }
         return nk;
     };
-    int base[NPT];
+#ifndef GTF_TAG_PACK_MASK
+#define GTF_TAG_PACK_MASK 1   // 1: the count pass keeps the kept bits of out-edges R .. R + 31, so the write pass
+                              // reloads only their neighbour indices (no second radius gather)
+#endif
+    // (pack) the count pass of the out-edges past the first R: the kept bits of the next 32
+    auto rest_count = [&](int j, uint32_t& km) {
+        int nk = 0;
+        km = 0u;
+        for (int i = o0[j] + R; i < o1[j]; i += R) {
+            int x[R];
+            double rx[R];
 #pragma unroll
-    for (int j = 0; j < NPT; j++) base[j] = o0[j];
+            for (int r = 0; r < R; r++) x[r] = i + r < o1[j] ? dst(i + r) : 0;
+#pragma unroll
+            for (int r = 0; r < R; r++) rx[r] = i + r < o1[j] ? radius[x[r]] : 0.0;
+#pragma unroll
+            for (int r = 0; r < R; r++)
+                if (i + r < o1[j] && !(rx[r] > ru[j])) {
+                    const int off = i + r - o0[j] - R;
+                    if (off < 32) km |= 1u << off;
+                    nk++;
+                }
+        }
+        return nk;
+    };
+    // ... and its write pass: the bits' neighbours reloaded, anything past them recomputed
+    auto rest_write = [&](int j, uint32_t km, int at) {
+        int nk = 0;
+        while (km) {
+            const int off = __builtin_ctz(km);
+            km &= km - 1u;
+            csr.kidx[at + nk++] = dst(o0[j] + R + off);
+        }
+        for (int i = o0[j] + R + 32; i < o1[j]; i++) {
+            const int x = dst(i);
+            if (!(radius[x] > ru[j])) csr.kidx[at + nk++] = x;
+        }
+        return nk;
+    };
+    int base[NPT];
+    uint32_t kmask[NPT];
+#pragma unroll
+    for (int j = 0; j < NPT; j++) {
+        base[j] = o0[j];
+        kmask[j] = 0u;
+    }
     if (pack) {   // (uniform) the counts first, then every node's place in its run
         int nk[NPT];
 #pragma unroll
@@ -280,7 +323,7 @@ __global__ void __launch_bounds__(BLOCK) k_tag_prepare_csr(gtf_graph g, const do
             nk[j] = 0;
 #pragma unroll
             for (int r = 0; r < R; r++) nk[j] += o0[j] + r < o1[j] && !(rw[j][r] > ru[j]);
-            if (o1[j] - o0[j] > R) nk[j] += rest(j, false, 0);
+            if (o1[j] - o0[j] > R) nk[j] += GTF_TAG_PACK_MASK ? rest_count(j, kmask[j]) : rest(j, false, 0);
         }
 #pragma unroll
         for (int j = 0; j < NPT; j++) {
@@ -297,7 +340,8 @@ __global__ void __launch_bounds__(BLOCK) k_tag_prepare_csr(gtf_graph g, const do
 #pragma unroll
         for (int r = 0; r < R; r++)
             if (o0[j] + r < o1[j] && !(rw[j][r] > ru[j])) csr.kidx[base[j] + nk++] = w[j][r];
-        if (o1[j] - o0[j] > R) nk += rest(j, true, base[j] + nk);
+        if (o1[j] - o0[j] > R)
+            nk += pack && GTF_TAG_PACK_MASK ? rest_write(j, kmask[j], base[j] + nk) : rest(j, true, base[j] + nk);
         csr_node(csr, u, base[j], nk);
     }
 }

@@ -20,7 +20,7 @@ from gtf.device import DeviceGraph  # noqa: E402
 from gtf.params import Params  # noqa: E402
 
 KEYS = ("GTF_TAG_CSR", "GTF_TAG_KWORD", "GTF_TAG_NPT", "GTF_TAG_PREP_NPT", "GTF_TAG_R", "GTF_TAG_BATCH0",
-        "GTF_TAG_PACK", "GTF_TAG_COOP", "GTF_TAG_AHEAD", "GTF_TAG_POLL", "GTF_TAG_PREP_COOP")
+        "GTF_TAG_PACK", "GTF_TAG_COOP", "GTF_TAG_AHEAD", "GTF_TAG_POLL", "GTF_TAG_PREP_COOP", "GTF_TAG_SPEC")
 
 
 def parse(arg):
